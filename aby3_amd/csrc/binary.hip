@@ -1,0 +1,179 @@
+// Bit-sliced binary engine (Sh3BinaryEvaluator) on gfx950.
+//
+// Memory is wire-major: mem[share][wire][word], one u64 word = 64 rows, the
+// row count padded to a multiple of 2048 (Sh3BinaryEvaluator.cpp:84). A gate
+// batch is a set of mutually independent gates of one communication level;
+// each workgroup handles one gate (wave-uniform type and wire ids, read
+// through the scalar cache) over 512 consecutive words, 2 words (16 B) per
+// lane, so every load and store is a fully coalesced 1 KiB wave access.
+// The AND-gate masks z are produced up front by aby3g_share_draws
+// (ABY3G_DRAW_BIN: z[k][w] = getShares() of Sh3BinaryEvaluator.cpp:1406-1434
+// for the k-th AND-type gate), so the gate kernel is pure streaming.
+#include "common.h"
+
+namespace aby3g {
+
+namespace {
+
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
+constexpr u32 kGateBlock = 256;
+
+__global__ void __launch_bounds__(kGateBlock) k_bin_gates(const aby3g_gate* __restrict__ gates, u64* __restrict__ mem,
+                                                          u64 wires, u64 words, const u64* __restrict__ z,
+                                                          u64* __restrict__ sendbuf) {
+    const aby3g_gate g = gates[blockIdx.y];
+    const u64 w = ((u64)blockIdx.x * kGateBlock + threadIdx.x) * 2;
+    if (w >= words) return;
+    u64* s0 = mem;
+    u64* s1 = mem + wires * words;
+    const u64x2 x0 = *reinterpret_cast<const u64x2*>(s0 + g.in0 * words + w);
+    const u64x2 x1 = *reinterpret_cast<const u64x2*>(s1 + g.in0 * words + w);
+    u64x2 o0, o1;
+    switch (g.type) {
+        case ABY3G_GATE_COPY:
+            o0 = x0;
+            o1 = x1;
+            break;
+        case ABY3G_GATE_INV:
+            o0 = ~x0;
+            o1 = ~x1;
+            break;
+        default: {
+            const u64x2 y0 = *reinterpret_cast<const u64x2*>(s0 + g.in1 * words + w);
+            const u64x2 y1 = *reinterpret_cast<const u64x2*>(s1 + g.in1 * words + w);
+            if (g.type == ABY3G_GATE_XOR) {
+                o0 = x0 ^ y0;
+                o1 = x1 ^ y1;
+                break;
+            }
+            if (g.type == ABY3G_GATE_NXOR) {
+                o0 = ~(x0 ^ y0);
+                o1 = ~(x1 ^ y1);
+                break;
+            }
+            // AND-type (Sh3BinaryEvaluator.cpp:700-1065): share 0 only.
+            u64x2 r;
+            if (g.type == ABY3G_GATE_AND)
+                r = (x0 & y0) ^ (x0 & y1) ^ (x1 & y0);
+            else if (g.type == ABY3G_GATE_OR)
+                r = (x0 & y0) ^ (x0 & y1) ^ (x1 & y0) ^ x0 ^ y0;
+            else if (g.type == ABY3G_GATE_NOR)
+                r = (~x0 & ~y0) ^ (~x0 & ~y1) ^ (~x1 & ~y0);
+            else /* NA_AND */
+                r = (~x0 & y0) ^ (~x0 & y1) ^ (~x1 & y0);
+            r ^= *reinterpret_cast<const u64x2*>(z + (u64)g.z_row * words + w);
+            *reinterpret_cast<u64x2*>(s0 + g.out * words + w) = r;
+            *reinterpret_cast<u64x2*>(sendbuf + (u64)g.send_row * words + w) = r;
+            return;
+        }
+    }
+    *reinterpret_cast<u64x2*>(s0 + g.out * words + w) = o0;
+    *reinterpret_cast<u64x2*>(s1 + g.out * words + w) = o1;
+}
+
+__global__ void __launch_bounds__(kGateBlock) k_bin_unpack(const u64* __restrict__ recv, const u32* __restrict__ outw,
+                                                           u64* __restrict__ mem, u64 wires, u64 words) {
+    const u32 j = blockIdx.y;
+    const u64 w = ((u64)blockIdx.x * kGateBlock + threadIdx.x) * 2;
+    if (w >= words) return;
+    const u32 wire = outw[j];
+    *reinterpret_cast<u64x2*>(mem + (wires + wire) * words + w) =
+        *reinterpret_cast<const u64x2*>(recv + (u64)j * words + w);
+}
+
+// One wave per (64-row word w, 64-bit column c): lane r holds row 64w + r;
+// the ballot of bit b over the wave is word w of wire b (LSB = row 64w).
+__global__ void __launch_bounds__(256) k_bits_to_wires(const i64* __restrict__ in, u64 rows, u64 cols64, u32 nbits,
+                                                       u64* __restrict__ wrows, u64 words) {
+    const u32 lane = threadIdx.x & 63;
+    const u64 waveId = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const u64 nw = words * cols64;
+    if (waveId >= nw) return;
+    const u64 w = waveId % words, c = waveId / words;
+    const u64 r = w * 64 + lane;
+    const u64 v = r < rows ? (u64)in[r * cols64 + c] : 0;
+    u64 mine = 0;
+#pragma unroll 8
+    for (u32 b = 0; b < 64; ++b) {
+        const u64 m = __ballot((v >> b) & 1);
+        if (lane == b) mine = m;
+    }
+    const u64 bit = c * 64 + lane;
+    if (bit < nbits) wrows[bit * words + w] = mine;
+}
+
+__global__ void __launch_bounds__(256) k_wires_to_bits(const u64* __restrict__ mem, const u32* __restrict__ wires,
+                                                       u32 nbits, u64 words, i64* __restrict__ out, u64 rows) {
+    const u32 lane = threadIdx.x & 63;
+    const u64 waveId = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const u64 cols = (nbits + 63) / 64;
+    const u64 nw = ((rows + 63) / 64) * cols;
+    if (waveId >= nw) return;
+    const u64 rw = (rows + 63) / 64;
+    const u64 w = waveId % rw, c = waveId / rw;
+    const u64 bit = c * 64 + lane;
+    const u64 v = bit < nbits ? mem[(u64)wires[bit] * words + w] : 0;
+    u64 mine = 0;
+#pragma unroll 8
+    for (u32 r = 0; r < 64; ++r) {
+        const u64 m = __ballot((v >> r) & 1);
+        if (lane == r) mine = m;
+    }
+    const u64 row = w * 64 + lane;
+    if (row < rows) out[row * cols + c] = (i64)mine;
+}
+
+}  // namespace
+
+}  // namespace aby3g
+
+using namespace aby3g;
+
+extern "C" {
+
+int aby3g_bin_gates(const aby3g_gate* gates, uint32_t ngates, uint64_t* mem, uint64_t wires, uint64_t words,
+                    const uint64_t* z, uint64_t* sendbuf, aby3g_stream stream) {
+    return guarded([&] {
+        ABY3G_REQUIRE(words % 32 == 0, "words must be padded to a multiple of 32 (2048 rows)");
+        if (!ngates || !words) return;
+        dim3 grid((u32)((words / 2 + kGateBlock - 1) / kGateBlock), ngates);
+        launch(PROBE_BINARY, k_bin_gates, grid, dim3(kGateBlock), 0, S(stream), gates, mem, wires, words, z, sendbuf);
+    });
+}
+
+int aby3g_bin_unpack(const uint64_t* recvbuf, const uint32_t* out_wires, uint32_t n, uint64_t* mem, uint64_t wires,
+                     uint64_t words, aby3g_stream stream) {
+    return guarded([&] {
+        ABY3G_REQUIRE(words % 32 == 0, "words must be padded to a multiple of 32 (2048 rows)");
+        if (!n || !words) return;
+        dim3 grid((u32)((words / 2 + kGateBlock - 1) / kGateBlock), n);
+        launch(PROBE_BINARY, k_bin_unpack, grid, dim3(kGateBlock), 0, S(stream), recvbuf, out_wires, mem, wires,
+               words);
+    });
+}
+
+int aby3g_bits_to_wires(const int64_t* in, uint64_t rows, uint64_t cols64, uint32_t nbits, uint64_t* wire_rows,
+                        uint64_t words, aby3g_stream stream) {
+    return guarded([&] {
+        ABY3G_REQUIRE(nbits <= cols64 * 64, "nbits exceeds input columns");
+        ABY3G_REQUIRE(words * 64 >= rows, "words too small for rows");
+        if (!nbits || !words) return;
+        u64 waves = words * cols64;
+        launch(PROBE_OTHER, k_bits_to_wires, dim3((u32)((waves * 64 + 255) / 256)), dim3(256), 0, S(stream), in, rows,
+               cols64, nbits, wire_rows, words);
+    });
+}
+
+int aby3g_wires_to_bits(const uint64_t* mem_share, const uint32_t* wires, uint32_t nbits, uint64_t words, int64_t* out,
+                        uint64_t rows, aby3g_stream stream) {
+    return guarded([&] {
+        ABY3G_REQUIRE(words * 64 >= rows, "words too small for rows");
+        if (!nbits || !rows) return;
+        u64 waves = ((rows + 63) / 64) * ((nbits + 63) / 64);
+        launch(PROBE_OTHER, k_wires_to_bits, dim3((u32)((waves * 64 + 255) / 256)), dim3(256), 0, S(stream),
+               mem_share, wires, nbits, words, out, rows);
+    });
+}
+
+}  // extern "C"

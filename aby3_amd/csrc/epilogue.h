@@ -1,0 +1,140 @@
+// Element-wise epilogues of asyncMul that need AES-CTR randomness: the
+// zero-share add (Sh3Evaluator.cpp:101-105) and the truncation pair
+// (Sh3Evaluator.cpp:503-566, 670-673). They are templated on the source of
+// the local share product so that the Hadamard mode computes it in place and
+// the GEMM mode reduces its split-K partial slabs in the same pass.
+#pragma once
+#include "common.h"
+
+namespace aby3g {
+
+constexpr u32 kEpiBlock = 256;
+constexpr u32 kEpiWin = 512;  // elements per window (2 per thread)
+constexpr size_t kAesLds = kAesLdsWords * sizeof(u32);
+
+// win[0 .. 2*nc) <- words of PRNG stream k covering stream words
+// [wbase, wbase + E); the word of element e is win[(wbase & 1) + e].
+__device__ __forceinline__ void stream_window(const u32* T, const AesKey& k, u64 wbase, u32 E, u64* win) {
+    const u64 c0 = wbase >> 1;
+    const u32 nc = (u32)(((wbase + E - 1) >> 1) - c0 + 1);
+    const u32 lane32 = threadIdx.x & 31;
+    for (u32 j = threadIdx.x; j < nc; j += blockDim.x) {
+        u64 lo, hi;
+        aes_ctr_block(T, lane32, k, c0 + j, lo, hi);
+        win[2 * j] = lo;
+        win[2 * j + 1] = hi;
+    }
+}
+
+// No product: plain getTruncationTuple.
+struct SrcNone {
+    __device__ u64 operator()(u64) const { return 0; }
+};
+// GEMM: sum of split-K partial slabs [nsplit][n].
+struct SrcSlabs {
+    const i64* P;
+    u32 nsplit;
+    u64 stride;
+    __device__ u64 operator()(u64 i) const {
+        u64 v = 0;
+        for (u32 s = 0; s < nsplit; ++s) v += (u64)P[s * stride + i];
+        return v;
+    }
+};
+// Hadamard: A0 B0 + A0 B1 + A1 B0 = A0 (B0 + B1) + A1 B0, mod 2^64.
+struct SrcHadamard {
+    const i64 *A0, *A1, *B0, *B1;
+    __device__ u64 operator()(u64 i) const {
+        u64 a0 = (u64)A0[i], a1 = (u64)A1[i], b0 = (u64)B0[i], b1 = (u64)B1[i];
+        return a0 * (b0 + b1) + a1 * b0;
+    }
+};
+
+// C0[i] = src(i): the share product without a zero-share (used when the
+// caller adds randomness itself).
+template <class Src>
+__global__ void __launch_bounds__(kEpiBlock) k_finish_plain(Src src, u64 n, i64* __restrict__ C0) {
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x)
+        C0[i] = (i64)src(i);
+}
+
+// C0[i] = src(i) + getShare(draw_base + i)   (Sh3Evaluator.cpp:101-105)
+template <class Src>
+__global__ void __launch_bounds__(kEpiBlock) k_finish_zero_share(const u32* __restrict__ T0g, Src src, u64 n,
+                                                                 AesKey kp, AesKey kn, u64 base,
+                                                                 i64* __restrict__ C0) {
+    extern __shared__ u32 lds[];
+    aes_fill_lds(lds, T0g);
+    const u32 lane32 = threadIdx.x & 31;
+    const u64 c_first = base >> 1, c_last = (base + n - 1) >> 1;
+    for (u64 c = c_first + (u64)blockIdx.x * blockDim.x + threadIdx.x; c <= c_last;
+         c += (u64)gridDim.x * blockDim.x) {
+        u64 p[2], q[2];
+        aes_ctr_block(lds, lane32, kp, c, p[0], p[1]);
+        aes_ctr_block(lds, lane32, kn, c, q[0], q[1]);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            u64 j = 2 * c + h;
+            if (j < base || j - base >= n) continue;
+            u64 i = j - base;
+            C0[i] = (i64)(src(i) + p[h] - q[h]);
+        }
+    }
+}
+
+// R = t0 >> 2, RT = (t0 >> (d+2), t1 >> (d+2)); z = src(i) - R when z != null.
+template <class Src>
+__global__ void __launch_bounds__(kEpiBlock) k_finish_trunc(const u32* __restrict__ T0g, Src src, AesKey kn, u64 nw0,
+                                                            AesKey kp, u64 pw0, u64 n, u32 d, i64* __restrict__ R,
+                                                            i64* __restrict__ RT0, i64* __restrict__ RT1,
+                                                            i64* __restrict__ z) {
+    extern __shared__ u32 lds[];
+    aes_fill_lds(lds, T0g);
+    __shared__ u64 wn[kEpiWin + 2], wp[kEpiWin + 2];
+    for (u64 e0 = (u64)blockIdx.x * kEpiWin; e0 < n; e0 += (u64)gridDim.x * kEpiWin) {
+        const u32 E = (u32)min((u64)kEpiWin, n - e0);
+        __syncthreads();
+        stream_window(lds, kn, nw0 + e0, E, wn);
+        stream_window(lds, kp, pw0 + e0, E, wp);
+        __syncthreads();
+        const u32 on = (u32)((nw0 + e0) & 1), op = (u32)((pw0 + e0) & 1);
+        for (u32 e = threadIdx.x; e < E; e += blockDim.x) {
+            const i64 t0 = (i64)wn[on + e], t1 = (i64)wp[op + e];
+            const i64 r = t0 >> 2;
+            const u64 i = e0 + e;
+            if (R) R[i] = r;
+            if (z) z[i] = (i64)(src(i) - (u64)r);
+            RT0[i] = t0 >> (d + 2);
+            RT1[i] = t1 >> (d + 2);
+        }
+    }
+}
+
+template <class Src>
+void launch_finish_zero_share(Src src, u64 n, const aby3g_zero_share& zs, i64* C0, hipStream_t s) {
+    if (!n) return;
+    AesKey kp = expand_key(zs.k_prev), kn = expand_key(zs.k_next);
+    u64 counters = ((zs.draw_base + n - 1) >> 1) - (zs.draw_base >> 1) + 1;
+    launch(PROBE_EPILOGUE, k_finish_zero_share<Src>, dim3(aes_grid(counters, kEpiBlock)), dim3(kEpiBlock), kAesLds, s,
+           aes_table(), src, n, kp, kn, zs.draw_base, C0);
+}
+
+template <class Src>
+void launch_finish_plain(Src src, u64 n, i64* C0, hipStream_t s) {
+    if (!n) return;
+    launch(PROBE_EPILOGUE, k_finish_plain<Src>, dim3(aes_grid(n, kEpiBlock)), dim3(kEpiBlock), 0, s, src, n, C0);
+}
+
+template <class Src>
+void launch_finish_trunc(Src src, const aby3g_trunc_streams& ts, u64 n, unsigned d, i64* R, i64* RT0, i64* RT1,
+                         i64* z, hipStream_t s) {
+    ABY3G_REQUIRE(ts.next_off % 8 == 0 && ts.prev_off % 8 == 0, "stream offsets must be multiples of 8");
+    ABY3G_REQUIRE(d < 62, "shift too large");
+    if (!n) return;
+    AesKey kn = expand_key(ts.next_seed), kp = expand_key(ts.prev_seed);
+    u32 grid = aes_grid((n + kEpiWin - 1) / kEpiWin, 1);
+    launch(PROBE_EPILOGUE, k_finish_trunc<Src>, dim3(grid), dim3(kEpiBlock), kAesLds, s, aes_table(), src, kn,
+           ts.next_off / 8, kp, ts.prev_off / 8, n, (u32)d, R, RT0, RT1, z);
+}
+
+}  // namespace aby3g

@@ -1,0 +1,110 @@
+// Element-wise helpers of the protocols around the hot kernels: share sums
+// and differences, fixed-point constants, the trunc finalize, bitwise ops on
+// binary shares and the gather/scatter of the merge network.
+#include "common.h"
+
+namespace aby3g {
+
+namespace {
+
+constexpr u32 kB = 256;
+
+inline u32 ew_grid(u64 n) {
+    u64 g = (n + kB - 1) / kB;
+    if (g > 8192) g = 8192;
+    return (u32)(g ? g : 1);
+}
+
+#define GRID_STRIDE(i, n) for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += (u64)gridDim.x * blockDim.x)
+
+__global__ void k_lincomb(u64 n, u64 ca, const i64* __restrict__ a, u64 cb, const i64* __restrict__ b, u64 c,
+                          i64* __restrict__ out) {
+    GRID_STRIDE(i, n) {
+        u64 v = ca * (u64)a[i] + c;
+        if (b) v += cb * (u64)b[i];
+        out[i] = (i64)v;
+    }
+}
+
+// Sh3Evaluator.cpp:712-718: C[party] += (za + zb + zo) >> d
+__global__ void k_trunc_finalize(u64 n, const i64* __restrict__ za, const i64* __restrict__ zb,
+                                 const i64* __restrict__ zo, u32 d, i64* __restrict__ c) {
+    GRID_STRIDE(i, n) {
+        const i64 s = (i64)((u64)za[i] + (u64)zb[i] + (u64)zo[i]);
+        c[i] = (i64)((u64)c[i] + (u64)(s >> d));
+    }
+}
+
+__global__ void k_bitop(int op, u64 n, const u64* __restrict__ a, const u64* __restrict__ b, u64* __restrict__ out) {
+    GRID_STRIDE(i, n) {
+        u64 v;
+        switch (op) {
+            case 0: v = a[i] ^ b[i]; break;
+            case 1: v = a[i] & b[i]; break;
+            case 2: v = ~a[i]; break;
+            case 3: v = 0 - (a[i] & 1); break;
+            default: v = a[i]; break;
+        }
+        out[i] = v;
+    }
+}
+
+__global__ void k_gather(u64 n, const u32* __restrict__ idx, const u64* __restrict__ src, u64* __restrict__ dst) {
+    GRID_STRIDE(i, n) dst[i] = src[idx[i]];
+}
+__global__ void k_scatter(u64 n, const u32* __restrict__ idx, const u64* __restrict__ src, u64* __restrict__ dst) {
+    GRID_STRIDE(i, n) dst[idx[i]] = src[i];
+}
+
+}  // namespace
+
+}  // namespace aby3g
+
+using namespace aby3g;
+
+extern "C" {
+
+int aby3g_i64_lincomb(uint64_t n, int64_t ca, const int64_t* a, int64_t cb, const int64_t* b, int64_t c, int64_t* out,
+                      aby3g_stream stream) {
+    return guarded([&] {
+        if (!n) return;
+        launch(PROBE_OTHER, k_lincomb, dim3(ew_grid(n)), dim3(kB), 0, S(stream), n, (u64)ca, a, (u64)cb, b, (u64)c,
+               out);
+    });
+}
+
+int aby3g_trunc_finalize(int party, const int64_t* z_a, const int64_t* z_b, const int64_t* z_own, unsigned d,
+                         int64_t* C, uint64_t n, aby3g_stream stream) {
+    return guarded([&] {
+        ABY3G_REQUIRE(party >= 0 && party <= 2, "party out of range");
+        ABY3G_REQUIRE(d < 64, "shift too large");
+        if (party == 2 || !n) return;  // only P0 and P1 finalize (Sh3Evaluator.cpp:692)
+        launch(PROBE_EPILOGUE, k_trunc_finalize, dim3(ew_grid(n)), dim3(kB), 0, S(stream), n, z_a, z_b, z_own, (u32)d,
+               C + (u64)party * n);
+    });
+}
+
+int aby3g_u64_bitop(int op, uint64_t n, const uint64_t* a, const uint64_t* b, uint64_t* out, aby3g_stream stream) {
+    return guarded([&] {
+        ABY3G_REQUIRE(op >= 0 && op <= 4, "bad op");
+        ABY3G_REQUIRE(op >= 2 || b != nullptr, "binary op needs b");
+        if (!n) return;
+        launch(PROBE_OTHER, k_bitop, dim3(ew_grid(n)), dim3(kB), 0, S(stream), op, n, a, b, out);
+    });
+}
+
+int aby3g_u64_gather(uint64_t n, const uint32_t* idx, const uint64_t* src, uint64_t* dst, aby3g_stream stream) {
+    return guarded([&] {
+        if (!n) return;
+        launch(PROBE_OTHER, k_gather, dim3(ew_grid(n)), dim3(kB), 0, S(stream), n, idx, src, dst);
+    });
+}
+
+int aby3g_u64_scatter(uint64_t n, const uint32_t* idx, const uint64_t* src, uint64_t* dst, aby3g_stream stream) {
+    return guarded([&] {
+        if (!n) return;
+        launch(PROBE_OTHER, k_scatter, dim3(ew_grid(n)), dim3(kB), 0, S(stream), n, idx, src, dst);
+    });
+}
+
+}  // extern "C"

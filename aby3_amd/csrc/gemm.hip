@@ -1,0 +1,323 @@
+// Share product of Sh3Evaluator::asyncMul on gfx950.
+//
+// GEMM mode (upstream semantics, Sh3Evaluator.cpp:96-99 / 662-665):
+//   C0 = A0 B0 + A0 B1 + A1 B0 = [A0 | A1] . [[B0 + B1]; [B0]]   (mod 2^64)
+// CDNA4 has no 64-bit integer MFMA, so every 64-bit operand is split into 8
+// balanced base-256 digits d_p in [-128, 127] (x = sum_p d_p 2^(8p) mod 2^64)
+// and the product mod 2^64 is
+//   sum_{s=0..7} 2^(8s) * sum_{p+q=s} A_p . B_q
+// i.e. 36 int8 digit-pair GEMMs accumulated into 8 exact i32 planes
+// (|plane| <= 8 * K' * 2^14 < 2^31 for K' <= 8192 per split) and recombined
+// in i64 in the epilogue. MFMA: v_mfma_i32_32x32x32_i8, one 32x32 output tile
+// and 8 planes (128 accumulator VGPRs) per wave, 2x2 waves per 64x64 tile.
+//
+// Digit layout in HBM (built once per call by k_digits_*): for every row of
+// A (resp. column of B) and every 32-wide slice of K', the 8 planes x 32
+// digits are one contiguous 256-byte record, so a K-stage of a 64-row tile is
+// 64 contiguous-per-row 256 B records. In LDS a record's 16-byte chunk g of
+// row r is stored at slot g ^ (r & 15): the 16 lanes of each ds_read_b128
+// lane group read 16 different rows at the same chunk and land on 16
+// different bank slots.
+#include "epilogue.h"
+
+namespace aby3g {
+
+namespace {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+constexpr u32 BM = 64, BN = 64, BK = 32;  // output tile, K' per stage
+constexpr u32 kThreads = 256;             // 4 waves, 2 x 2
+constexpr u32 kRec = 256;                 // bytes per (row, stage) record
+
+inline u64 roundup(u64 x, u64 m) { return (x + m - 1) / m * m; }
+
+struct GemmPlan {
+    u64 M, K, N;
+    u64 Mp, Np, Kp, Kc;  // padded sizes; Kc = K' = 2*Kp
+    u32 splits;          // split-K factor
+    u64 kPerSplit;       // K' per split (multiple of BK)
+    size_t aBytes, bBytes, pBytes, total;
+};
+
+GemmPlan plan_gemm(u64 M, u64 K, u64 N) {
+    GemmPlan p;
+    p.M = M;
+    p.K = K;
+    p.N = N;
+    p.Mp = roundup(M ? M : 1, BM);
+    p.Np = roundup(N ? N : 1, BN);
+    p.Kp = roundup(K ? K : 1, 16);
+    p.Kc = 2 * p.Kp;
+    const u64 stages = p.Kc / BK;
+    const u64 tiles = (p.Mp / BM) * (p.Np / BN);
+    // Enough workgroups for two per CU, at least 8 stages per split, and
+    // K' per split <= 8192 so every i32 plane stays exact.
+    u32 s = 1;
+    while (tiles * s < 512 && stages / (2 * s) >= 8) s *= 2;
+    while ((stages + s - 1) / s * BK > 8192) s *= 2;
+    p.splits = s;
+    p.kPerSplit = (stages + s - 1) / s * BK;
+    p.aBytes = p.Mp * p.Kc * 8;
+    p.bBytes = p.Np * p.Kc * 8;
+    p.pBytes = (u64)s * M * N * 8;
+    p.total = roundup(p.aBytes, 256) + roundup(p.bBytes, 256) + roundup(p.pBytes, 256);
+    return p;
+}
+
+// Balanced base-256 digits of 16 consecutive K' values, written as one
+// 16-byte chunk per plane.
+__device__ __forceinline__ void digits16(const u64 (&x)[16], v4i (&planes)[8]) {
+    u32 carry[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) carry[j] = 0;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+        u32 w[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            u32 b = (u32)((x[j] >> (8 * p)) & 0xff) + carry[j];  // 0..256
+            carry[j] = b >= 128 ? 1u : 0u;
+            u32 d = b & 0xff;  // two's complement byte of b - 256*carry
+            w[j >> 2] |= d << (8 * (j & 3));
+        }
+        planes[p] = v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
+    }
+}
+
+// Ad[m][K'/32][8][32] from A0 | A1 (row m, K' = [0, Kp) <- A0, [Kp, 2Kp) <- A1).
+__global__ void __launch_bounds__(256) k_digits_A(const i64* __restrict__ A0, const i64* __restrict__ A1, u64 M,
+                                                  u64 K, u64 Kp, u64 Mp, u8* __restrict__ Ad) {
+    const u64 chunks = 2 * Kp / 16;
+    const u64 total = Mp * chunks;
+    for (u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (u64)gridDim.x * blockDim.x) {
+        const u64 m = t / chunks, ch = t % chunks;
+        const u64 k0 = ch * 16;
+        u64 x[16];
+        const bool second = k0 >= Kp;
+        const i64* src = second ? A1 : A0;
+        const u64 kb = second ? k0 - Kp : k0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            u64 k = kb + j;
+            x[j] = (m < M && k < K) ? (u64)src[m * K + k] : 0;
+        }
+        v4i planes[8];
+        digits16(x, planes);
+        u8* rec = Ad + (m * (2 * Kp / BK) + k0 / BK) * kRec + (k0 % BK);
+#pragma unroll
+        for (int p = 0; p < 8; ++p) *reinterpret_cast<v4i*>(rec + p * 32) = planes[p];
+    }
+}
+
+// Bd[n][K'/32][8][32] from B' = [[B0 + B1]; [B0]] (column n).
+__global__ void __launch_bounds__(256) k_digits_B(const i64* __restrict__ B0, const i64* __restrict__ B1, u64 K,
+                                                  u64 N, u64 Kp, u64 Np, u8* __restrict__ Bd) {
+    const u64 chunks = 2 * Kp / 16;
+    for (u64 ch = blockIdx.y; ch < chunks; ch += gridDim.y) {
+        const u64 k0 = ch * 16;
+        const bool second = k0 >= Kp;
+        const u64 kb = second ? k0 - Kp : k0;
+        for (u64 n = (u64)blockIdx.x * blockDim.x + threadIdx.x; n < Np; n += (u64)gridDim.x * blockDim.x) {
+            u64 x[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                u64 k = kb + j;
+                u64 v = 0;
+                if (n < N && k < K) {
+                    v = (u64)B0[k * N + n];
+                    if (!second) v += (u64)B1[k * N + n];
+                }
+                x[j] = v;
+            }
+            v4i planes[8];
+            digits16(x, planes);
+            u8* rec = Bd + (n * (2 * Kp / BK) + k0 / BK) * kRec + (k0 % BK);
+#pragma unroll
+            for (int p = 0; p < 8; ++p) *reinterpret_cast<v4i*>(rec + p * 32) = planes[p];
+        }
+    }
+}
+
+// One 64x64 output tile over K' range [kBegin, kBegin + kLen) of split z.
+__global__ void __launch_bounds__(kThreads, 2) k_share_gemm(const u8* __restrict__ Ad, const u8* __restrict__ Bd,
+                                                            u64 M, u64 N, u64 stagesTotal, u64 stagesPerSplit,
+                                                            i64* __restrict__ P) {
+    __shared__ __attribute__((aligned(16))) u8 lds[2][2][BM * kRec];  // [buf][A|B][row][256 B]
+    const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const u64 m0 = (u64)blockIdx.x * BM, n0 = (u64)blockIdx.y * BN;
+    const u64 s0 = (u64)blockIdx.z * stagesPerSplit;
+    const u64 s1 = min(stagesTotal, s0 + stagesPerSplit);
+    if (s0 >= s1) {
+        // empty split: still define its slab
+        for (u32 i = tid; i < BM * BN; i += kThreads) {
+            u64 m = m0 + i / BN, n = n0 + i % BN;
+            if (m < M && n < N) P[(u64)blockIdx.z * M * N + m * N + n] = 0;
+        }
+        return;
+    }
+
+    // global -> LDS staging: 1024 chunks of 16 B per operand tile, 4 per thread
+    v4i ra[4], rb[4];
+    auto gload = [&](u64 st) {
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const u32 q = it * kThreads + tid;
+            const u32 row = q >> 4, slot = q & 15, g = slot ^ (row & 15);
+            ra[it] = *reinterpret_cast<const v4i*>(Ad + ((m0 + row) * stagesTotal + st) * kRec + g * 16);
+            rb[it] = *reinterpret_cast<const v4i*>(Bd + ((n0 + row) * stagesTotal + st) * kRec + g * 16);
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const u32 q = it * kThreads + tid;
+            *reinterpret_cast<v4i*>(&lds[buf][0][q * 16]) = ra[it];
+            *reinterpret_cast<v4i*>(&lds[buf][1][q * 16]) = rb[it];
+        }
+    };
+
+    v16i acc[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) acc[s] = v16i{0};
+
+    const u32 wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
+    const u32 fr = lane & 31, fh = lane >> 5;
+    const u32 rowA = wr + fr, rowB = wc + fr;
+
+    gload(s0);
+    lstore(0);
+    __syncthreads();
+    int buf = 0;
+    for (u64 st = s0; st < s1; ++st) {
+        const bool more = st + 1 < s1;
+        if (more) gload(st + 1);
+        v4i a[8], b[8];
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            const u32 g = 2 * p + fh;
+            a[p] = *reinterpret_cast<const v4i*>(&lds[buf][0][rowA * kRec + ((g ^ (rowA & 15)) * 16)]);
+            b[p] = *reinterpret_cast<const v4i*>(&lds[buf][1][rowB * kRec + ((g ^ (rowB & 15)) * 16)]);
+        }
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+#pragma unroll
+            for (int p = 0; p <= s; ++p) acc[s] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[p], b[s - p], acc[s], 0, 0, 0);
+        }
+        if (more) lstore(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+
+    // recombine planes in i64 and store the split's slab
+    i64* slab = P + (u64)blockIdx.z * M * N;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        u64 v = 0;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) v += (u64)(i64)acc[s][r] << (8 * s);
+        const u64 m = m0 + wr + (r & 3) + 8 * (r >> 2) + 4 * fh;
+        const u64 n = n0 + wc + fr;
+        if (m < M && n < N) slab[m * N + n] = (i64)v;
+    }
+}
+
+struct Workspace {
+    u8* Ad;
+    u8* Bd;
+    i64* P;
+};
+
+Workspace carve(const GemmPlan& p, void* ws) {
+    u8* base = (u8*)ws;
+    Workspace w;
+    w.Ad = base;
+    w.Bd = base + roundup(p.aBytes, 256);
+    w.P = (i64*)(base + roundup(p.aBytes, 256) + roundup(p.bBytes, 256));
+    return w;
+}
+
+// Runs the digit split and the MFMA GEMM; leaves `splits` partial slabs in w.P.
+void run_gemm(const GemmPlan& p, const i64* A, const i64* B, const Workspace& w, hipStream_t s) {
+    const i64* A0 = A;
+    const i64* A1 = A + p.M * p.K;
+    const i64* B0 = B;
+    const i64* B1 = B + p.K * p.N;
+    const u64 chunks = p.Kc / 16;
+    u64 ga = (p.Mp * chunks + 255) / 256;
+    launch(PROBE_DIGITS, k_digits_A, dim3((u32)min(ga, (u64)8192)), dim3(256), 0, s, A0, A1, p.M, p.K, p.Kp, p.Mp, w.Ad);
+    u32 gbx = (u32)((p.Np + 255) / 256);
+    u32 gby = (u32)min(chunks, (u64)1024);
+    launch(PROBE_DIGITS, k_digits_B, dim3(gbx, gby), dim3(256), 0, s, B0, B1, p.K, p.N, p.Kp, p.Np, w.Bd);
+    const u64 stages = p.Kc / BK;
+    launch(PROBE_GEMM, k_share_gemm, dim3((u32)(p.Mp / BM), (u32)(p.Np / BN), p.splits), dim3(kThreads), 0, s,
+           (const u8*)w.Ad, (const u8*)w.Bd, p.M, p.N, stages, p.kPerSplit / BK, w.P);
+}
+
+void check_ws(const GemmPlan& p, void* ws, size_t bytes) {
+    ABY3G_REQUIRE(ws != nullptr && bytes >= p.total, "workspace too small (see aby3g_mul_workspace_bytes)");
+}
+
+}  // namespace
+
+}  // namespace aby3g
+
+using namespace aby3g;
+
+extern "C" {
+
+size_t aby3g_mul_workspace_bytes(int mode, uint64_t M, uint64_t K, uint64_t N) {
+    if (mode != ABY3G_MUL_GEMM) return 0;
+    return plan_gemm(M, K, N).total;
+}
+
+int aby3g_mul_local(int mode, const int64_t* A, const int64_t* B, int64_t* C0, uint64_t M, uint64_t K, uint64_t N,
+                    const aby3g_zero_share* zs, void* workspace, size_t workspace_bytes, aby3g_stream stream) {
+    return guarded([&] {
+        ABY3G_REQUIRE(mode == ABY3G_MUL_HADAMARD || mode == ABY3G_MUL_GEMM, "bad mode");
+        const u64 n = M * N;
+        if (!n) return;
+        if (mode == ABY3G_MUL_HADAMARD) {
+            SrcHadamard src{A, A + n, B, B + n};
+            if (zs)
+                launch_finish_zero_share(src, n, *zs, C0, S(stream));
+            else
+                launch_finish_plain(src, n, C0, S(stream));
+            return;
+        }
+        GemmPlan p = plan_gemm(M, K, N);
+        check_ws(p, workspace, workspace_bytes);
+        Workspace w = carve(p, workspace);
+        run_gemm(p, A, B, w, S(stream));
+        SrcSlabs src{w.P, p.splits, n};
+        if (zs)
+            launch_finish_zero_share(src, n, *zs, C0, S(stream));
+        else
+            launch_finish_plain(src, n, C0, S(stream));
+    });
+}
+
+int aby3g_mul_trunc_local(int mode, const int64_t* A, const int64_t* B, uint64_t M, uint64_t K, uint64_t N,
+                          unsigned d, const aby3g_trunc_streams* ts, int64_t* z, int64_t* C, void* workspace,
+                          size_t workspace_bytes, aby3g_stream stream) {
+    return guarded([&] {
+        ABY3G_REQUIRE(mode == ABY3G_MUL_HADAMARD || mode == ABY3G_MUL_GEMM, "bad mode");
+        ABY3G_REQUIRE(ts != nullptr, "null trunc streams");
+        const u64 n = M * N;
+        if (!n) return;
+        if (mode == ABY3G_MUL_HADAMARD) {
+            SrcHadamard src{A, A + n, B, B + n};
+            launch_finish_trunc(src, *ts, n, d, nullptr, C, C + n, z, S(stream));
+            return;
+        }
+        GemmPlan p = plan_gemm(M, K, N);
+        check_ws(p, workspace, workspace_bytes);
+        Workspace w = carve(p, workspace);
+        run_gemm(p, A, B, w, S(stream));
+        SrcSlabs src{w.P, p.splits, n};
+        launch_finish_trunc(src, *ts, n, d, nullptr, C, C + n, z, S(stream));
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,252 @@
+// Runtime plumbing of the C-ABI: errors, device memory, streams, events, the
+// kernel-timing probe, and the host half of AES (key schedule, T-table).
+#include "common.h"
+#include <cstring>
+#include <mutex>
+#include <map>
+
+namespace aby3g {
+
+namespace {
+thread_local std::string t_err;
+
+struct ProbeRec {
+    hipEvent_t a, b;
+    int family;
+};
+struct Probe {
+    bool on = false;
+    hipEvent_t pending = nullptr;
+    std::vector<ProbeRec> recs;
+    double ms[8] = {0};
+    u64 launches[8] = {0};
+    std::vector<hipEvent_t> pool;
+    hipEvent_t get() {
+        if (!pool.empty()) {
+            hipEvent_t e = pool.back();
+            pool.pop_back();
+            return e;
+        }
+        hipEvent_t e;
+        ABY3G_CHECK_HIP(hipEventCreate(&e));
+        return e;
+    }
+    void drain() {
+        for (auto& r : recs) {
+            ABY3G_CHECK_HIP(hipEventSynchronize(r.b));
+            float t = 0;
+            ABY3G_CHECK_HIP(hipEventElapsedTime(&t, r.a, r.b));
+            ms[r.family] += t;
+            launches[r.family] += 1;
+            pool.push_back(r.a);
+            pool.push_back(r.b);
+        }
+        recs.clear();
+    }
+};
+thread_local Probe t_probe;
+
+// FIPS-197 S-box from its definition (inverse in GF(2^8), then the affine map).
+struct Tables {
+    u8 sbox[256];
+    u32 T0[256];
+    Tables() {
+        auto gmul = [](u8 a, u8 b) {
+            u8 p = 0;
+            for (int i = 0; i < 8; ++i) {
+                if (b & 1) p ^= a;
+                bool hi = a & 0x80;
+                a = (u8)(a << 1);
+                if (hi) a ^= 0x1b;
+                b >>= 1;
+            }
+            return p;
+        };
+        for (int x = 0; x < 256; ++x) {
+            u8 inv = 0;
+            for (int y = 1; x && y < 256; ++y)
+                if (gmul((u8)x, (u8)y) == 1) {
+                    inv = (u8)y;
+                    break;
+                }
+            u8 r = 0x63;
+            for (int i = 0; i < 8; ++i) {
+                int bit = ((inv >> i) ^ (inv >> ((i + 4) & 7)) ^ (inv >> ((i + 5) & 7)) ^ (inv >> ((i + 6) & 7)) ^
+                           (inv >> ((i + 7) & 7))) & 1;
+                r ^= (u8)(bit << i);
+            }
+            sbox[x] = r;
+            u8 s = r, s2 = gmul(r, 2), s3 = gmul(r, 3);
+            T0[x] = (u32)s2 | ((u32)s << 8) | ((u32)s << 16) | ((u32)s3 << 24);
+        }
+    }
+};
+const Tables& tables() {
+    static Tables t;
+    return t;
+}
+
+std::mutex g_tab_mu;
+std::map<int, u32*> g_tab_dev;
+}  // namespace
+
+void set_error(const std::string& msg) { t_err = msg; }
+
+void probe_begin(hipStream_t s) {
+    if (!t_probe.on) return;
+    t_probe.pending = t_probe.get();
+    ABY3G_CHECK_HIP(hipEventRecord(t_probe.pending, s));
+}
+void probe_end(int family, hipStream_t s) {
+    if (!t_probe.on || !t_probe.pending) return;
+    hipEvent_t b = t_probe.get();
+    ABY3G_CHECK_HIP(hipEventRecord(b, s));
+    t_probe.recs.push_back(ProbeRec{t_probe.pending, b, family});
+    t_probe.pending = nullptr;
+    if (t_probe.recs.size() > 4096) t_probe.drain();
+}
+
+AesKey expand_key(const u8 key[16]) {
+    const u8* S = tables().sbox;
+    AesKey k;
+    for (int c = 0; c < 4; ++c)
+        k.rk[c] = (u32)key[4 * c] | ((u32)key[4 * c + 1] << 8) | ((u32)key[4 * c + 2] << 16) |
+                  ((u32)key[4 * c + 3] << 24);
+    u32 rcon = 1;
+    for (int i = 4; i < 44; ++i) {
+        u32 t = k.rk[i - 1];
+        if (i % 4 == 0) {
+            t = (t >> 8) | (t << 24);  // RotWord on a little-endian word
+            t = (u32)S[t & 0xff] | ((u32)S[(t >> 8) & 0xff] << 8) | ((u32)S[(t >> 16) & 0xff] << 16) |
+                ((u32)S[t >> 24] << 24);
+            t ^= rcon;
+            rcon = (rcon << 1) ^ ((rcon & 0x80) ? 0x11b : 0);
+        }
+        k.rk[i] = k.rk[i - 4] ^ t;
+    }
+    return k;
+}
+
+const u32* aes_table() {
+    int dev = 0;
+    ABY3G_CHECK_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(g_tab_mu);
+    auto it = g_tab_dev.find(dev);
+    if (it != g_tab_dev.end()) return it->second;
+    u32* p = nullptr;
+    ABY3G_CHECK_HIP(hipMalloc(&p, sizeof(tables().T0)));
+    ABY3G_CHECK_HIP(hipMemcpy(p, tables().T0, sizeof(tables().T0), hipMemcpyHostToDevice));
+    g_tab_dev[dev] = p;
+    return p;
+}
+
+}  // namespace aby3g
+
+using namespace aby3g;
+
+extern "C" {
+
+const char* aby3g_last_error(void) { return t_err.c_str(); }
+int aby3g_version(void) { return 1; }
+
+int aby3g_device_count(int* n) {
+    return guarded([&] { ABY3G_CHECK_HIP(hipGetDeviceCount(n)); });
+}
+int aby3g_set_device(int device) {
+    return guarded([&] { ABY3G_CHECK_HIP(hipSetDevice(device)); });
+}
+
+int aby3g_malloc(void** ptr, size_t bytes) {
+    return guarded([&] {
+        hipError_t e = hipMalloc(ptr, bytes ? bytes : 16);
+        if (e != hipSuccess) throw Error{ABY3G_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e)};
+    });
+}
+int aby3g_free(void* ptr) {
+    return guarded([&] { ABY3G_CHECK_HIP(hipFree(ptr)); });
+}
+int aby3g_host_malloc(void** ptr, size_t bytes) {
+    return guarded([&] { ABY3G_CHECK_HIP(hipHostMalloc(ptr, bytes ? bytes : 16, hipHostMallocDefault)); });
+}
+int aby3g_host_free(void* ptr) {
+    return guarded([&] { ABY3G_CHECK_HIP(hipHostFree(ptr)); });
+}
+int aby3g_memcpy(void* dst, const void* src, size_t bytes, int kind, aby3g_stream stream) {
+    return guarded([&] {
+        if (!bytes) return;
+        hipMemcpyKind k = kind == 0   ? hipMemcpyHostToDevice
+                          : kind == 1 ? hipMemcpyDeviceToHost
+                          : kind == 2 ? hipMemcpyDeviceToDevice
+                                      : hipMemcpyDefault;
+        ABY3G_CHECK_HIP(hipMemcpyAsync(dst, src, bytes, k, S(stream)));
+    });
+}
+int aby3g_memset(void* dst, int value, size_t bytes, aby3g_stream stream) {
+    return guarded([&] {
+        if (bytes) ABY3G_CHECK_HIP(hipMemsetAsync(dst, value, bytes, S(stream)));
+    });
+}
+int aby3g_stream_create(aby3g_stream* stream) {
+    return guarded([&] {
+        hipStream_t s;
+        ABY3G_CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        *stream = s;
+    });
+}
+int aby3g_stream_destroy(aby3g_stream stream) {
+    return guarded([&] { ABY3G_CHECK_HIP(hipStreamDestroy(S(stream))); });
+}
+int aby3g_stream_sync(aby3g_stream stream) {
+    return guarded([&] { ABY3G_CHECK_HIP(hipStreamSynchronize(S(stream))); });
+}
+int aby3g_device_sync(void) {
+    return guarded([&] { ABY3G_CHECK_HIP(hipDeviceSynchronize()); });
+}
+int aby3g_event_create(aby3g_event* ev) {
+    return guarded([&] {
+        hipEvent_t e;
+        ABY3G_CHECK_HIP(hipEventCreate(&e));
+        *ev = e;
+    });
+}
+int aby3g_event_destroy(aby3g_event ev) {
+    return guarded([&] { ABY3G_CHECK_HIP(hipEventDestroy((hipEvent_t)ev)); });
+}
+int aby3g_event_record(aby3g_event ev, aby3g_stream stream) {
+    return guarded([&] { ABY3G_CHECK_HIP(hipEventRecord((hipEvent_t)ev, S(stream))); });
+}
+int aby3g_event_sync(aby3g_event ev) {
+    return guarded([&] { ABY3G_CHECK_HIP(hipEventSynchronize((hipEvent_t)ev)); });
+}
+int aby3g_stream_wait_event(aby3g_stream stream, aby3g_event ev) {
+    return guarded([&] { ABY3G_CHECK_HIP(hipStreamWaitEvent(S(stream), (hipEvent_t)ev, 0)); });
+}
+int aby3g_event_elapsed_ms(aby3g_event start, aby3g_event end, float* ms) {
+    return guarded([&] { ABY3G_CHECK_HIP(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)end)); });
+}
+
+int aby3g_probe_enable(int on) {
+    return guarded([&] {
+        if (!on) t_probe.drain();
+        t_probe.on = on != 0;
+    });
+}
+int aby3g_probe_read(int family, double* ms, uint64_t* launches) {
+    return guarded([&] {
+        ABY3G_REQUIRE(family >= 0 && family < 8, "family out of range");
+        t_probe.drain();
+        *ms = t_probe.ms[family];
+        *launches = t_probe.launches[family];
+    });
+}
+int aby3g_probe_reset(void) {
+    return guarded([&] {
+        t_probe.drain();
+        for (int i = 0; i < 8; ++i) {
+            t_probe.ms[i] = 0;
+            t_probe.launches[i] = 0;
+        }
+    });
+}
+
+}  // extern "C"

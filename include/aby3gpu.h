@@ -1,0 +1,245 @@
+/*
+ * aby3gpu.h -- C-ABI of the MI355X (gfx950) local-compute engine for ABY3's
+ * replicated-secret-sharing hot path.
+ *
+ * Every entry point replaces one local-compute step of the reference
+ * (Fannxy/aby3 @ 2024-10-24, paths relative to /root/reference). The host
+ * runtime (aby3_amd/host: Sh3Runtime / Sh3Evaluator / Sh3Encryptor /
+ * Sh3BinaryEvaluator / Sh3Piecewise) is the only intended caller; it owns the
+ * protocol, the message schedule and every stream offset, and calls these
+ * functions with plain device pointers.
+ *
+ * Conventions
+ *   - All data pointers are DEVICE pointers owned by the caller unless a
+ *     parameter says "host". Calls are asynchronous on `stream` (a hipStream_t
+ *     passed as void*; NULL = the default stream) and thread-compatible.
+ *   - A shared matrix of one party is ONE contiguous allocation [2][rows][cols]
+ *     of int64: share 0 (x_i) followed by share 1 (x_{i-1}) -- the two
+ *     Eigen buffers of si64Matrix (aby3/sh3/Sh3Types.h:198-271) made adjacent.
+ *   - Arithmetic is mod 2^64 (two's complement wrap), shifts are arithmetic.
+ *   - Randomness follows cryptoTools: AES(k, c) encrypts LE64(c) || 0^8;
+ *     PRNG(seed) is the byte stream of AES(seed, 0), AES(seed, 1), ...
+ *     (SURVEY.md Appendix A). Stream positions are explicit arguments.
+ *   - Return value: 0 on success, nonzero ABY3G_E* on error; the message is
+ *     available from aby3g_last_error() (thread-local). No exceptions cross.
+ */
+#ifndef ABY3GPU_H
+#define ABY3GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* aby3g_stream;
+typedef void* aby3g_event;
+
+enum { ABY3G_OK = 0, ABY3G_EINVAL = 1, ABY3G_EHIP = 2, ABY3G_ENOMEM = 3 };
+
+/* ------------------------------------------------------------------ misc -- */
+const char* aby3g_last_error(void);
+int aby3g_version(void);
+int aby3g_device_count(int* n);
+int aby3g_set_device(int device);
+
+/* Memory, streams and events. The host runtime reaches the GPU only through
+ * this header. kind: 0 host->device, 1 device->host, 2 device->device,
+ * 3 let the runtime infer. */
+int aby3g_malloc(void** ptr, size_t bytes);
+int aby3g_free(void* ptr);
+int aby3g_host_malloc(void** ptr, size_t bytes); /* pinned host memory */
+int aby3g_host_free(void* ptr);
+int aby3g_memcpy(void* dst, const void* src, size_t bytes, int kind, aby3g_stream stream);
+int aby3g_memset(void* dst, int value, size_t bytes, aby3g_stream stream);
+int aby3g_stream_create(aby3g_stream* stream);
+int aby3g_stream_destroy(aby3g_stream stream);
+int aby3g_stream_sync(aby3g_stream stream);
+int aby3g_device_sync(void);
+int aby3g_event_create(aby3g_event* ev);
+int aby3g_event_destroy(aby3g_event ev);
+int aby3g_event_record(aby3g_event ev, aby3g_stream stream);
+int aby3g_event_sync(aby3g_event ev);
+int aby3g_stream_wait_event(aby3g_stream stream, aby3g_event ev);
+int aby3g_event_elapsed_ms(aby3g_event start, aby3g_event end, float* ms);
+
+/* Kernel timing probe: when enabled, every kernel launched by this library on
+ * the calling thread is bracketed by events; aby3g_probe_read() returns the
+ * accumulated device time (ms) and launch count per kernel family:
+ * 0 share GEMM (MFMA), 1 mul epilogue / hadamard,
+ * 2 binary gate layers, 3 AES streams, 4 other, 5 GEMM digit planes.
+ * Used by bench.py. */
+int aby3g_probe_enable(int on);
+int aby3g_probe_read(int family, double* ms, uint64_t* launches);
+int aby3g_probe_reset(void);
+
+/* --------------------------------------------------- AES / PRNG streams -- */
+/* oc::AES::ecbEncCounterMode: out[i] = AES(key, ctr_base + i), 16 B each.
+ * Replaces the host AES-NI refills of Sh3ShareGen.h:50-56 and SharedOT.cpp:15. */
+int aby3g_aes_ctr(const uint8_t key[16], uint64_t ctr_base, uint64_t nblocks, void* out, aby3g_stream stream);
+
+/* oc::PRNG(seed) bytes [byte_off, byte_off + nbytes) (both multiples of 8).
+ * Replaces mPrevCommon/mNextCommon.get(...) (Sh3Evaluator.cpp:526-527,
+ * Sh3BinaryEvaluator.h:96-102, Sh3Evaluator.cpp:151-153,188,234-235). */
+int aby3g_prng_fill(const uint8_t seed[16], uint64_t byte_off, uint64_t nbytes, void* out, aby3g_stream stream);
+
+/* Sh3ShareGen draws j = draw_base .. draw_base+n-1 with the two zero-share
+ * keys (k_prev = mShareGen[0], k_next = mShareGen[1]; Sh3ShareGen.h:19-20).
+ *   ABY3G_DRAW_ARITH:    out0[i] = getShare()       (+ addend[i])   Sh3ShareGen.h:60-75
+ *   ABY3G_DRAW_BIN:      out0[i] = getBinaryShare() (^ addend[i])   Sh3ShareGen.h:77-92
+ *   ABY3G_DRAW_RANDPAIR: (out0[i], out1[i]) = getRandIntShare()     Sh3ShareGen.h:95-109
+ * addend may be NULL. Used by Sh3Encryptor::local/remote*Matrix
+ * (Sh3Encryptor.cpp:229-340) and the binary engine's AND-gate masks
+ * (Sh3BinaryEvaluator.cpp:1406-1434, where z[k][w] is draw k*words + w). */
+enum { ABY3G_DRAW_ARITH = 0, ABY3G_DRAW_BIN = 1, ABY3G_DRAW_RANDPAIR = 2 };
+int aby3g_share_draws(int kind, const uint8_t k_prev[16], const uint8_t k_next[16], uint64_t draw_base, uint64_t n,
+                      const int64_t* addend, int64_t* out0, int64_t* out1, aby3g_stream stream);
+
+/* -------------------------------------------------- arithmetic evaluator -- */
+/* Local share product of Sh3Evaluator::asyncMul:
+ *   ABY3G_MUL_HADAMARD  C0(i) = A0(i)B0(i) + A0(i)B1(i) + A1(i)B0(i)
+ *                       (the fork: Sh3Evaluator.cpp:101-103, 667-668);
+ *                       A, B, C are M x N (K is ignored).
+ *   ABY3G_MUL_GEMM      C0 = A0 B0 + A0 B1 + A1 B0 = [A0|A1] [[B0+B1];[B0]]
+ *                       (upstream: Sh3Evaluator.cpp:96-99, 662-665);
+ *                       A is [2][M][K], B is [2][K][N], C is M x N.
+ * GEMM runs on int8 MFMA over an exact balanced base-256 digit split
+ * (36 digit-pair planes, i32 accumulation, i64 recombination). */
+enum { ABY3G_MUL_HADAMARD = 0, ABY3G_MUL_GEMM = 1 };
+
+/* Zero-share added to C0 (Sh3Evaluator.cpp:104: C0(i) += getShare(), draw
+ * draw_base + i in row-major order). */
+typedef struct {
+    uint8_t k_prev[16];
+    uint8_t k_next[16];
+    uint64_t draw_base;
+} aby3g_zero_share;
+
+/* Truncation-pair streams (Sh3Evaluator.cpp:526-527): t0 <- next stream at
+ * next_off, t1 <- prev stream at prev_off, 8 bytes per element, row-major. */
+typedef struct {
+    uint8_t next_seed[16];
+    uint64_t next_off;
+    uint8_t prev_seed[16];
+    uint64_t prev_off;
+} aby3g_trunc_streams;
+
+/* Scratch needed by aby3g_mul_local / aby3g_mul_trunc_local (0 for Hadamard). */
+size_t aby3g_mul_workspace_bytes(int mode, uint64_t M, uint64_t K, uint64_t N);
+
+/* asyncMul without truncation, local part (Sh3Evaluator.cpp:92-116):
+ * C0 = share product (+ zero-share if zs != NULL). The caller sends C0 to
+ * next and receives C1 from prev. zs is a HOST pointer. */
+int aby3g_mul_local(int mode, const int64_t* A, const int64_t* B, int64_t* C0, uint64_t M, uint64_t K, uint64_t N,
+                    const aby3g_zero_share* zs, void* workspace, size_t workspace_bytes, aby3g_stream stream);
+
+/* getTruncationTuple (Sh3Evaluator.cpp:503-566): R = t0 >> 2,
+ * RT = (t0 >> (d+2), t1 >> (d+2)); RT is [2][n]. ts is a HOST pointer. */
+int aby3g_trunc_tuple(const aby3g_trunc_streams* ts, uint64_t n, unsigned d, int64_t* R, int64_t* RT,
+                      aby3g_stream stream);
+
+/* asyncMul with truncation, round-1 local part (Sh3Evaluator.cpp:658-673):
+ * z = share product - R (the value sent to P0/P1), C = RT ([2][M][N]). */
+int aby3g_mul_trunc_local(int mode, const int64_t* A, const int64_t* B, uint64_t M, uint64_t K, uint64_t N, unsigned d,
+                          const aby3g_trunc_streams* ts, int64_t* z, int64_t* C, void* workspace,
+                          size_t workspace_bytes, aby3g_stream stream);
+
+/* Round-2 continuation (Sh3Evaluator.cpp:703-719), parties 0 and 1:
+ * C[party] += (z_a + z_b + z_own) >> d  over n elements ([2][n] layout). */
+int aby3g_trunc_finalize(int party, const int64_t* z_a, const int64_t* z_b, const int64_t* z_own, unsigned d,
+                         int64_t* C, uint64_t n, aby3g_stream stream);
+
+/* --------------------------------------------- 3-party OT multiplications -- */
+/* A stream position: PRNG(seed) at byte offset off. */
+typedef struct {
+    uint8_t seed[16];
+    uint64_t off;
+} aby3g_stream_pos;
+
+/* asyncMul(si64Matrix A, sbMatrix B (1 bit), C), party 0 (Sh3Evaluator.cpp:132-163):
+ * per element: z <- prev, c0 <- next, c1 <- prev (prev advances 16n, next 8n);
+ * C = (c0, c1); s0[bb0] = -(c0+c1)-z, s0[bb0^1] = A0+A1 + that;
+ * send_msgs = SharedOT::send pads (ot_key, ctr ot_ctr) ^ s0  ([n][2]);
+ * help_msgs = SharedOT::help pads (ot_key, ctr ot_ctr + n) chosen by B0 ([n]). */
+int aby3g_bitmul_p0(const int64_t* A, const int64_t* B, uint64_t n, const aby3g_stream_pos* prev,
+                    const aby3g_stream_pos* next, const uint8_t ot_key[16], uint64_t ot_ctr, int64_t* C,
+                    int64_t* send_msgs, int64_t* help_msgs, aby3g_stream stream);
+/* party 2 (:202-240): z <- next, c0 <- next per element (next advances 16n);
+ * C share 0 = c0; help_msgs = pads(ot_key, ot_ctr) chosen by B1;
+ * send_msgs = pads(ot_key, ot_ctr + n) ^ s1 with s1[bb1] = z, s1[bb1^1] = A1 + z. */
+int aby3g_bitmul_p2(const int64_t* A, const int64_t* B, uint64_t n, const aby3g_stream_pos* next,
+                    const uint8_t ot_key[16], uint64_t ot_ctr, int64_t* C, int64_t* help_msgs, int64_t* send_msgs,
+                    aby3g_stream stream);
+/* SharedOT::recv (SharedOT.cpp:102-126): out[i] (+)= msgs[i][c_i] ^ mc[i] where
+ * c_i = choice_src[i] & 1; accumulate != 0 adds into out (mod 2^64). */
+int aby3g_ot_recv(const int64_t* msgs, const int64_t* mc, const int64_t* choice_src, uint64_t n, int accumulate,
+                  int64_t* out, aby3g_stream stream);
+/* asyncMul(i64 a, sbMatrix B, C) party 0 (Sh3Evaluator.cpp:430-447):
+ * s0[bb] = getShare(), s0[bb^1] = a + that, bb = B0^B1;
+ * msgs_next = pads(ot_next_key, ctr_next) ^ s0; msgs_prev = pads(ot_prev_key, ctr_prev) ^ s0. */
+int aby3g_pubmul_p0(int64_t a, const int64_t* B, uint64_t n, const aby3g_zero_share* zs,
+                    const uint8_t ot_next_key[16], uint64_t ctr_next, const uint8_t ot_prev_key[16],
+                    uint64_t ctr_prev, int64_t* msgs_next, int64_t* msgs_prev, aby3g_stream stream);
+/* parties 1 and 2 (:452-487): share_out[i] = getShare(); help_msgs = pads(ot_key, ctr)
+ * chosen by choice_src (P1: B share 0, P2: B share 1). */
+int aby3g_pubmul_helper(const int64_t* choice_src, uint64_t n, const aby3g_zero_share* zs, const uint8_t ot_key[16],
+                        uint64_t ctr, int64_t* share_out, int64_t* help_msgs, aby3g_stream stream);
+
+/* ------------------------------------------------------- binary engine -- */
+/* Gate types of the bit-sliced engine (Sh3BinaryEvaluator.cpp:700-1065) plus
+ * INV (local NOT of both shares). AND, OR, NOR, NA_AND are "AND-type": their
+ * share 0 is masked by z and sent to next; share 1 arrives next level. */
+enum {
+    ABY3G_GATE_XOR = 0,
+    ABY3G_GATE_NXOR = 1,
+    ABY3G_GATE_AND = 2,
+    ABY3G_GATE_OR = 3,
+    ABY3G_GATE_NOR = 4,
+    ABY3G_GATE_NA_AND = 5,
+    ABY3G_GATE_COPY = 6,
+    ABY3G_GATE_INV = 7
+};
+/* One gate of a batch. z_row: row of the z matrix (AND-type gates);
+ * send_row: row of the level's send buffer (AND-type gates). */
+typedef struct {
+    uint32_t in0, in1, out, type;
+    uint32_t z_row, send_row;
+} aby3g_gate;
+
+/* Evaluate a batch of mutually independent gates over `words` 64-row words.
+ * mem = [2][wires][words] u64 (wire-major, Sh3Types.h:537-599 sPackedBin),
+ * z = [nAnd][words] masks (aby3g_share_draws ABY3G_DRAW_BIN with the setCir
+ * keys), sendbuf = [levelAnds][words]. gates is a DEVICE array. */
+int aby3g_bin_gates(const aby3g_gate* gates, uint32_t ngates, uint64_t* mem, uint64_t wires, uint64_t words,
+                    const uint64_t* z, uint64_t* sendbuf, aby3g_stream stream);
+/* Level entry (:555-573): share-1 row of out_wires[j] <- recvbuf row j. */
+int aby3g_bin_unpack(const uint64_t* recvbuf, const uint32_t* out_wires, uint32_t n, uint64_t* mem, uint64_t wires,
+                     uint64_t words, aby3g_stream stream);
+/* setInput (:200-276): bit-transpose a [rows][cols64] i64 share matrix into
+ * nbits consecutive wire rows starting at wire_rows (stride `words`),
+ * zero padding rows >= rows. */
+int aby3g_bits_to_wires(const int64_t* in, uint64_t rows, uint64_t cols64, uint32_t nbits, uint64_t* wire_rows,
+                        uint64_t words, aby3g_stream stream);
+/* getOutput (:1285-1404): transpose wire rows (wire ids in the DEVICE array
+ * wires, row base = mem_share) back to [rows][ceil(nbits/64)] i64. */
+int aby3g_wires_to_bits(const uint64_t* mem_share, const uint32_t* wires, uint32_t nbits, uint64_t words,
+                        int64_t* out, uint64_t rows, aby3g_stream stream);
+
+/* ------------------------------------------------ element-wise helpers -- */
+/* out[i] = ca*a[i] + cb*b[i] + c (mod 2^64); b may be NULL. Covers share
+ * sums/differences (BuildingBlocks.cpp:475-480, Sh3Piecewise.cpp:403-470,
+ * :543-563), fixed-point constants and output accumulation. */
+int aby3g_i64_lincomb(uint64_t n, int64_t ca, const int64_t* a, int64_t cb, const int64_t* b, int64_t c, int64_t* out,
+                      aby3g_stream stream);
+/* Bitwise ops on u64 vectors: 0 xor, 1 and, 2 not(a), 3 lsb-to-mask (-(a&1)),
+ * 4 copy. b may be NULL for unary ops. */
+int aby3g_u64_bitop(int op, uint64_t n, const uint64_t* a, const uint64_t* b, uint64_t* out, aby3g_stream stream);
+/* dst[i] = src[idx[i]] (gather) and dst[idx[i]] = src[i] (scatter), u64. */
+int aby3g_u64_gather(uint64_t n, const uint32_t* idx, const uint64_t* src, uint64_t* dst, aby3g_stream stream);
+int aby3g_u64_scatter(uint64_t n, const uint32_t* idx, const uint64_t* src, uint64_t* dst, aby3g_stream stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ABY3GPU_H */

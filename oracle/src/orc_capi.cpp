@@ -1,0 +1,285 @@
+// TEST INFRASTRUCTURE ONLY -- C entry points of the CPU oracle for ctypes
+// (tests/oracle.py). Plain pointers and sizes; errors return nonzero.
+#include "orc_core.h"
+#include <cstring>
+#include <string>
+
+using namespace orc;
+
+namespace {
+thread_local std::string g_err;
+template <class F>
+int guard(F&& f) {
+    try {
+        f();
+        return 0;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return 1;
+    }
+}
+Mat toMat(const int64_t* p, u64 r, u64 c) {
+    Mat m(r, c);
+    memcpy(m.v.data(), p, 8 * r * c);
+    return m;
+}
+SMat toSMat(const int64_t* s0, const int64_t* s1, u64 r, u64 c) {
+    SMat m;
+    m.s[0] = toMat(s0, r, c);
+    m.s[1] = toMat(s1, r, c);
+    return m;
+}
+// shares layout for the 3-party outputs: [party][share][rows*cols]
+void putShared(const Shared& x, int64_t* out) {
+    u64 n = x[0].size();
+    for (int p = 0; p < 3; ++p)
+        for (int s = 0; s < 2; ++s) memcpy(out + (2 * p + s) * n, x[p].s[s].v.data(), 8 * n);
+}
+Circuit toCircuit(uint32_t wires, const uint32_t* gates, uint64_t ngates, const uint32_t* levels, uint64_t nlevels,
+                  const uint32_t* inWires, const uint32_t* inSizes, uint64_t nin, const uint32_t* outWires,
+                  const uint32_t* outSizes, uint64_t nout) {
+    Circuit c;
+    c.wireCount = wires;
+    c.gates.resize(ngates);
+    for (u64 g = 0; g < ngates; ++g) c.gates[g] = Gate{gates[4 * g], gates[4 * g + 1], gates[4 * g + 2], gates[4 * g + 3]};
+    c.levelCounts.assign(levels, levels + nlevels);
+    u64 o = 0;
+    for (u64 b = 0; b < nin; ++b) {
+        c.inputs.emplace_back(inWires + o, inWires + o + inSizes[b]);
+        o += inSizes[b];
+    }
+    o = 0;
+    for (u64 b = 0; b < nout; ++b) {
+        c.outputs.emplace_back(outWires + o, outWires + o + outSizes[b]);
+        o += outSizes[b];
+    }
+    return c;
+}
+}  // namespace
+
+extern "C" {
+
+const char* orc_last_error() { return g_err.c_str(); }
+int orc_aesni_available() { return aesni_available() ? 1 : 0; }
+
+int orc_aes_ref_encrypt(const uint8_t key[16], const uint8_t in[16], uint8_t out[16]) {
+    return guard([&] {
+        AesRef a;
+        a.setKey(key);
+        a.encrypt(in, out);
+    });
+}
+
+int orc_aes_ctr(const uint8_t key[16], uint64_t base, uint64_t n, uint8_t* out, int use_ref) {
+    return guard([&] {
+        if (use_ref) {
+            AesRef a;
+            a.setKey(key);
+            for (u64 i = 0; i < n; ++i) {
+                Block b = a.encrypt(toBlock(base + i));
+                memcpy(out + 16 * i, &b, 16);
+            }
+        } else {
+            AesNI a;
+            a.setKey(key);
+            a.ctr(base, n, (Block*)out);
+        }
+    });
+}
+
+int orc_prng_bytes(const uint8_t seed[16], uint64_t off, uint64_t n, uint8_t* out) {
+    return guard([&] { prng_bytes(seed, off, n, out); });
+}
+
+// Sh3ShareGen draws j = base .. base+n-1 with keys (k_prev, k_next).
+// kind 0: getShare, 1: getBinaryShare, 2: getRandIntShare (out0 = r[0], out1 = r[1])
+int orc_share_draws(int kind, const uint8_t kprev[16], const uint8_t knext[16], uint64_t base, uint64_t n,
+                    int64_t* out0, int64_t* out1) {
+    return guard([&] {
+        ShareGen g;
+        g.key[0].setKey(kprev);
+        g.key[1].setKey(knext);
+        g.drawIdx = base;
+        for (u64 i = 0; i < n; ++i) {
+            if (kind == 0)
+                out0[i] = g.getShare();
+            else if (kind == 1)
+                out0[i] = g.getBinaryShare();
+            else {
+                auto r = g.getRandIntShare();
+                out0[i] = r[0];
+                out1[i] = r[1];
+            }
+        }
+    });
+}
+
+// Keys a party derives in Sh3ShareGen::init + Sh3Evaluator::init:
+// out = [kSharePrev | kShareNext | kOtPrev | kOtNext] (4 x 16 bytes)
+int orc_party_keys(const uint8_t prevSeed[16], const uint8_t nextSeed[16], uint8_t out[64]) {
+    return guard([&] {
+        Party p;
+        Block ps, ns;
+        memcpy(&ps, prevSeed, 16);
+        memcpy(&ns, nextSeed, 16);
+        p.initEvaluator(0, ps, ns);
+        memcpy(out, p.gen.keyBytes[0], 16);
+        memcpy(out + 16, p.gen.keyBytes[1], 16);
+        prng_bytes(nextSeed, 16, 16, out + 32);
+        prng_bytes(prevSeed, 16, 16, out + 48);
+    });
+}
+
+int orc_local_product(int mode, const int64_t* A0, const int64_t* A1, const int64_t* B0, const int64_t* B1, uint64_t M,
+                      uint64_t K, uint64_t N, int64_t* C0) {
+    return guard([&] {
+        SMat A = toSMat(A0, A1, M, K);
+        SMat B = mode == MUL_GEMM ? toSMat(B0, B1, K, N) : toSMat(B0, B1, M, K);
+        Mat c;
+        localProduct((MulMode)mode, A, B, c);
+        memcpy(C0, c.v.data(), 8 * c.size());
+    });
+}
+
+// getTruncationTuple with the next/prev streams at the given byte offsets.
+int orc_trunc_tuple(const uint8_t nextSeed[16], uint64_t nextOff, const uint8_t prevSeed[16], uint64_t prevOff,
+                    uint64_t n, uint64_t d, int64_t* R, int64_t* RT0, int64_t* RT1) {
+    return guard([&] {
+        Party p;
+        p.gen.next.init(nextSeed);
+        p.gen.next.off = nextOff;
+        p.gen.prev.init(prevSeed);
+        p.gen.prev.off = prevOff;
+        TruncPair t = truncationTuple(p, n, 1, d);
+        memcpy(R, t.R.v.data(), 8 * n);
+        memcpy(RT0, t.RT.s[0].v.data(), 8 * n);
+        memcpy(RT1, t.RT.s[1].v.data(), 8 * n);
+    });
+}
+
+// Full 3-party protocol simulations from plaintext inputs. Inputs are shared
+// by party 0 with Encryptor seeds toBlock(0, i); the evaluator uses
+// toBlock(1, i) (Sh3EvaluatorTests.cpp:617-623). out_shares: [3][2][n].
+int orc_sim_mul(int mode, int trunc, uint64_t d, const int64_t* a, const int64_t* b, uint64_t M, uint64_t K,
+                uint64_t N, int64_t* out_shares, int64_t* out_plain) {
+    return guard([&] {
+        auto enc = makeEncryptors(0);
+        auto ev = makeEvaluators(1);
+        Mat am = toMat(a, M, K);
+        Mat bm = mode == MUL_GEMM ? toMat(b, K, N) : toMat(b, M, K);
+        Shared A = shareInt(enc, 0, am), B = shareInt(enc, 0, bm);
+        Shared C = trunc ? mulTrunc(ev, (MulMode)mode, A, B, d) : mul(ev, (MulMode)mode, A, B);
+        if (!consistent(C)) throw std::runtime_error("inconsistent shares");
+        putShared(C, out_shares);
+        Mat r = revealInt(C);
+        memcpy(out_plain, r.v.data(), 8 * r.size());
+    });
+}
+
+// a * b for a shared i64 vector and a shared bit vector (kind 0, Sh3Evaluator.cpp:119-263)
+// or public a * shared bit (kind 1, :418-501).
+int orc_sim_mul_bit(int kind, const int64_t* a, int64_t apub, const int64_t* bits, uint64_t n, int64_t* out_shares,
+                    int64_t* out_plain) {
+    return guard([&] {
+        auto enc = makeEncryptors(0);
+        auto ev = makeEvaluators(1);
+        Shared B = shareBin(enc, 0, toMat(bits, n, 1));
+        Shared C;
+        if (kind == 0) {
+            Shared A = shareInt(enc, 0, toMat(a, n, 1));
+            C = mulBit(ev, A, B);
+        } else {
+            C = mulPubBit(ev, apub, B);
+        }
+        if (!consistent(C)) throw std::runtime_error("inconsistent shares");
+        putShared(C, out_shares);
+        Mat r = revealInt(C);
+        memcpy(out_plain, r.v.data(), 8 * n);
+    });
+}
+
+// Evaluate a serialized circuit on binary-shared 64-bit inputs (one i64 column
+// per 64 input wires). ins: [nin][rows*inCols[b]]; outs: revealed [nout][rows*outCols].
+int orc_sim_circuit(uint32_t wires, const uint32_t* gates, uint64_t ngates, const uint32_t* levels, uint64_t nlevels,
+                    const uint32_t* inWires, const uint32_t* inSizes, uint64_t nin, const uint32_t* outWires,
+                    const uint32_t* outSizes, uint64_t nout, uint64_t rows, const int64_t* ins, int64_t* outs,
+                    int64_t* out_shares) {
+    return guard([&] {
+        Circuit c = toCircuit(wires, gates, ngates, levels, nlevels, inWires, inSizes, nin, outWires, outSizes, nout);
+        auto enc = makeEncryptors(0);
+        auto ev = makeEvaluators(1);
+        std::vector<Shared> sh(nin);
+        u64 off = 0;
+        std::vector<const Shared*> ptrs;
+        for (u64 b = 0; b < nin; ++b) {
+            u64 cols = (inSizes[b] + 63) / 64;
+            sh[b] = shareBin(enc, 0, toMat(ins + off, rows, cols));
+            off += rows * cols;
+        }
+        for (auto& s : sh) ptrs.push_back(&s);
+        auto o = evalCircuit(ev, c, ptrs);
+        off = 0;
+        u64 soff = 0;
+        for (u64 b = 0; b < nout; ++b) {
+            if (!consistent(o[b])) throw std::runtime_error("inconsistent shares");
+            Mat r = revealBin(o[b]);
+            memcpy(outs + off, r.v.data(), 8 * r.size());
+            off += r.size();
+            if (out_shares) {
+                putShared(o[b], out_shares + soff);
+                soff += 6 * r.size();
+            }
+        }
+    });
+}
+
+// Piecewise eval (3PC) with the reference's sigmoid (aby3ML.h:121-139) or a
+// ReLU-like (thresholds {0}, coefs {{}, {0, 1}}): kind 0 sigmoid, 1 relu.
+int orc_sim_piecewise(int kind, uint32_t wires, const uint32_t* gates, uint64_t ngates, const uint32_t* levels,
+                      uint64_t nlevels, const uint32_t* inWires, const uint32_t* inSizes, uint64_t nin,
+                      const uint32_t* outWires, const uint32_t* outSizes, uint64_t nout, const int64_t* x, uint64_t n,
+                      uint64_t D, int64_t* out_shares, int64_t* out_plain) {
+    return guard([&] {
+        Circuit c = toCircuit(wires, gates, ngates, levels, nlevels, inWires, inSizes, nin, outWires, outSizes, nout);
+        Piecewise pw;
+        if (kind == 0) {
+            pw.thresholds = {Coef{false, 0, -0.5}, Coef{false, 0, 0.5}};
+            pw.coefs = {{}, {Coef{false, 0, 0.5}, Coef{true, 1, 0}}, {Coef{true, 1, 0}}};
+        } else {
+            pw.thresholds = {Coef{true, 0, 0}};
+            pw.coefs = {{}, {Coef{true, 0, 0}, Coef{true, 1, 0}}};
+        }
+        auto enc = makeEncryptors(0);
+        auto ev = makeEvaluators(1);
+        Shared X = shareInt(enc, 0, toMat(x, n, 1));
+        Shared Y = piecewiseEval(ev, pw, c, X, D);
+        if (!consistent(Y)) throw std::runtime_error("inconsistent shares");
+        putShared(Y, out_shares);
+        Mat r = revealInt(Y);
+        memcpy(out_plain, r.v.data(), 8 * n);
+    });
+}
+
+int orc_sim_fetch_msb(uint32_t wires, const uint32_t* gates, uint64_t ngates, const uint32_t* levels,
+                      uint64_t nlevels, const uint32_t* inWires, const uint32_t* inSizes, uint64_t nin,
+                      const uint32_t* outWires, const uint32_t* outSizes, uint64_t nout, const int64_t* a,
+                      const int64_t* b, uint64_t n, int64_t* out_plain) {
+    return guard([&] {
+        Circuit c = toCircuit(wires, gates, ngates, levels, nlevels, inWires, inSizes, nin, outWires, outSizes, nout);
+        auto enc = makeEncryptors(0);
+        auto ev = makeEvaluators(1);
+        Shared A = shareInt(enc, 0, toMat(a, n, 1));
+        Shared B = shareInt(enc, 0, toMat(b, n, 1));
+        // cipher_gt: diff = B - A (BuildingBlocks.cpp:525-532)
+        Shared diff = A;
+        for (int p = 0; p < 3; ++p)
+            for (int s = 0; s < 2; ++s)
+                for (u64 k = 0; k < n; ++k)
+                    diff[p].s[s].v[k] = (i64)((u64)B[p].s[s].v[k] - (u64)A[p].s[s].v[k]);
+        Shared r = fetchMsb(ev, c, diff);
+        Mat m = revealBin(r);
+        memcpy(out_plain, m.v.data(), 8 * n);
+    });
+}
+
+}  // extern "C"

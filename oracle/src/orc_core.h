@@ -1,0 +1,200 @@
+// TEST INFRASTRUCTURE ONLY -- CPU oracle. Only tests/, __graft_entry__.smoke()
+// and bench.py's cpu_baseline leg may use anything under oracle/.
+//
+// A single-process, CPU-only restatement of the reference's replicated
+// secret-sharing hot path (Fannxy/aby3 @ 2024-10-24). Every routine cites the
+// reference file:line it follows. The three parties are simulated in one
+// process; "messages" are plain vectors handed from one party to the next in
+// the order the reference's Channels deliver them.
+//
+// Parity anchors: revealed results are pinned by the
+// reference's own tests (Sh3EvaluatorTests.cpp, Sh3BinaryEvaluatorTests.cpp,
+// Test.cpp, BoolTest.cpp, SortTest.cpp); share-level bytes are pinned only by
+// the cryptoTools AES/PRNG semantics (FIPS-197 KAT + Appendix A).
+#pragma once
+#include "orc_aes.h"
+#include <array>
+#include <vector>
+#include <string>
+#include <stdexcept>
+
+namespace orc {
+
+// --------------------------------------------------------------------------
+// Correlated randomness of one party.
+//   Sh3ShareGen::init        aby3/sh3/Sh3ShareGen.h:9-23
+//   Sh3ShareGen::getShare    aby3/sh3/Sh3ShareGen.h:60-75   (v0 - v1)
+//   getBinaryShare           aby3/sh3/Sh3ShareGen.h:77-92   (v0 ^ v1)
+//   getRandIntShare          aby3/sh3/Sh3ShareGen.h:95-109  (v1, v0)
+//   Sh3Evaluator::init       aby3/sh3/Sh3Evaluator.cpp:9-15 (OT keys)
+// --------------------------------------------------------------------------
+struct Stream {  // oc::PRNG restated as (key, byte offset)
+    u8 seed[16];
+    u64 off = 0;
+    void init(const u8 s[16]) { std::copy(s, s + 16, seed); off = 0; }
+    void get(void* dst, u64 nbytes) { prng_bytes(seed, off, nbytes, (u8*)dst); off += nbytes; }
+    Block getBlock() { Block b; get(&b, 16); return b; }
+    i64 getI64() { i64 v; get(&v, 8); return v; }
+};
+
+struct ShareGen {
+    Stream prev, next;      // mPrevCommon, mNextCommon
+    AesNI key[2];           // mShareGen[0] (prev), mShareGen[1] (next)
+    u8 keyBytes[2][16];
+    u64 drawIdx = 0;        // j: index of the next 8-byte draw
+
+    void init(const Block& prevSeed, const Block& nextSeed);
+    // raw halves of the two AES-CTR buffers for draw j
+    void halves(u64 j, u64& v0, u64& v1) const;
+    i64 getShare();
+    i64 getBinaryShare();
+    std::array<i64, 2> getRandIntShare();
+};
+
+// SharedOT (aby3/OT/SharedOT.cpp:6-180): pads = AES(k, ctr) as {lo, hi}.
+struct SharedOT {
+    AesNI aes;
+    u64 idx = ~0ull;
+    void setSeed(const Block& seed) { aes.setKey((const u8*)&seed); idx = 0; }
+    // send(): msgs[i][c] = pad_i[c] ^ m[i][c]   (SharedOT.cpp:6-28)
+    std::vector<std::array<i64, 2>> send(const std::vector<std::array<i64, 2>>& m);
+    // help(): mc[i] = pad_i[choice_i]          (SharedOT.cpp:30-94)
+    std::vector<i64> help(const std::vector<u8>& choices);
+};
+// recv(): out[i] = msgs[i][c_i] ^ mc[i]       (SharedOT.cpp:102-126)
+std::vector<i64> ot_recv(const std::vector<std::array<i64, 2>>& msgs, const std::vector<i64>& mc,
+                         const std::vector<u8>& choices);
+
+struct Party {
+    int idx = 0;
+    ShareGen gen;
+    SharedOT otPrev;  // mOtPrevRecver: key = next stream bytes [16,32)
+    SharedOT otNext;  // mOtNextRecver: key = prev stream bytes [16,32)
+    // Sh3Evaluator::init (Sh3Evaluator.cpp:9-15)
+    void initEvaluator(int pIdx, const Block& prevSeed, const Block& nextSeed);
+    // Sh3Encryptor::init: ShareGen only
+    void initEncryptor(int pIdx, const Block& prevSeed, const Block& nextSeed);
+};
+
+// Seeds used by the reference's unit tests (Sh3EvaluatorTests.cpp:41-47,617-623):
+// party i: prevSeed = toBlock(c, i), nextSeed = toBlock(c, (i+1)%3).
+std::array<Party, 3> makeEvaluators(u64 c);
+std::array<Party, 3> makeEncryptors(u64 c);
+
+// --------------------------------------------------------------------------
+// Shared matrices. One party holds (x_i, x_{i-1}) (Sh3Encryptor.cpp:222-226).
+// --------------------------------------------------------------------------
+struct Mat {
+    u64 rows = 0, cols = 0;
+    std::vector<i64> v;
+    Mat() = default;
+    Mat(u64 r, u64 c) : rows(r), cols(c), v(r * c, 0) {}
+    i64& operator()(u64 r, u64 c) { return v[r * cols + c]; }
+    i64 operator()(u64 r, u64 c) const { return v[r * cols + c]; }
+    u64 size() const { return v.size(); }
+};
+struct SMat {  // si64Matrix / sbMatrix payload (share 0 = own, share 1 = prev's)
+    std::array<Mat, 2> s;
+    SMat() = default;
+    SMat(u64 r, u64 c) { s[0] = Mat(r, c); s[1] = Mat(r, c); }
+    u64 rows() const { return s[0].rows; }
+    u64 cols() const { return s[0].cols; }
+    u64 size() const { return s[0].size(); }
+};
+using Shared = std::array<SMat, 3>;  // the three parties' views
+
+// Sh3Encryptor::localIntMatrix / remoteIntMatrix (Sh3Encryptor.cpp:229-279)
+Shared shareInt(std::array<Party, 3>& enc, int owner, const Mat& m);
+// Sh3Encryptor::localBinMatrix / remoteBinMatrix (Sh3Encryptor.cpp:282-340)
+Shared shareBin(std::array<Party, 3>& enc, int owner, const Mat& m);
+// reveal / revealAll (Sh3Encryptor.cpp:497-551): x0 + x1 + x2 / x0 ^ x1 ^ x2
+Mat revealInt(const Shared& x);
+Mat revealBin(const Shared& x);
+// consistency: party i's share 1 == party i-1's share 0 (testUtils.cpp:92-109)
+bool consistent(const Shared& x);
+
+// --------------------------------------------------------------------------
+// Arithmetic evaluator (Sh3Evaluator.cpp).
+// --------------------------------------------------------------------------
+enum MulMode { MUL_HADAMARD = 0, MUL_GEMM = 1 };
+
+// Local share product C0 = A0*B0 + A0*B1 + A1*B0.
+//   Hadamard: Sh3Evaluator.cpp:101-103 (fork), 667-668
+//   GEMM:     Sh3Evaluator.cpp:96-99 (upstream), 662-665
+// Computed the way Eigen evaluates the expression: three i64 GEMMs, summed.
+void localProduct(MulMode mode, const SMat& A, const SMat& B, Mat& C0);
+
+// asyncMul(si64Matrix, si64Matrix) without truncation (Sh3Evaluator.cpp:92-116):
+// C0 = prod + getShare(); send C0 to next; C1 <- prev.
+Shared mul(std::array<Party, 3>& ev, MulMode mode, const Shared& A, const Shared& B);
+
+// getTruncationTuple (Sh3Evaluator.cpp:503-566)
+struct TruncPair { Mat R; SMat RT; };
+TruncPair truncationTuple(Party& p, u64 rows, u64 cols, u64 d);
+
+// asyncMul(..., shift) (Sh3Evaluator.cpp:651-730)
+Shared mulTrunc(std::array<Party, 3>& ev, MulMode mode, const Shared& A, const Shared& B, u64 d);
+// the per-party halves of that protocol, used by kernel-level parity tests
+void mulTruncLocal(Party& p, MulMode mode, const SMat& A, const SMat& B, u64 d, Mat& zOut, SMat& C);
+void truncFinalize(int pIdx, const Mat& zSum3, u64 d, SMat& C);
+
+// asyncMul(si64Matrix A, sbMatrix B (1 bit), C) via 3-party OT (Sh3Evaluator.cpp:119-263)
+Shared mulBit(std::array<Party, 3>& ev, const Shared& A, const Shared& B);
+// asyncMul(i64 a, sbMatrix B, C) (Sh3Evaluator.cpp:418-501)
+Shared mulPubBit(std::array<Party, 3>& ev, i64 a, const Shared& B);
+
+// --------------------------------------------------------------------------
+// Binary engine (Sh3BinaryEvaluator.cpp). Circuits are data: a gate list in
+// evaluation order split into communication levels (levelByAndDepth order).
+// --------------------------------------------------------------------------
+enum GateType : u32 { G_XOR = 0, G_NXOR = 1, G_AND = 2, G_OR = 3, G_NOR = 4, G_NA_AND = 5, G_COPY = 6, G_INV = 7 };
+inline bool isAndType(u32 t) { return t == G_AND || t == G_OR || t == G_NOR || t == G_NA_AND; }
+struct Gate { u32 in0, in1, out, type; };
+struct Circuit {
+    u32 wireCount = 0;
+    std::vector<Gate> gates;
+    std::vector<u32> levelCounts;               // gates per communication level
+    std::vector<std::vector<u32>> inputs;       // input bundles (wire ids, LSB first)
+    std::vector<std::vector<u32>> outputs;      // output bundles
+};
+
+// Word layout of the engine memory: wire-major, `words` u64 per wire, rows
+// padded to a multiple of 2048 (Sh3BinaryEvaluator.cpp:84, mMem.reset(width, wires, 8)).
+inline u64 paddedWords(u64 rows) { return 32 * ((rows + 2047) / 2048); }
+
+// Evaluate `cir` on 3 parties. inputs[b] are the bundle sharings (64-bit
+// words, one column per 64 wires). Consumes 16 bytes of each party's prev and
+// next stream for the AND keys (Sh3BinaryEvaluator.h:96-102).
+std::vector<Shared> evalCircuit(std::array<Party, 3>& ev, const Circuit& cir,
+                                const std::vector<const Shared*>& inputs);
+
+// One communication level of one party (the kernel-level unit, roundCallback
+// Sh3BinaryEvaluator.cpp:539-1196). mem = [2][wires][words]; zFlat = z words of
+// every AND-type gate of the circuit, [andIndex][words]; sends = packed share-0
+// words of this level's AND-type outputs.
+void evalLevel(const Circuit& cir, u64 gateBegin, u64 gateCount, u64 andBegin, std::vector<u64>& mem,
+               u64 words, const std::vector<u64>& zFlat, std::vector<u64>& sendBuf);
+
+// --------------------------------------------------------------------------
+// Piecewise (Sh3Piecewise.cpp:184-567), MSB compare (BuildingBlocks.cpp:464-532)
+// --------------------------------------------------------------------------
+struct Coef { bool isInt; i64 i; double d; i64 fixed(u64 D) const; };
+struct Piecewise {
+    std::vector<Coef> thresholds;
+    std::vector<std::vector<Coef>> coefs;
+};
+// The circuit the reference builds with int_Sh3Piecewise_helper is supplied by
+// the caller (the product's circuit library); the oracle only evaluates it.
+Shared piecewiseEval(std::array<Party, 3>& ev, const Piecewise& pw, const Circuit& helper,
+                     const Shared& x, u64 D);
+
+// fetch_msb: x0+x2 reshare + MSB(a+b) circuit (BuildingBlocks.cpp:464-522)
+Shared fetchMsb(std::array<Party, 3>& ev, const Circuit& msbCir, const Shared& diff);
+
+// bool_not (BoolBasic.cpp:315-342): x1 is inverted
+Shared boolNot(const Shared& x);
+
+// Plain reference helpers
+i64 fixedMulPlain(i64 a, i64 b, u64 D);  // Sh3FixedPoint.cpp:8-20 (int128 divide)
+
+}  // namespace orc

@@ -1,0 +1,314 @@
+"""Kernel-level parity: every C-ABI entry point against the CPU oracle on the
+same seeded inputs, bit-exact (all arithmetic is integer)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle as orc
+from aby3_amd import native as nt
+
+pytestmark = pytest.mark.gpu
+
+U64 = 2**64
+
+
+_KEEP = []  # device tensors whose pointers were handed to a kernel stay alive
+
+
+@pytest.fixture(autouse=True)
+def _release():
+    yield
+    _KEEP.clear()
+
+
+def dev(a):
+    import torch
+
+    t = torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to("cuda")
+    _KEEP.append(t)
+    return t
+
+
+def empty(n):
+    import torch
+
+    return torch.zeros(n, dtype=torch.int64, device="cuda")
+
+
+def host(t):
+    import torch
+
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def P(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def rnd(seed, n):
+    return np.random.default_rng(seed).integers(-(2**63), 2**63 - 1, size=n, dtype=np.int64, endpoint=True)
+
+
+def k16(seed):
+    return bytes(np.random.default_rng(seed).integers(0, 256, size=16, dtype=np.uint8))
+
+
+@pytest.mark.parametrize("base,n", [(0, 1), (5, 1000), (2**40 + 3, 4097)])
+def test_aes_ctr(gpu, base, n):
+    key = k16(1)
+    out = empty(2 * n)
+    gpu.aes_ctr(nt.key16(key), base, n, P(out), None)
+    assert np.array_equal(host(out).view(np.uint64), orc.aes_ctr(key, base, n))
+
+
+@pytest.mark.parametrize("off,n", [(0, 8), (8, 24), (16, 1000), (40, 4096 * 8 + 8)])
+def test_prng_fill(gpu, off, n):
+    seed = k16(2)
+    out = empty(n // 8)
+    gpu.prng_fill(nt.key16(seed), off, n, P(out), None)
+    assert host(out).tobytes() == orc.prng_bytes(seed, off, n)
+
+
+@pytest.mark.parametrize("kind", [nt.DRAW_ARITH, nt.DRAW_BIN, nt.DRAW_RANDPAIR])
+@pytest.mark.parametrize("base,n", [(0, 1), (1, 2), (513, 5000)])
+def test_share_draws(gpu, kind, base, n):
+    kp, kn = k16(3), k16(4)
+    o0, o1 = empty(n), empty(n)
+    gpu.share_draws(kind, nt.key16(kp), nt.key16(kn), base, n, None, P(o0), P(o1), None)
+    r0, r1 = orc.share_draws(kind, kp, kn, base, n)
+    assert np.array_equal(host(o0), r0)
+    if kind == nt.DRAW_RANDPAIR:
+        assert np.array_equal(host(o1), r1)
+    if kind != nt.DRAW_RANDPAIR:
+        add = rnd(5, n)
+        gpu.share_draws(kind, nt.key16(kp), nt.key16(kn), base, n, P(dev(add)), P(o0), None, None)
+        exp = (r0.view(np.uint64) + add.view(np.uint64)) if kind == nt.DRAW_ARITH else (r0 ^ add).view(np.uint64)
+        assert np.array_equal(host(o0).view(np.uint64), exp)
+
+
+def _zs(kp, kn, base):
+    z = nt.ZeroShare()
+    z.k_prev[:] = kp
+    z.k_next[:] = kn
+    z.draw_base = base
+    return z
+
+
+def _mats(M, K, N, mode, seed):
+    A = rnd(seed, 2 * M * K)
+    B = rnd(seed + 1, 2 * (K * N if mode == nt.MUL_GEMM else M * K))
+    return A, B
+
+
+SHAPES = [(nt.MUL_HADAMARD, 128, 128, 128), (nt.MUL_HADAMARD, 7, 3, 3), (nt.MUL_GEMM, 10, 10, 10),
+          (nt.MUL_GEMM, 33, 17, 65), (nt.MUL_GEMM, 256, 128, 1), (nt.MUL_GEMM, 128, 256, 1),
+          (nt.MUL_GEMM, 192, 512, 320), (nt.MUL_GEMM, 1024, 1024, 1024)]
+
+
+@pytest.mark.parametrize("mode,M,K,N", SHAPES)
+@pytest.mark.parametrize("with_zs", [False, True])
+def test_mul_local(gpu, mode, M, K, N, with_zs):
+    if mode == nt.MUL_HADAMARD:
+        K = N
+    A, B = _mats(M, K, N, mode, 10 + M + K + N)
+    n = M * N
+    kb = K * N if mode == nt.MUL_GEMM else M * N
+    exp = orc.local_product(mode, A[:M * K], A[M * K:], B[:kb], B[kb:], M, K, N)
+    ws_bytes = gpu.dll.aby3g_mul_workspace_bytes(mode, M, K, N)
+    ws = empty(max(ws_bytes // 8, 1))
+    C0 = empty(n)
+    zs = None
+    if with_zs:
+        kp, kn = k16(6), k16(7)
+        zs = ctypes.byref(_zs(kp, kn, 77))
+        exp = (exp.view(np.uint64) + orc.share_draws(0, kp, kn, 77, n)[0].view(np.uint64)).view(np.int64)
+    gpu.mul_local(mode, P(dev(A)), P(dev(B)), P(C0), M, K, N, zs, P(ws), ws_bytes, None)
+    assert np.array_equal(host(C0), exp)
+
+
+def test_gemm_digit_extremes(gpu):
+    """Operands at the digit-carry corners: all-ones, 2^63, 0x7f/0x80 bytes."""
+    M = K = N = 64
+    vals = np.array([-1, -(2**63), 2**63 - 1, 0x7F7F7F7F7F7F7F7F, -0x7F7F7F7F7F7F7F80, 0x8080808080808080 - 2**64,
+                     1, 0], dtype=np.int64)
+    rng = np.random.default_rng(9)
+    A = vals[rng.integers(0, len(vals), 2 * M * K)]
+    B = vals[rng.integers(0, len(vals), 2 * K * N)]
+    exp = orc.local_product(nt.MUL_GEMM, A[:M * K], A[M * K:], B[:K * N], B[K * N:], M, K, N)
+    ws_bytes = gpu.dll.aby3g_mul_workspace_bytes(nt.MUL_GEMM, M, K, N)
+    ws = empty(ws_bytes // 8)
+    C0 = empty(M * N)
+    gpu.mul_local(nt.MUL_GEMM, P(dev(A)), P(dev(B)), P(C0), M, K, N, None, P(ws), ws_bytes, None)
+    assert np.array_equal(host(C0), exp)
+
+
+def _ts(ns, noff, ps, poff):
+    t = nt.TruncStreams()
+    t.next_seed[:] = ns
+    t.next_off = noff
+    t.prev_seed[:] = ps
+    t.prev_off = poff
+    return t
+
+
+@pytest.mark.parametrize("noff,poff", [(32, 32), (40, 32), (32, 48)])
+@pytest.mark.parametrize("d", [8, 16, 27])
+def test_trunc_tuple(gpu, noff, poff, d):
+    ns, ps = k16(11), k16(12)
+    n = 3001
+    R, RT = empty(n), empty(2 * n)
+    gpu.trunc_tuple(ctypes.byref(_ts(ns, noff, ps, poff)), n, d, P(R), P(RT), None)
+    eR, e0, e1 = orc.trunc_tuple(ns, noff, ps, poff, n, d)
+    rt = host(RT)
+    assert np.array_equal(host(R), eR)
+    assert np.array_equal(rt[:n], e0) and np.array_equal(rt[n:], e1)
+
+
+@pytest.mark.parametrize("mode,M,K,N", [SHAPES[0], SHAPES[3], SHAPES[4], SHAPES[7]])
+def test_mul_trunc_local(gpu, mode, M, K, N):
+    if mode == nt.MUL_HADAMARD:
+        K = N
+    d = 16
+    A, B = _mats(M, K, N, mode, 20 + M)
+    n = M * N
+    kb = K * N if mode == nt.MUL_GEMM else M * N
+    prod = orc.local_product(mode, A[:M * K], A[M * K:], B[:kb], B[kb:], M, K, N)
+    ns, ps = k16(13), k16(14)
+    eR, e0, e1 = orc.trunc_tuple(ns, 32, ps, 40, n, d)
+    ws_bytes = gpu.dll.aby3g_mul_workspace_bytes(mode, M, K, N)
+    ws = empty(max(ws_bytes // 8, 1))
+    z, C = empty(n), empty(2 * n)
+    gpu.mul_trunc_local(mode, P(dev(A)), P(dev(B)), M, K, N, d, ctypes.byref(_ts(ns, 32, ps, 40)), P(z), P(C), P(ws),
+                        ws_bytes, None)
+    assert np.array_equal(host(z), (prod.view(np.uint64) - eR.view(np.uint64)).view(np.int64))
+    c = host(C)
+    assert np.array_equal(c[:n], e0) and np.array_equal(c[n:], e1)
+
+
+@pytest.mark.parametrize("party", [0, 1, 2])
+def test_trunc_finalize(gpu, party):
+    n, d = 999, 13
+    za, zb, zo, C = rnd(1, n), rnd(2, n), rnd(3, n), rnd(4, 2 * n)
+    Cd = dev(C)
+    gpu.trunc_finalize(party, P(dev(za)), P(dev(zb)), P(dev(zo)), d, P(Cd), n, None)
+    s = (za.view(np.uint64) + zb.view(np.uint64) + zo.view(np.uint64)).view(np.int64) >> d
+    exp = C.copy()
+    if party < 2:
+        exp[party * n:(party + 1) * n] = (exp[party * n:(party + 1) * n].view(np.uint64) + s.view(np.uint64)).view(
+            np.int64)
+    assert np.array_equal(host(Cd), exp)
+
+
+def _bits_ref(x, nbits, words):
+    rows = x.shape[0]
+    out = np.zeros((nbits, words), dtype=np.uint64)
+    xu = x.view(np.uint64)
+    for b in range(nbits):
+        col = (xu[:, b // 64] >> np.uint64(b % 64)) & np.uint64(1)
+        for r in np.nonzero(col)[0]:
+            out[b, r // 64] |= np.uint64(1) << np.uint64(r % 64)
+    return out
+
+
+@pytest.mark.parametrize("rows,nbits", [(1, 1), (100, 64), (2048, 64), (3000, 70)])
+def test_transposes(gpu, rows, nbits):
+    cols = (nbits + 63) // 64
+    x = rnd(rows + nbits, rows * cols).reshape(rows, cols)
+    if nbits % 64:
+        x[:, -1] &= np.int64((1 << (nbits % 64)) - 1)
+    words = 32 * ((rows + 2047) // 2048)
+    W = empty(nbits * words)
+    gpu.bits_to_wires(P(dev(x)), rows, cols, nbits, P(W), words, None)
+    w = host(W).view(np.uint64).reshape(nbits, words)
+    assert np.array_equal(w, _bits_ref(x, nbits, words))
+    import torch
+
+    wires = torch.arange(nbits, dtype=torch.int32, device="cuda")
+    out = empty(rows * cols)
+    gpu.wires_to_bits(P(W), P(wires), nbits, words, P(out), rows, None)
+    assert np.array_equal(host(out).reshape(rows, cols), x)
+
+
+def _gate_ref(t, x0, x1, y0, y1, z):
+    if t == 0:
+        return x0 ^ y0, x1 ^ y1
+    if t == 1:
+        return ~(x0 ^ y0), ~(x1 ^ y1)
+    if t == 6:
+        return x0, x1
+    if t == 7:
+        return ~x0, ~x1
+    if t == 2:
+        r = (x0 & y0) ^ (x0 & y1) ^ (x1 & y0)
+    elif t == 3:
+        r = (x0 & y0) ^ (x0 & y1) ^ (x1 & y0) ^ x0 ^ y0
+    elif t == 4:
+        r = (~x0 & ~y0) ^ (~x0 & ~y1) ^ (~x1 & ~y0)
+    else:
+        r = (~x0 & y0) ^ (~x0 & y1) ^ (~x1 & y0)
+    return r ^ z, None
+
+
+def test_bin_gates_and_unpack(gpu):
+    import torch
+
+    wires, words = 40, 64
+    rng = np.random.default_rng(3)
+    mem = rng.integers(0, 2**64, size=2 * wires * words, dtype=np.uint64)
+    z = rng.integers(0, 2**64, size=4 * words, dtype=np.uint64)
+    gates = [(0, 1, 20, 0), (2, 3, 21, 1), (4, 5, 22, 2), (6, 7, 23, 3), (8, 9, 24, 4), (10, 11, 25, 5),
+             (12, 0, 26, 6), (13, 0, 27, 7)]
+    arr = (nt.Gate * len(gates))()
+    zrow = 0
+    for i, (a, b, o, t) in enumerate(gates):
+        arr[i].in0, arr[i].in1, arr[i].out, arr[i].type = a, b, o, t
+        if t in (2, 3, 4, 5):
+            arr[i].z_row = arr[i].send_row = zrow
+            zrow += 1
+    gdev = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to("cuda")
+    memd = dev(mem.view(np.int64))
+    send = empty(4 * words)
+    gpu.bin_gates(P(gdev), len(gates), P(memd), wires, words, P(dev(z.view(np.int64))), P(send), None)
+    out = host(memd).view(np.uint64).reshape(2, wires, words)
+    snd = host(send).view(np.uint64).reshape(4, words)
+    m = mem.reshape(2, wires, words)
+    zr = 0
+    for a, b, o, t in gates:
+        r0, r1 = _gate_ref(t, m[0, a], m[1, a], m[0, b], m[1, b], z.reshape(4, words)[zr] if t in (2, 3, 4, 5) else 0)
+        assert np.array_equal(out[0, o], r0), t
+        if r1 is not None:
+            assert np.array_equal(out[1, o], r1), t
+        else:
+            assert np.array_equal(snd[zr], r0)
+            zr += 1
+    # unpack: share-1 rows of the AND outputs <- a received buffer
+    recv = rng.integers(0, 2**64, size=4 * words, dtype=np.uint64)
+    outw = torch.tensor([22, 23, 24, 25], dtype=torch.int32, device="cuda")
+    gpu.bin_unpack(P(dev(recv.view(np.int64))), P(outw), 4, P(memd), wires, words, None)
+    out = host(memd).view(np.uint64).reshape(2, wires, words)
+    assert np.array_equal(out[1, 22:26], recv.reshape(4, words))
+
+
+def test_lincomb_bitops(gpu):
+    import torch
+
+    n = 1000
+    a, b = rnd(1, n), rnd(2, n)
+    o = empty(n)
+    gpu.i64_lincomb(n, 3, P(dev(a)), -5, P(dev(b)), 7, P(o), None)
+    exp = (np.uint64(3) * a.view(np.uint64) + np.uint64(2**64 - 5) * b.view(np.uint64) + np.uint64(7)).view(np.int64)
+    assert np.array_equal(host(o), exp)
+    for op, f in [(0, lambda x, y: x ^ y), (1, lambda x, y: x & y), (2, lambda x, y: ~x),
+                  (3, lambda x, y: -(x & 1)), (4, lambda x, y: x)]:
+        gpu.u64_bitop(op, n, P(dev(a)), P(dev(b)), P(o), None)
+        assert np.array_equal(host(o), f(a, b)), op
+    idx = np.random.default_rng(4).permutation(n).astype(np.int32)
+    idxd = torch.from_numpy(idx).to("cuda")
+    gpu.u64_gather(n, P(idxd), P(dev(a)), P(o), None)
+    assert np.array_equal(host(o), a[idx])
+    gpu.u64_scatter(n, P(idxd), P(dev(a)), P(o), None)
+    exp = np.zeros(n, dtype=np.int64)
+    exp[idx] = a
+    assert np.array_equal(host(o), exp)

@@ -225,6 +225,21 @@ int aby3g_event_elapsed_ms(aby3g_event start, aby3g_event end, float* ms) {
     return guarded([&] { ABY3G_CHECK_HIP(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)end)); });
 }
 
+int aby3g_aes_block_host(const uint8_t key[16], uint64_t ctr, uint8_t out[16]) {
+    return guarded([&] {
+        static std::vector<u32> rep = [] {
+            std::vector<u32> r(kAesLdsWords);
+            for (int i = 0; i < kAesLdsWords; ++i) r[i] = tables().T0[i >> 5];
+            return r;
+        }();
+        AesKey k = expand_key(key);
+        u64 lo, hi;
+        aes_ctr_block(rep.data(), 0, k, ctr, lo, hi);
+        std::memcpy(out, &lo, 8);
+        std::memcpy(out + 8, &hi, 8);
+    });
+}
+
 int aby3g_probe_enable(int on) {
     return guarded([&] {
         if (!on) t_probe.drain();

@@ -1,0 +1,238 @@
+#include "Basic.h"
+#include <cmath>
+
+namespace aby3 {
+
+CircuitLibrary& basicLibrary() {
+    thread_local CircuitLibrary lib;
+    return lib;
+}
+
+void evalCircuit(BetaCircuit* cir, const std::vector<const sbMatrix*>& in, const std::vector<sbMatrix*>& out,
+                 Sh3Evaluator& eval, Sh3Runtime& runtime) {
+    Sh3BinaryEvaluator binEng;
+    binEng.setCir(cir, in[0]->rows(), eval.mShareGen);
+    for (size_t i = 0; i < in.size(); ++i) binEng.setInput(i, *in[i]);
+    binEng.asyncEvaluate(runtime.noDependencies())
+        .then([&](Sh3Task&) {
+            for (size_t i = 0; i < out.size(); ++i) binEng.getOutput(i, *out[i]);
+        })
+        .get();
+}
+
+// Binary two-input sharing of an arithmetic value: c0 = (sign * (x0 + x2), 0, 0)
+// reshared by P0, c1 = (0, x1, 0) (BuildingBlocks.cpp:475-502, :709-735).
+static void arithToTwoBin(int pIdx, const si64Matrix& x, i64 sign, sbMatrix& c0, sbMatrix& c1, Sh3Runtime& rt) {
+    Gpu& g = rt.gpu();
+    const u64 n = x.size(), b8 = n * sizeof(i64);
+    c0.resize(n, 64);
+    c1.resize(n, 64);
+    c1.setZero();
+    if (pIdx == 0)
+        GPU_CALL(aby3g_i64_lincomb(n, sign, x.share(0), sign, x.share(1), 0, c0.share(0), g.stream()));
+    else
+        GPU_CALL(aby3g_memset(c0.share(0), 0, b8, g.stream()));
+    if (pIdx == 1) d2d(c1.share(0), x.share(0), b8, g);
+    if (pIdx == 2) d2d(c1.share(1), x.share(1), b8, g);
+    rt.mComm.mNext.asyncSendDevice(c0.share(0), b8, g);
+    rt.mComm.mPrev.asyncRecvDevice(c0.share(1), b8, g).get();
+}
+
+int fetch_msb(int pIdx, const si64Matrix& diffAB, sbMatrix& res, Sh3Evaluator& eval, Sh3Runtime& runtime) {
+    sbMatrix c0, c1;
+    arithToTwoBin(pIdx, diffAB, 1, c0, c1, runtime);
+    evalCircuit(basicLibrary().int_comp_helper(64), {&c0, &c1}, {&res}, eval, runtime);
+    return 0;
+}
+
+static void sub(const si64Matrix& a, const si64Matrix& b, si64Matrix& out, Gpu& g) {
+    if (a.rows() != b.rows() || a.cols() != b.cols()) throw std::runtime_error("shape mismatch " LOCATION);
+    out.resize(a.rows(), a.cols());
+    GPU_CALL(aby3g_i64_lincomb(2 * a.size(), 1, a.data(), -1, b.data(), 0, out.data(), g.stream()));
+}
+
+int cipher_gt(int pIdx, const si64Matrix& A, const si64Matrix& B, sbMatrix& res, Sh3Evaluator& eval,
+              Sh3Runtime& runtime) {
+    si64Matrix diff;
+    sub(B, A, diff, runtime.gpu());
+    return fetch_msb(pIdx, diff, res, eval, runtime);
+}
+
+int cipher_ge(int pIdx, const si64Matrix& A, const si64Matrix& B, sbMatrix& res, Sh3Evaluator& eval,
+              Sh3Runtime& runtime) {
+    si64Matrix diff;
+    sub(A, B, diff, runtime.gpu());
+    fetch_msb(pIdx, diff, res, eval, runtime);
+    // flip bit 0 of both shares of every party: all three shares flip
+    Gpu& g = runtime.gpu();
+    DeviceBuffer ones(g, res.size() * 2 * 8);
+    std::vector<i64> h(res.size() * 2, 1);
+    toDevice(ones.data(), h.data(), h.size() * 8, g);
+    GPU_CALL(aby3g_u64_bitop(0, 2 * res.size(), (const u64*)res.data(), ones.as<u64>(), (u64*)res.data(), g.stream()));
+    return 0;
+}
+
+int circuit_cipher_eq(int pIdx, const si64Matrix& A, const si64Matrix& B, sbMatrix& res, Sh3Evaluator& eval,
+                      Sh3Runtime& runtime) {
+    si64Matrix diff;
+    sub(A, B, diff, runtime.gpu());
+    sbMatrix c0, c1;
+    arithToTwoBin(pIdx, diff, -1, c0, c1, runtime);
+    evalCircuit(basicLibrary().int_eq(64), {&c0, &c1}, {&res}, eval, runtime);
+    return 0;
+}
+
+int cipher_mul(int, const si64Matrix& A, const si64Matrix& B, si64Matrix& res, Sh3Evaluator& eval,
+               Sh3Runtime& runtime) {
+    eval.asyncMul(runtime, A, B, res, MulMode::Hadamard).get();
+    return 0;
+}
+
+int cipher_mul(int, const si64Matrix& A, const sbMatrix& B, si64Matrix& res, Sh3Evaluator& eval,
+               Sh3Runtime& runtime) {
+    eval.asyncMul(runtime, A, B, res).get();
+    return 0;
+}
+
+void bool_cipher_lt(int, const sbMatrix& A, const sbMatrix& B, sbMatrix& res, Sh3Evaluator& eval,
+                    Sh3Runtime& runtime) {
+    evalCircuit(basicLibrary().int_int_lt(A.bitCount()), {&A, &B}, {&res}, eval, runtime);
+}
+void bool_cipher_eq(int, const sbMatrix& A, const sbMatrix& B, sbMatrix& res, Sh3Evaluator& eval,
+                    Sh3Runtime& runtime) {
+    evalCircuit(basicLibrary().int_eq(A.bitCount()), {&A, &B}, {&res}, eval, runtime);
+}
+void bool_cipher_and(int, const sbMatrix& A, const sbMatrix& B, sbMatrix& res, Sh3Evaluator& eval,
+                     Sh3Runtime& runtime) {
+    evalCircuit(basicLibrary().int_int_bitwiseAnd(A.bitCount()), {&A, &B}, {&res}, eval, runtime);
+}
+void bool_cipher_or(int, const sbMatrix& A, const sbMatrix& B, sbMatrix& res, Sh3Evaluator& eval,
+                    Sh3Runtime& runtime) {
+    evalCircuit(basicLibrary().int_int_bitwiseOr(A.bitCount()), {&A, &B}, {&res}, eval, runtime);
+}
+void bool_cipher_add(int, const sbMatrix& A, const sbMatrix& B, sbMatrix& res, Sh3Evaluator& eval,
+                     Sh3Runtime& runtime) {
+    evalCircuit(basicLibrary().int_int_add(A.bitCount()), {&A, &B}, {&res}, eval, runtime);
+}
+void bool_cipher_sub(int, const sbMatrix& A, const sbMatrix& B, sbMatrix& res, Sh3Evaluator& eval,
+                     Sh3Runtime& runtime) {
+    evalCircuit(basicLibrary().int_int_sub(A.bitCount()), {&A, &B}, {&res}, eval, runtime);
+}
+
+void bool_cipher_not(int pIdx, const sbMatrix& A, sbMatrix& res) {
+    Gpu& g = A.gpu();
+    const u64 n = A.size();
+    if (&res != &A) {
+        res.resize(A.rows(), A.bitCount());
+        d2d(res.data(), A.data(), 2 * n * 8, g);
+    }
+    if (pIdx == 1) GPU_CALL(aby3g_u64_bitop(2, n, (const u64*)res.share(0), nullptr, (u64*)res.share(0), g.stream()));
+    if (pIdx == 2) GPU_CALL(aby3g_u64_bitop(2, n, (const u64*)res.share(1), nullptr, (u64*)res.share(1), g.stream()));
+}
+
+void bool_cipher_max_min_split(int, const sbMatrix& A, const sbMatrix& B, sbMatrix& resMax, sbMatrix& resMin,
+                               Sh3Evaluator& eval, Sh3Runtime& runtime) {
+    evalCircuit(basicLibrary().cmp_swap(A.bitCount()), {&A, &B}, {&resMin, &resMax}, eval, runtime);
+}
+void bool_cipher_max(int pIdx, const sbMatrix& A, const sbMatrix& B, sbMatrix& res, Sh3Evaluator& eval,
+                     Sh3Runtime& runtime) {
+    sbMatrix mn;
+    bool_cipher_max_min_split(pIdx, A, B, res, mn, eval, runtime);
+}
+void bool_cipher_min(int pIdx, const sbMatrix& A, const sbMatrix& B, sbMatrix& res, Sh3Evaluator& eval,
+                     Sh3Runtime& runtime) {
+    sbMatrix mx;
+    bool_cipher_max_min_split(pIdx, A, B, mx, res, eval, runtime);
+}
+
+// gather rows idx of a 64-bit sbMatrix (both shares)
+static void gatherRows(const sbMatrix& src, const std::vector<u32>& idx, sbMatrix& dst, Gpu& g) {
+    const u64 n = idx.size(), R = src.rows();
+    dst.resize(n, 64);
+    DeviceBuffer di(g, n * 4);
+    toDevice(di.data(), idx.data(), n * 4, g);
+    for (int s = 0; s < 2; ++s)
+        GPU_CALL(aby3g_u64_gather(n, di.as<u32>(), (const u64*)src.share(s), (u64*)dst.share(s), g.stream()));
+    (void)R;
+}
+static void scatterRows(const sbMatrix& src, const std::vector<u32>& idx, sbMatrix& dst, Gpu& g) {
+    const u64 n = idx.size();
+    DeviceBuffer di(g, n * 4);
+    toDevice(di.data(), idx.data(), n * 4, g);
+    for (int s = 0; s < 2; ++s)
+        GPU_CALL(aby3g_u64_scatter(n, di.as<u32>(), (const u64*)src.share(s), (u64*)dst.share(s), g.stream()));
+}
+
+int odd_even_merge(const sbMatrix& data1, const sbMatrix& data2, sbMatrix& res, int pIdx, Sh3Evaluator& eval,
+                   Sh3Runtime& runtime) {
+    // Sort.cpp:327-406
+    Gpu& g = runtime.gpu();
+    const u64 L1 = data1.rows(), L2 = data2.rows(), length = std::max(L1, L2);
+    if (data1.bitCount() != 64 || data2.bitCount() != 64) throw std::runtime_error("64-bit keys expected");
+    // pad with max(last1, last2)
+    std::vector<u32> i1{(u32)(L1 - 1)}, i2{(u32)(L2 - 1)};
+    sbMatrix max1, max2, maxEle;
+    gatherRows(data1, i1, max1, g);
+    gatherRows(data2, i2, max2, g);
+    bool_cipher_max(pIdx, max1, max2, maxEle, eval, runtime);
+    sbMatrix result(2 * length, 64);
+    {
+        std::vector<u32> zeros(2 * length, 0);
+        gatherRows(maxEle, zeros, result, g);
+        std::vector<u32> even(L1), odd(L2);
+        for (u64 i = 0; i < L1; ++i) even[i] = (u32)(2 * i);
+        for (u64 i = 0; i < L2; ++i) odd[i] = (u32)(2 * i + 1);
+        scatterRows(data1, even, result, g);
+        scatterRows(data2, odd, result, g);
+    }
+    size_t t = (size_t)std::ceil(std::log2((double)length) + 1);
+    size_t q = (size_t)1 << (t - 1);
+    size_t d = 1, r = 0;
+    while (d > 0) {
+        std::vector<u32> xm, ym;
+        for (size_t i = r; i + d < 2 * length; i += 2) {
+            xm.push_back((u32)i);
+            ym.push_back((u32)(i + d));
+        }
+        if (!xm.empty()) {
+            sbMatrix X, Y, mx, mn;
+            gatherRows(result, xm, X, g);
+            gatherRows(result, ym, Y, g);
+            bool_cipher_max_min_split(pIdx, X, Y, mx, mn, eval, runtime);
+            scatterRows(mn, xm, result, g);
+            scatterRows(mx, ym, result, g);
+        }
+        d = q - 1;
+        q >>= 1;
+        r = 1;
+    }
+    std::vector<u32> head(L1 + L2);
+    for (u64 i = 0; i < L1 + L2; ++i) head[i] = (u32)i;
+    gatherRows(result, head, res, g);
+    return 0;
+}
+
+int odd_even_multi_merge(std::vector<sbMatrix>& data, sbMatrix& sorted, int pIdx, Sh3Evaluator& eval,
+                         Sh3Runtime& runtime) {
+    // Sort.cpp:413-437
+    size_t k = data.size();
+    while (k != 1) {
+        if (k % 2) {
+            sbMatrix res;
+            odd_even_merge(data[k - 2], data[k - 1], res, pIdx, eval, runtime);
+            data[k - 2] = std::move(res);
+            k -= 1;
+        } else {
+            for (size_t i = 0; i < k; i += 2) {
+                sbMatrix res;
+                odd_even_merge(data[i], data[i + 1], res, pIdx, eval, runtime);
+                data[i / 2] = std::move(res);
+            }
+            k >>= 1;
+        }
+    }
+    sorted = std::move(data[0]);
+    return 0;
+}
+
+}  // namespace aby3

@@ -1,0 +1,180 @@
+#include "Channel.h"
+#include <map>
+
+namespace aby3 {
+
+namespace {
+struct Slot {
+    void* ptr = nullptr;
+    size_t cap = 0;
+    int device = -1;
+    std::unique_ptr<Event> ready;     // recorded on the sender's stream
+    std::unique_ptr<Event> consumed;  // recorded on the receiver's stream
+    bool busy = false;
+    bool consumedRecorded = false;
+};
+struct Msg {
+    bool device = false;
+    std::vector<u8> host;
+    Slot* slot = nullptr;
+    size_t bytes = 0;
+};
+}  // namespace
+
+struct Pipe {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::map<u64, Msg> msgs;
+    u64 sendSeq = 0, recvTicket = 0;
+    std::vector<std::unique_ptr<Slot>> slots;
+    u64 sent = 0, received = 0;
+
+    ~Pipe() {
+        for (auto& s : slots)
+            if (s->ptr) {
+                aby3g_set_device(s->device);
+                aby3g_device_sync();
+                aby3g_free(s->ptr);
+            }
+    }
+
+    void push(Msg&& m) {
+        std::lock_guard<std::mutex> lk(mu);
+        sent += m.bytes;
+        msgs.emplace(sendSeq++, std::move(m));
+        cv.notify_all();
+    }
+    Msg pop(u64 ticket) {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return msgs.count(ticket) != 0; });
+        Msg m = std::move(msgs[ticket]);
+        msgs.erase(ticket);
+        received += m.bytes;
+        return m;
+    }
+    Slot* acquire(size_t bytes, int device) {
+        std::lock_guard<std::mutex> lk(mu);
+        for (auto& s : slots)
+            if (!s->busy && s->cap >= bytes && s->device == device) {
+                s->busy = true;
+                return s.get();
+            }
+        auto s = std::make_unique<Slot>();
+        s->cap = bytes < 4096 ? 4096 : bytes;
+        s->device = device;
+        GPU_CALL(aby3g_malloc(&s->ptr, s->cap));
+        s->ready = std::make_unique<Event>();
+        s->busy = true;
+        slots.push_back(std::move(s));
+        return slots.back().get();
+    }
+    void releaseSlot(Slot* s) {
+        std::lock_guard<std::mutex> lk(mu);
+        s->busy = false;
+    }
+};
+
+struct RecvFuture::State {
+    std::shared_ptr<Pipe> pipe;
+    u64 ticket = 0;
+    void* dst = nullptr;
+    size_t bytes = 0;
+    Gpu* gpu = nullptr;  // null: host payload
+    bool done = false;
+    std::mutex mu;
+};
+
+void RecvFuture::get() const {
+    if (!mState) throw std::runtime_error("RecvFuture::get on an empty future");
+    State& st = *mState;
+    std::lock_guard<std::mutex> lk(st.mu);
+    if (st.done) return;
+    Msg m = st.pipe->pop(st.ticket);
+    if (m.bytes != st.bytes)
+        throw std::runtime_error("channel: message size mismatch (expected " + std::to_string(st.bytes) + ", got " +
+                                 std::to_string(m.bytes) + ")");
+    if (!st.gpu) {
+        if (m.device) throw std::runtime_error("channel: device payload received into a host buffer");
+        if (st.bytes) std::memcpy(st.dst, m.host.data(), st.bytes);
+    } else {
+        if (!m.device) throw std::runtime_error("channel: host payload received into a device buffer");
+        Slot* s = m.slot;
+        Gpu& g = *st.gpu;
+        GPU_CALL(aby3g_set_device(g.device()));
+        if (st.bytes) {
+            GPU_CALL(aby3g_stream_wait_event(g.stream(), s->ready->get()));
+            GPU_CALL(aby3g_memcpy(st.dst, s->ptr, st.bytes, 3, g.stream()));
+        }
+        if (!s->consumed) s->consumed = std::make_unique<Event>();
+        s->consumed->record(g.stream());
+        s->consumedRecorded = true;
+        st.pipe->releaseSlot(s);
+    }
+    st.done = true;
+}
+
+void Channel::asyncSendCopy(const void* data, size_t bytes) {
+    if (!mOut) throw std::runtime_error("channel not connected");
+    Msg m;
+    m.bytes = bytes;
+    m.host.assign((const u8*)data, (const u8*)data + bytes);
+    mOut->push(std::move(m));
+}
+
+RecvFuture Channel::asyncRecv(void* dst, size_t bytes) {
+    if (!mIn) throw std::runtime_error("channel not connected");
+    RecvFuture f;
+    f.mState = std::make_shared<RecvFuture::State>();
+    f.mState->pipe = mIn;
+    f.mState->dst = dst;
+    f.mState->bytes = bytes;
+    {
+        std::lock_guard<std::mutex> lk(mIn->mu);
+        f.mState->ticket = mIn->recvTicket++;
+    }
+    return f;
+}
+
+void Channel::asyncSendDevice(const void* src, size_t bytes, Gpu& gpu) {
+    if (!mOut) throw std::runtime_error("channel not connected");
+    GPU_CALL(aby3g_set_device(gpu.device()));
+    Slot* s = mOut->acquire(bytes, gpu.device());
+    if (s->consumedRecorded) GPU_CALL(aby3g_stream_wait_event(gpu.stream(), s->consumed->get()));
+    if (bytes) GPU_CALL(aby3g_memcpy(s->ptr, src, bytes, 3, gpu.stream()));
+    s->ready->record(gpu.stream());
+    Msg m;
+    m.device = true;
+    m.slot = s;
+    m.bytes = bytes;
+    mOut->push(std::move(m));
+}
+
+RecvFuture Channel::asyncRecvDevice(void* dst, size_t bytes, Gpu& gpu) {
+    RecvFuture f = asyncRecv(dst, bytes);
+    f.mState->gpu = &gpu;
+    return f;
+}
+
+u64 Channel::bytesSent() const { return mOut ? mOut->sent : 0; }
+u64 Channel::bytesRecv() const { return mIn ? mIn->received : 0; }
+void Channel::resetStats() {
+    if (mOut) mOut->sent = 0;
+    if (mIn) mIn->received = 0;
+}
+
+std::vector<CommPkg> makeLocalRing() {
+    // pipe[i][j]: messages from party i to party j
+    std::shared_ptr<Pipe> p[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            if (i != j) p[i][j] = std::make_shared<Pipe>();
+    std::vector<CommPkg> c(3);
+    for (int i = 0; i < 3; ++i) {
+        int nx = (i + 1) % 3, pv = (i + 2) % 3;
+        c[i].mNext = Channel(p[i][nx], p[nx][i]);
+        c[i].mPrev = Channel(p[i][pv], p[pv][i]);
+    }
+    return c;
+}
+
+}  // namespace aby3

@@ -1,0 +1,81 @@
+// Ordered point-to-point message channels between parties (the role of
+// cryptoTools' oc::Channel in the reference; CommPkg = {mPrev, mNext},
+// aby3/sh3/Sh3Types.h:32-34).
+//
+// Semantics kept from the reference:
+//   * FIFO per direction, untyped on the wire: the receiver must post its
+//     receives in the order the sender sent (sizes are checked);
+//   * asyncSendCopy copies the payload at send time;
+//   * asyncRecv returns a future; the payload is usable after get().
+// Device payloads never touch the host: the sender copies into a staging slot
+// on its own stream and records an event; the receiver's get() makes its
+// stream wait for that event and copies the slot into the destination (peer
+// copy over xGMI when the parties sit on different GPUs). Every enqueue on a
+// party's stream is issued by that party's thread, so stream order equals the
+// protocol order.
+#pragma once
+#include "Device.h"
+#include <condition_variable>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+namespace aby3 {
+
+struct Pipe;  // one direction
+
+class RecvFuture {
+public:
+    RecvFuture() = default;
+    // Waits for the message and makes its payload available at the
+    // destination (device payload: ordered on the receiver's stream).
+    void get() const;
+    bool valid() const { return (bool)mState; }
+
+    struct State;
+    std::shared_ptr<State> mState;
+};
+
+class Channel {
+public:
+    Channel() = default;
+    Channel(std::shared_ptr<Pipe> out, std::shared_ptr<Pipe> in) : mOut(std::move(out)), mIn(std::move(in)) {}
+
+    // host payloads
+    void asyncSendCopy(const void* data, size_t bytes);
+    template <class T>
+    void asyncSendCopy(const T& v) {
+        asyncSendCopy(&v, sizeof(T));
+    }
+    void send(const void* data, size_t bytes) { asyncSendCopy(data, bytes); }
+    RecvFuture asyncRecv(void* dst, size_t bytes);
+    void recv(void* dst, size_t bytes) { asyncRecv(dst, bytes).get(); }
+    template <class T>
+    void recv(T& v) {
+        recv(&v, sizeof(T));
+    }
+
+    // device payloads, enqueued on / delivered to `gpu`'s stream
+    void asyncSendDevice(const void* src, size_t bytes, Gpu& gpu);
+    RecvFuture asyncRecvDevice(void* dst, size_t bytes, Gpu& gpu);
+
+    u64 bytesSent() const;
+    u64 bytesRecv() const;
+    void resetStats();
+
+    bool connected() const { return mOut && mIn; }
+
+private:
+    std::shared_ptr<Pipe> mOut, mIn;
+};
+
+struct CommPkg {
+    Channel mPrev, mNext;
+};
+
+// Three in-process parties connected in a ring: result[i].mNext talks to
+// party i+1, result[i].mPrev to party i-1.
+std::vector<CommPkg> makeLocalRing();
+
+}  // namespace aby3

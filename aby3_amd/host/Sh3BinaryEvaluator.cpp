@@ -1,0 +1,164 @@
+#include "Sh3BinaryEvaluator.h"
+
+namespace aby3 {
+
+void Sh3BinaryEvaluator::setCir(BetaCircuit* cir, u64 width, Sh3ShareGen& gen) {
+    block p = gen.getPrevBlock();
+    block n = gen.getNextBlock();
+    setCir(cir, width, p, n);
+}
+
+void Sh3BinaryEvaluator::upload(Gpu& g) {
+    auto it = mDev.find(mCir);
+    if (it != mDev.end() && it->second->gates.gpu() == &g) {
+        mCur = it->second.get();
+        return;
+    }
+    auto d = std::make_unique<DevCircuit>();
+    const BetaCircuit& c = *mCir;
+    std::vector<aby3g_gate> gs(c.mBatchGates.size());
+    for (size_t i = 0; i < gs.size(); ++i) {
+        const BetaGate& b = c.mBatchGates[i];
+        gs[i] = aby3g_gate{b.in0, b.in1, b.out, (u32)b.type, c.mBatchZRow[i], c.mBatchSendRow[i]};
+    }
+    if (!gs.empty()) {
+        d->gates.reset(g, gs.size() * sizeof(aby3g_gate));
+        toDevice(d->gates.data(), gs.data(), gs.size() * sizeof(aby3g_gate), g);
+    }
+    // per level, the AND outputs in level-list order = send/recv row order
+    size_t gi = 0;
+    d->hostOutWires.resize(c.mLevelCounts.size());
+    d->outWires.resize(c.mLevelCounts.size());
+    for (size_t L = 0; L < c.mLevelCounts.size(); ++L) {
+        for (u32 k = 0; k < c.mLevelCounts[L]; ++k, ++gi)
+            if (isAndType(c.mLevelGates[gi].type)) d->hostOutWires[L].push_back(c.mLevelGates[gi].out);
+        auto& v = d->hostOutWires[L];
+        if (!v.empty()) {
+            d->outWires[L].reset(g, v.size() * 4);
+            toDevice(d->outWires[L].data(), v.data(), v.size() * 4, g);
+        }
+    }
+    std::vector<u32> all;
+    for (auto& o : c.mOutputs) {
+        d->outputOffsets.push_back((u32)all.size());
+        all.insert(all.end(), o.begin(), o.end());
+    }
+    if (!all.empty()) {
+        d->allOutputWires.reset(g, all.size() * 4);
+        toDevice(d->allOutputWires.data(), all.data(), all.size() * 4, g);
+    }
+    mCur = d.get();
+    mDev[mCir] = std::move(d);
+}
+
+void Sh3BinaryEvaluator::setCir(BetaCircuit* cir, u64 width, block prevSeed, block nextSeed) {
+    if (!cir->levelized()) cir->levelByAndDepth();
+    mCir = cir;
+    mRows = width;
+    mWords = 32 * ((width + 2047) / 2048);
+    mLevel = 0;
+    mKeyPrev = prevSeed;
+    mKeyNext = nextSeed;
+    Gpu& g = Gpu::current();
+    mGpu = &g;
+    upload(g);
+    const u64 memBytes = 2 * (u64)cir->mWireCount * mWords * 8;
+    if (mMem.bytes() < memBytes || mMem.gpu() != &g) mMem.reset(g, memBytes ? memBytes : 8);
+    // all AND masks of the circuit: z[k][w] = binary draw k*words + w
+    const u64 zWords = (u64)cir->mAndCount * mWords;
+    if (zWords) {
+        if (mZ.bytes() < zWords * 8 || mZ.gpu() != &g) mZ.reset(g, zWords * 8);
+        GPU_CALL(aby3g_share_draws(ABY3G_DRAW_BIN, mKeyPrev.data(), mKeyNext.data(), 0, zWords, nullptr,
+                                   mZ.as<i64>(), nullptr, g.stream()));
+    }
+    u32 maxAnds = 0;
+    for (u32 a : cir->mLevelAndCounts) maxAnds = std::max(maxAnds, a);
+    const u64 sb = (u64)maxAnds * mWords * 8;
+    for (auto& s : mSend)
+        if (s.bytes() < sb || s.gpu() != &g) s.reset(g, sb ? sb : 8);
+    if (mRecv.bytes() < sb || mRecv.gpu() != &g) mRecv.reset(g, sb ? sb : 8);
+}
+
+void Sh3BinaryEvaluator::setInput(u64 i, const sbMatrix& in) {
+    if (!mCir) throw RTE_LOC;
+    if (i >= mCir->mInputs.size()) throw std::invalid_argument("input index out of bounds");
+    const auto& wires = mCir->mInputs[i];
+    if (in.bitCount() != wires.size()) throw std::invalid_argument("input data wrong size");
+    if (in.rows() != mRows) throw std::invalid_argument("incorrect number of rows");
+    for (size_t k = 1; k < wires.size(); ++k)
+        if (wires[k] != wires[k - 1] + 1) throw std::runtime_error("expecting contiguous input wires. " LOCATION);
+    Gpu& g = *mGpu;
+    const u64 W = mCir->mWireCount;
+    for (int s = 0; s < 2; ++s)
+        GPU_CALL(aby3g_bits_to_wires(in.share(s), mRows, in.i64Cols(), (u32)wires.size(),
+                                     mMem.as<u64>() + ((u64)s * W + wires[0]) * mWords, mWords, g.stream()));
+    mLevel = 0;
+}
+
+void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
+    if (mLevel > mCir->mLevelCounts.size())
+        throw std::runtime_error("evaluateRound() was called but no rounds remain... " LOCATION);
+    Gpu& g = task.getRuntime().gpu();
+    const u64 W = mCir->mWireCount;
+    const u64 rowBytes = mWords * 8;
+    if (mLevel) {
+        // share 1 of last level's AND outputs arrived from prev (:555-573)
+        const u32 nAnd = mCir->mLevelAndCounts[mLevel - 1];
+        if (nAnd) {
+            mRecvFutr.get();
+            GPU_CALL(aby3g_bin_unpack(mRecv.as<u64>(), mCur->outWires[mLevel - 1].as<u32>(), nAnd, mMem.as<u64>(), W,
+                                      mWords, g.stream()));
+        }
+    }
+    if (mLevel < mCir->mLevelCounts.size()) {
+        DeviceBuffer& send = mSend[mLevel & 1];
+        for (const auto& b : mCir->mLevelBatches[mLevel])
+            GPU_CALL(aby3g_bin_gates(mCur->gates.as<aby3g_gate>() + b.begin, b.count, mMem.as<u64>(), W, mWords,
+                                     mZ.as<u64>(), send.as<u64>(), g.stream()));
+        const u32 nAnd = mCir->mLevelAndCounts[mLevel];
+        if (nAnd) {
+            comm.mNext.asyncSendDevice(send.data(), nAnd * rowBytes, g);
+            mRecvFutr = comm.mPrev.asyncRecvDevice(mRecv.data(), nAnd * rowBytes, g);
+        }
+    }
+    ++mLevel;
+    if (hasMoreRounds()) task.then([this](CommPkg& c, Sh3Task& t) { roundCallback(c, t); }, "callback");
+}
+
+Sh3Task Sh3BinaryEvaluator::asyncEvaluate(Sh3Task dep) {
+    return dep.then([this](CommPkg& comm, Sh3Task& self) { roundCallback(comm, self); }, "bin-eval-closure")
+        .getClosure();
+}
+
+Sh3Task Sh3BinaryEvaluator::asyncEvaluate(Sh3Task dep, BetaCircuit* cir, Sh3ShareGen& gen,
+                                          std::vector<const sbMatrix*> inputs, std::vector<sbMatrix*> outputs) {
+    if (cir->mInputs.size() != inputs.size() || cir->mOutputs.size() != outputs.size()) throw RTE_LOC;
+    return dep
+        .then([this, cir, &gen, inputs](CommPkg& comm, Sh3Task& self) {
+            const u64 width = inputs[0]->rows();
+            setCir(cir, width, gen);
+            for (size_t i = 0; i < inputs.size(); ++i) {
+                if (inputs[i]->rows() != width) throw RTE_LOC;
+                setInput(i, *inputs[i]);
+            }
+            roundCallback(comm, self);
+        })
+        .getClosure()
+        .then([this, outputs](Sh3Task&) {
+            for (size_t i = 0; i < outputs.size(); ++i) getOutput(i, *outputs[i]);
+        });
+}
+
+void Sh3BinaryEvaluator::getOutput(u64 i, sbMatrix& out) {
+    if (i >= mCir->mOutputs.size()) throw RTE_LOC;
+    const auto& wires = mCir->mOutputs[i];
+    out.resize(mRows, wires.size());
+    Gpu& g = *mGpu;
+    const u64 W = mCir->mWireCount;
+    const u32* dw = mCur->allOutputWires.as<u32>() + mCur->outputOffsets[i];
+    for (int s = 0; s < 2; ++s)
+        GPU_CALL(aby3g_wires_to_bits(mMem.as<u64>() + (u64)s * W * mWords, dw, (u32)wires.size(), mWords,
+                                     out.share(s), mRows, g.stream()));
+}
+
+}  // namespace aby3

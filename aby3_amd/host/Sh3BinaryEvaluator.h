@@ -1,0 +1,55 @@
+// Bit-sliced binary evaluator (aby3/sh3/Sh3BinaryEvaluator.h/.cpp) on the GPU.
+//
+// Memory: one device allocation [2][wires][words] (wire-major, 64 rows per
+// u64, rows padded to a multiple of 2048 as mMem.reset(width, wires, 8)).
+// AND masks: all z words of the circuit are generated on device before the
+// first round (they depend only on the setCir keys), z[k][w] = draw
+// k*words + w of the (prev, next) keys -- exactly getShares()'s counter
+// schedule (Sh3BinaryEvaluator.cpp:1406-1434).
+// One communication round per AND level, as roundCallback (:539-1196):
+// unpack last level's received shares, run this level's gate batches, send
+// the AND outputs' share 0 to next, post the receive from prev.
+#pragma once
+#include "Circuit.h"
+#include "Sh3Runtime.h"
+#include "Sh3ShareGen.h"
+#include "Sh3Types.h"
+
+namespace aby3 {
+
+class Sh3BinaryEvaluator {
+public:
+    // consumes 16 bytes of the prev and next streams for the AND keys
+    // (Sh3BinaryEvaluator.h:96-102)
+    void setCir(BetaCircuit* cir, u64 width, Sh3ShareGen& gen);
+    void setCir(BetaCircuit* cir, u64 width, block prevSeed, block nextSeed);
+    void setInput(u64 i, const sbMatrix& in);
+    Sh3Task asyncEvaluate(Sh3Task dep);
+    Sh3Task asyncEvaluate(Sh3Task dep, BetaCircuit* cir, Sh3ShareGen& gen, std::vector<const sbMatrix*> inputs,
+                          std::vector<sbMatrix*> outputs);
+    void getOutput(u64 i, sbMatrix& out);
+
+    bool hasMoreRounds() const { return mLevel <= mCir->mLevelCounts.size(); }
+    void roundCallback(CommPkg& comm, Sh3Task task);
+
+    BetaCircuit* mCir = nullptr;
+    u64 mRows = 0, mWords = 0, mLevel = 0;
+    block mKeyPrev, mKeyNext;
+    DeviceBuffer mMem, mZ, mSend[2], mRecv;
+    RecvFuture mRecvFutr;
+
+private:
+    struct DevCircuit {
+        DeviceBuffer gates;                 // aby3g_gate per batched gate
+        std::vector<DeviceBuffer> outWires; // per level: AND output wires (unpack order)
+        std::vector<std::vector<u32>> hostOutWires;
+        DeviceBuffer allOutputWires;        // output bundles, concatenated
+        std::vector<u32> outputOffsets;
+    };
+    std::map<const BetaCircuit*, std::unique_ptr<DevCircuit>> mDev;
+    DevCircuit* mCur = nullptr;
+    Gpu* mGpu = nullptr;
+    void upload(Gpu& g);
+};
+
+}  // namespace aby3

@@ -77,6 +77,7 @@ _SIGS = {
     "aby3g_probe_enable": (c_int, [c_int]),
     "aby3g_probe_read": (c_int, [c_int, POINTER(c_double), POINTER(c_uint64)]),
     "aby3g_probe_reset": (c_int, []),
+    "aby3g_aes_block_host": (c_int, [c_u8p, c_uint64, c_u8p]),
     "aby3g_aes_ctr": (c_int, [c_u8p, c_uint64, c_uint64, c_void_p, c_void_p]),
     "aby3g_prng_fill": (c_int, [c_u8p, c_uint64, c_uint64, c_void_p, c_void_p]),
     "aby3g_share_draws": (c_int, [c_int, c_u8p, c_u8p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p]),

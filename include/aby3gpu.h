@@ -79,6 +79,12 @@ int aby3g_probe_reset(void);
  * Replaces the host AES-NI refills of Sh3ShareGen.h:50-56 and SharedOT.cpp:15. */
 int aby3g_aes_ctr(const uint8_t key[16], uint64_t ctr_base, uint64_t nblocks, void* out, aby3g_stream stream);
 
+/* Host-side AES-128 of one counter block, out = AES(key, LE64(ctr) || 0^8).
+ * Runs on the CPU (no GPU work, no synchronization); the host runtime uses
+ * it only to derive keys from the first blocks of a PRNG stream
+ * (Sh3ShareGen.h:19-20, Sh3Evaluator.cpp:13-14, Sh3BinaryEvaluator.h:96-102). */
+int aby3g_aes_block_host(const uint8_t key[16], uint64_t ctr, uint8_t out[16]);
+
 /* oc::PRNG(seed) bytes [byte_off, byte_off + nbytes) (both multiples of 8).
  * Replaces mPrevCommon/mNextCommon.get(...) (Sh3Evaluator.cpp:526-527,
  * Sh3BinaryEvaluator.h:96-102, Sh3Evaluator.cpp:151-153,188,234-235). */

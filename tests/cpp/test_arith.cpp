@@ -1,0 +1,145 @@
+// Protocol-level parity of the arithmetic evaluator: input sharing,
+// asyncMul (Hadamard and GEMM, with and without truncation), the OT bit
+// multiplications and reveal -- every party's shares bit-exact against the
+// CPU oracle on the reference tests' seeds (Sh3EvaluatorTests.cpp:594-690,
+// :350-410, :780-1032; Test.cpp:74-191).
+#include "harness.h"
+
+using namespace aby3;
+using namespace harness;
+
+static void mulTest(MulMode mode, u64 M, u64 K, u64 N, bool trunc, u64 d, u64 seed) {
+    const u64 bRows = mode == MulMode::Gemm ? K : M;
+    const u64 bCols = mode == MulMode::Gemm ? N : K;
+    i64Matrix a = randMat(M, K, seed), b = randMat(bRows, bCols, seed + 1);
+    if (trunc) {  // fixed-point operands: |x| < 2^20 keeps |sum a*b| far below 2^62 (truncation valid)
+        a = randMat(M, K, seed, -(1ll << 20), 1ll << 20);
+        b = randMat(bRows, bCols, seed + 1, -(1ll << 20), 1ll << 20);
+    }
+    ShareSink got;
+    std::vector<i64> revealed;
+    run3([&](harness::Party& p) {
+        si64Matrix A(M, K), B(bRows, bCols), C;
+        if (p.idx == 0) {
+            p.enc.localIntMatrix(p.rt, a, A).get();
+            p.enc.localIntMatrix(p.rt, b, B).get();
+        } else {
+            p.enc.remoteIntMatrix(p.rt, A).get();
+            p.enc.remoteIntMatrix(p.rt, B).get();
+        }
+        if (trunc)
+            p.eval.asyncMul(p.rt, A, B, C, d, mode).get();
+        else
+            p.eval.asyncMul(p.rt, A, B, C, mode).get();
+        got.put(p.idx, C);
+        i64Matrix r;
+        p.enc.revealAll(p.rt, C, r).get();
+        if (p.idx == 0) revealed = r.mData;
+    });
+    auto enc = orc::makeEncryptors(0);
+    auto ev = orc::makeEvaluators(1);
+    orc::Shared A = orc::shareInt(enc, 0, toOrc(a)), B = orc::shareInt(enc, 0, toOrc(b));
+    orc::MulMode om = mode == MulMode::Gemm ? orc::MUL_GEMM : orc::MUL_HADAMARD;
+    orc::Shared C = trunc ? orc::mulTrunc(ev, om, A, B, d) : orc::mul(ev, om, A, B);
+    got.expectEq(C, "asyncMul");
+    check(revealed == orc::revealInt(C).v, "revealAll");
+    // plaintext: exact product, and within 1 of the floor for truncation (:396-407)
+    orc::SMat As, Bs;
+    orc::Mat plain;
+    As.s[0] = toOrc(a);
+    As.s[1] = orc::Mat(M, K);
+    Bs.s[0] = toOrc(b);
+    Bs.s[1] = orc::Mat(bRows, bCols);
+    // (a0, 0) x (b0, 0) with A1 = B1 = 0 gives the plain product
+    orc::localProduct(om, As, Bs, plain);
+    for (u64 i = 0; i < plain.size(); ++i) {
+        if (!trunc) {
+            check(revealed[i] == plain.v[i], "plain product");
+        } else {
+            // three floored pair shares plus the floored reveal: the result lies in
+            // (floor(xy/2^d) - 4, floor(xy/2^d) + 1] (Sh3EvaluatorTests.cpp:396-407 bounds it by 4)
+            i64 e = plain.v[i] >> d;
+            check(revealed[i] - e <= 1 && e - revealed[i] < 4, "truncation error out of (-4, 1]");
+        }
+    }
+}
+
+static void bitMulTest(bool pub, u64 n, u64 seed) {
+    i64Matrix a = randMat(n, 1, seed), bits = randMat(n, 1, seed + 7, 0, 1);
+    const i64 apub = 0x123456789abcdefll;
+    ShareSink got;
+    std::vector<i64> revealed;
+    run3([&](harness::Party& p) {
+        si64Matrix A(n, 1), C;
+        sbMatrix B(n, 1);
+        if (p.idx == 0) {
+            p.enc.localBinMatrix(p.rt, bits, B).get();
+            if (!pub) p.enc.localIntMatrix(p.rt, a, A).get();
+        } else {
+            p.enc.remoteBinMatrix(p.rt, B).get();
+            if (!pub) p.enc.remoteIntMatrix(p.rt, A).get();
+        }
+        if (pub)
+            p.eval.asyncMul(p.rt, apub, B, C).get();
+        else
+            p.eval.asyncMul(p.rt, A, B, C).get();
+        got.put(p.idx, C);
+        i64Matrix r;
+        p.enc.revealAll(p.rt, C, r).get();
+        if (p.idx == 0) revealed = r.mData;
+    });
+    auto enc = orc::makeEncryptors(0);
+    auto ev = orc::makeEvaluators(1);
+    orc::Shared B = orc::shareBin(enc, 0, toOrc(bits));
+    orc::Shared C;
+    if (pub) {
+        C = orc::mulPubBit(ev, apub, B);
+    } else {
+        orc::Shared A = orc::shareInt(enc, 0, toOrc(a));
+        C = orc::mulBit(ev, A, B);
+    }
+    got.expectEq(C, pub ? "asyncMul(i64, sb)" : "asyncMul(si64, sb)");
+    for (u64 i = 0; i < n; ++i) check(revealed[i] == (bits(i, 0) ? (pub ? apub : a(i, 0)) : 0), "bit product");
+}
+
+static void arithBasic16() {
+    // Test.cpp:74-191: x = i, y = 16 - i; mul (Hadamard, the fork's cipher_mul)
+    const int T = 16;
+    i64Matrix x(T, 1), y(T, 1);
+    for (int i = 0; i < T; ++i) {
+        x(i, 0) = i;
+        y(i, 0) = T - i;
+    }
+    std::vector<i64> revealed;
+    run3([&](harness::Party& p) {
+        si64Matrix X(T, 1), Y(T, 1), Z;
+        if (p.idx == 0) {
+            p.enc.localIntMatrix(p.rt, x, X).get();
+            p.enc.localIntMatrix(p.rt, y, Y).get();
+        } else {
+            p.enc.remoteIntMatrix(p.rt, X).get();
+            p.enc.remoteIntMatrix(p.rt, Y).get();
+        }
+        p.eval.asyncMul(p.rt, X, Y, Z, MulMode::Hadamard).get();
+        i64Matrix r;
+        p.enc.revealAll(p.rt, Z, r).get();
+        if (p.idx == 0) revealed = r.mData;
+    });
+    for (int i = 0; i < T; ++i) check(revealed[i] == i * (T - i), "mul 16");
+}
+
+int main() {
+    test("share_reveal_and_hadamard_16 (Test.cpp arith_basic_test mul)", arithBasic16);
+    test("asyncMul_hadamard_128x128", [] { mulTest(MulMode::Hadamard, 128, 128, 128, false, 0, 1); });
+    test("asyncMul_gemm_10x10 (Sh3_Evaluator_mul_test)", [] { mulTest(MulMode::Gemm, 10, 10, 10, false, 0, 2); });
+    test("asyncMul_gemm_33x17x65", [] { mulTest(MulMode::Gemm, 33, 17, 65, false, 0, 3); });
+    test("asyncMul_gemm_256x128x1 (LR xw)", [] { mulTest(MulMode::Gemm, 256, 128, 1, false, 0, 4); });
+    test("asyncMul_trunc_hadamard_4x4_D8", [] { mulTest(MulMode::Hadamard, 4, 4, 4, true, 8, 5); });
+    test("asyncMul_trunc_gemm_4x4_D8 (matrixFixed_test)", [] { mulTest(MulMode::Gemm, 4, 4, 4, true, 8, 6); });
+    test("asyncMul_trunc_gemm_128x256x1_D27 (LR update)", [] { mulTest(MulMode::Gemm, 128, 256, 1, true, 27, 7); });
+    test("asyncMul_trunc_gemm_256x256x256_D16", [] { mulTest(MulMode::Gemm, 256, 256, 256, true, 16, 8); });
+    test("asyncMul_si64_x_sb (sh3_asyncArithBinMul_test)", [] { bitMulTest(false, 100, 9); });
+    test("asyncMul_i64_x_sb (sh3_asyncPubArithBinMul_test)", [] { bitMulTest(true, 100, 10); });
+    test("asyncMul_si64_x_sb_1000", [] { bitMulTest(false, 1000, 11); });
+    return g_failures ? 1 : 0;
+}

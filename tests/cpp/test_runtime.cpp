@@ -1,0 +1,118 @@
+// Scheduler / Sh3Runtime contract, restating the reference's
+// Task_schedule_test and Sh3_Runtime_schedule_test
+// (aby3_tests/Sh3RuntimeTests.cpp:15-154, 156-266): exact execution order.
+// CPU-only (the runtime is created without a device).
+#include "Sh3Runtime.h"
+#include <cstdio>
+#include <functional>
+
+using namespace aby3;
+
+static int failures = 0;
+#define CHECK(c)                                                              \
+    do {                                                                      \
+        if (!(c)) throw std::runtime_error("check failed: " #c " @" LOCATION); \
+    } while (0)
+
+static void run(const char* name, std::function<void()> f) {
+    try {
+        f();
+        std::printf("PASS %s\n", name);
+    } catch (const std::exception& e) {
+        ++failures;
+        std::printf("FAIL %s: %s\n", name, e.what());
+    }
+}
+
+static void task_schedule_test() {
+    Scheduler rt;
+    const i64 base = -1;
+    i64 task0 = rt.addTask(TaskType::Round, {base});
+    i64 task1 = rt.addTask(TaskType::Round, {base});
+    i64 task2 = rt.addTask(TaskType::Round, {task0, task1});
+    i64 task1b = rt.addTask(TaskType::Round, {base});
+    i64 task2b = rt.addTask(TaskType::Round, {task2});
+    i64 close1 = rt.addClosure({task2});
+    i64 task3 = rt.addTask(TaskType::Round, {close1});
+
+    CHECK(rt.currentTask() == task0);
+    rt.popTask();
+    CHECK(rt.currentTask() == task1);
+    rt.popTask();
+    CHECK(rt.currentTask() == task1b);
+    rt.popTask();
+    CHECK(rt.currentTask() == task2);
+    i64 task2c = rt.addTask(TaskType::Round, {task2});
+    rt.popTask();
+    CHECK(rt.currentTask() == task2b);
+    rt.popTask();
+    CHECK(rt.currentTask() == task2c);
+    rt.popTask();
+    CHECK(rt.currentTask() == task3);
+    rt.popTask();
+}
+
+static void runtime_schedule_test() {
+    Sh3Runtime rt;
+    CommPkg comm;
+    rt.init(0, comm, -1);
+    int counter = 0;
+    auto base = rt.noDependencies();
+
+    auto task0 = base.then([&](CommPkg&, Sh3Task) { CHECK(counter++ == 0); }, "task0");
+    auto task1 = base.then([&](CommPkg&, Sh3Task) { CHECK(counter++ == 1); }, "task1");
+    auto task2 = (task0 && task1)
+                     .then(
+                         [&](CommPkg&, Sh3Task self) {
+                             CHECK(counter++ == 2);
+                             self.then([&](CommPkg&, Sh3Task) { CHECK(counter++ == 5); }, "task2-sub1")
+                                 .then([&](CommPkg&, Sh3Task) { CHECK(counter++ == 6); }, "task2-sub2");
+                         },
+                         "task2");
+    task2.then([&](Sh3Task) { CHECK(counter++ == 4); }, "task2-cont.");
+    auto task3 = task2.getClosure().then([&](CommPkg&, Sh3Task) { CHECK(counter++ == 7); }, "task3");
+
+    task2.get();
+    CHECK(counter++ == 3);
+    task3.get();
+    CHECK(counter++ == 8);
+
+    base.then([&](CommPkg&, Sh3Task self) {
+        CHECK(counter++ == 9);
+        self.then([&](CommPkg&, Sh3Task) { CHECK(counter++ == 12); });
+    });
+    base.then([&](CommPkg&, Sh3Task self) {
+        CHECK(counter++ == 10);
+        self.then([&](CommPkg&, Sh3Task) { CHECK(counter++ == 13); });
+    });
+    rt.runOneRound();
+    CHECK(counter++ == 11);
+    rt.runOneRound();
+    CHECK(counter++ == 14);
+    rt.runAll();
+    CHECK(counter++ == 15);
+}
+
+static void reentrancy_test() {
+    Sh3Runtime rt;
+    CommPkg comm;
+    rt.init(0, comm, -1);
+    bool threw = false;
+    auto t = rt.noDependencies().then([&](CommPkg&, Sh3Task self) {
+        auto inner = self.then([](CommPkg&, Sh3Task) {});
+        try {
+            inner.get();  // Sh3Runtime.cpp:274-275 forbids this
+        } catch (const std::runtime_error&) {
+            threw = true;
+        }
+    });
+    rt.runAll();
+    CHECK(threw);
+}
+
+int main() {
+    run("Task_schedule_test", task_schedule_test);
+    run("Sh3_Runtime_schedule_test", runtime_schedule_test);
+    run("Sh3_Runtime_reentrancy_test", reentrancy_test);
+    return failures ? 1 : 0;
+}

@@ -49,6 +49,35 @@ __global__ void k_bitop(int op, u64 n, const u64* __restrict__ a, const u64* __r
     }
 }
 
+// one row per (y, x-chunk); both shares
+__global__ void k_gather_rows(const i64* __restrict__ src, u64 rows, u64 cols, const u32* __restrict__ idx, u64 n,
+                              i64* __restrict__ dst) {
+    const u64 total = 2 * n * cols;
+    GRID_STRIDE(t, total) {
+        const u64 s = t / (n * cols), rem = t % (n * cols), i = rem / cols, c = rem % cols;
+        dst[t] = src[s * rows * cols + (u64)idx[i] * cols + c];
+    }
+}
+
+// 64 x 64 tile transpose through LDS (padded rows: conflict-free)
+__global__ void __launch_bounds__(256) k_transpose(const i64* __restrict__ src, u64 rows, u64 cols,
+                                                   i64* __restrict__ dst) {
+    __shared__ i64 tile[64][65];
+    const u64 s = blockIdx.z;
+    const u64 r0 = (u64)blockIdx.y * 64, c0 = (u64)blockIdx.x * 64;
+    const i64* S = src + s * rows * cols;
+    i64* Dd = dst + s * rows * cols;
+    for (u32 k = threadIdx.x; k < 64 * 64; k += blockDim.x) {
+        const u32 r = k / 64, c = k % 64;
+        if (r0 + r < rows && c0 + c < cols) tile[r][c] = S[(r0 + r) * cols + c0 + c];
+    }
+    __syncthreads();
+    for (u32 k = threadIdx.x; k < 64 * 64; k += blockDim.x) {
+        const u32 c = k / 64, r = k % 64;  // output row = input column
+        if (r0 + r < rows && c0 + c < cols) Dd[(c0 + c) * rows + r0 + r] = tile[r][c];
+    }
+}
+
 __global__ void k_gather(u64 n, const u32* __restrict__ idx, const u64* __restrict__ src, u64* __restrict__ dst) {
     GRID_STRIDE(i, n) dst[i] = src[idx[i]];
 }
@@ -90,6 +119,24 @@ int aby3g_u64_bitop(int op, uint64_t n, const uint64_t* a, const uint64_t* b, ui
         ABY3G_REQUIRE(op >= 2 || b != nullptr, "binary op needs b");
         if (!n) return;
         launch(PROBE_OTHER, k_bitop, dim3(ew_grid(n)), dim3(kB), 0, S(stream), op, n, a, b, out);
+    });
+}
+
+int aby3g_i64_gather_rows(const int64_t* src, uint64_t rows, uint64_t cols, const uint32_t* idx, uint64_t n,
+                          int64_t* dst, aby3g_stream stream) {
+    return guarded([&] {
+        if (!n || !cols) return;
+        launch(PROBE_OTHER, k_gather_rows, dim3(ew_grid(2 * n * cols)), dim3(kB), 0, S(stream), src, rows, cols, idx,
+               n, dst);
+    });
+}
+
+int aby3g_i64_transpose(const int64_t* src, uint64_t rows, uint64_t cols, int64_t* dst, aby3g_stream stream) {
+    return guarded([&] {
+        ABY3G_REQUIRE(src != dst, "in-place transpose is not supported");
+        if (!rows || !cols) return;
+        dim3 grid((u32)((cols + 63) / 64), (u32)((rows + 63) / 64), 2);
+        launch(PROBE_OTHER, k_transpose, grid, dim3(256), 0, S(stream), src, rows, cols, dst);
     });
 }
 

@@ -1,0 +1,542 @@
+// C entry points (include/aby3.h): three persistent party threads running a
+// job of the hot path, for bench.py and the Python tests.
+#include <aby3.h>
+#include <atomic>
+#include <cmath>
+#include <condition_variable>
+#include <functional>
+#include <numeric>
+#include <thread>
+#include "Basic.h"
+#include "aby3ML.h"
+
+namespace aby3 {
+
+namespace {
+thread_local std::string t_err;
+
+struct PartyCtx {
+    int idx = 0;
+    Sh3Runtime rt;
+    Sh3Encryptor enc;
+    Sh3Evaluator eval;
+};
+
+u64 xorshift(u64& x) {
+    x ^= x << 13;
+    x ^= x >> 7;
+    x ^= x << 17;
+    return x;
+}
+i64Matrix randomMat(u64 r, u64 c, u64 seed, i64 bound) {
+    i64Matrix m(r, c);
+    u64 x = seed * 0x9E3779B97F4A7C15ull + 12345;
+    for (auto& v : m.mData) v = bound ? (i64)(xorshift(x) % (2 * (u64)bound)) - bound : (i64)xorshift(x);
+    return m;
+}
+
+struct Job {
+    virtual ~Job() = default;
+    virtual void setup(PartyCtx& p) = 0;
+    virtual void step(PartyCtx& p) = 0;
+    virtual bool check(PartyCtx&) { return true; }
+    virtual void info(double* out) = 0;
+};
+
+// ---- C2 / C1: asyncMul (+ truncation) ------------------------------------
+struct MulJob : Job {
+    u64 M, K, N, D;
+    MulMode mode;
+    bool trunc;
+    i64Matrix a, b;
+    si64Matrix A[3], B[3], C[3];
+    MulJob(u64 m, u64 k, u64 n, u64 d, MulMode md, bool t) : M(m), K(k), N(n), D(d), mode(md), trunc(t) {
+        const u64 br = mode == MulMode::Gemm ? K : M, bc = mode == MulMode::Gemm ? N : K;
+        // fixed-point operands in [-8, 8) * 2^D
+        const i64 bound = trunc ? (8ll << D) : 0;
+        a = randomMat(M, K, 1, bound);
+        b = randomMat(br, bc, 2, bound);
+    }
+    void setup(PartyCtx& p) override {
+        const u64 br = mode == MulMode::Gemm ? K : M, bc = mode == MulMode::Gemm ? N : K;
+        A[p.idx].resize(M, K);
+        B[p.idx].resize(br, bc);
+        if (p.idx == 0) {
+            p.enc.localIntMatrix(p.rt, a, A[0]).get();
+            p.enc.localIntMatrix(p.rt, b, B[0]).get();
+        } else {
+            p.enc.remoteIntMatrix(p.rt, A[p.idx]).get();
+            p.enc.remoteIntMatrix(p.rt, B[p.idx]).get();
+        }
+    }
+    void step(PartyCtx& p) override {
+        if (trunc)
+            p.eval.asyncMul(p.rt, A[p.idx], B[p.idx], C[p.idx], D, mode).get();
+        else
+            p.eval.asyncMul(p.rt, A[p.idx], B[p.idx], C[p.idx], mode).get();
+    }
+    bool check(PartyCtx& p) override {
+        i64Matrix r;
+        p.enc.revealAll(p.rt, C[p.idx], r).get();
+        if (p.idx != 0) return true;
+        // spot-check 64 entries against the plaintext product
+        u64 x = 99;
+        for (int t = 0; t < 64; ++t) {
+            const u64 i = xorshift(x) % M, j = xorshift(x) % N;
+            __int128 s = 0;
+            if (mode == MulMode::Gemm)
+                for (u64 k = 0; k < K; ++k) s += (__int128)a(i, k) * b(k, j);
+            else
+                s = (__int128)a(i, j) * b(i, j);
+            const i64 exact = (i64)(u64)s;
+            const i64 got = r(i, j);
+            if (trunc) {
+                const i64 e = (i64)(s >> D);
+                if (got - e > 1 || e - got >= 4) return false;
+            } else if (got != exact) {
+                return false;
+            }
+        }
+        return true;
+    }
+    void info(double* o) override {
+        o[ABY3H_INFO_MULTS_PER_STEP] = mode == MulMode::Gemm ? (double)M * N * K : (double)M * N;
+        o[ABY3H_INFO_GEMM_INT8_OPS] = mode == MulMode::Gemm ? 144.0 * M * N * K : 0;
+    }
+};
+
+// gate-kernel algorithmic bytes per padded word
+double gateBytes(const BetaCircuit& c) {
+    double b = 0;
+    for (const auto& g : c.mGates) {
+        switch (g.type) {
+            case GateType::a:
+            case GateType::Inv: b += 32; break;          // 2 reads, 2 writes
+            case GateType::Xor:
+            case GateType::Nxor: b += 48; break;         // 4 reads, 2 writes
+            default: b += 56 + 16; break;                 // 4 reads + z, share 0 + send; unpack 8 + 8
+        }
+    }
+    return b;
+}
+
+// ---- C3: fetch_msb / cipher_gt over `rows` values -------------------------
+struct MsbJob : Job {
+    u64 rows;
+    i64Matrix a, b;
+    si64Matrix A[3], B[3];
+    sbMatrix R[3];
+    CircuitLibrary lib;
+    explicit MsbJob(u64 r) : rows(r) {
+        a = randomMat(rows, 1, 3, 0);
+        b = randomMat(rows, 1, 4, 0);
+    }
+    void setup(PartyCtx& p) override {
+        A[p.idx].resize(rows, 1);
+        B[p.idx].resize(rows, 1);
+        if (p.idx == 0) {
+            p.enc.localIntMatrix(p.rt, a, A[0]).get();
+            p.enc.localIntMatrix(p.rt, b, B[0]).get();
+        } else {
+            p.enc.remoteIntMatrix(p.rt, A[p.idx]).get();
+            p.enc.remoteIntMatrix(p.rt, B[p.idx]).get();
+        }
+    }
+    void step(PartyCtx& p) override { cipher_gt(p.idx, A[p.idx], B[p.idx], R[p.idx], p.eval, p.rt); }
+    bool check(PartyCtx& p) override {
+        i64Matrix r;
+        p.enc.revealAll(p.rt, R[p.idx], r).get();
+        if (p.idx != 0) return true;
+        for (u64 i = 0; i < rows; ++i)
+            if ((r(i, 0) & 1) != (i64)(((u64)b(i, 0) - (u64)a(i, 0)) >> 63)) return false;
+        return true;
+    }
+    void info(double* o) override {
+        BetaCircuit* c = lib.int_comp_helper(64);
+        const double words = std::ceil(rows / 64.0), padded = 32.0 * ((rows + 2047) / 2048);
+        o[ABY3H_INFO_MULTS_PER_STEP] = c->mAndCount * words;
+        o[ABY3H_INFO_AND_WORDS] = c->mAndCount * words;
+        o[ABY3H_INFO_GATE_WORDS] = c->mGates.size() * words;
+        o[ABY3H_INFO_GATE_BYTES] = gateBytes(*c) * padded;
+    }
+};
+
+// ---- C4: one logistic-regression SGD iteration ----------------------------
+struct LrJob : Job {
+    u64 n, d, B, D, aB;
+    i64Matrix X, Y, w0;
+    si64Matrix sX[3], sY[3], sW[3];
+    std::unique_ptr<aby3ML> ml[3];
+    SgdState st[3];
+    std::vector<u32> perm;
+    u64 iter[3] = {0, 0, 0};
+    LrJob(u64 n_, u64 d_, u64 b_, u64 D_, u64 aB_) : n(n_), d(d_), B(b_), D(D_), aB(aB_) {
+        // synthetic LogisticModelGen-shaped data (main-logistic.cpp:82-100):
+        // features ~ U[-1, 1), labels from a planted model, fixed point D
+        X.resize(n, d);
+        Y.resize(n, 1);
+        w0.resize(d, 1);
+        u64 x = 234345;
+        std::vector<double> model(d, 0);
+        for (u64 j = 0; j < std::min<u64>(d, 10); ++j) model[j] = (double)(xorshift(x) % 10);
+        for (u64 i = 0; i < n; ++i) {
+            double dot = 0;
+            for (u64 j = 0; j < d; ++j) {
+                double v = (double)(xorshift(x) % 2000000) / 1e6 - 1.0;
+                X(i, j) = toFixed(v, D);
+                dot += v * model[j];
+            }
+            Y(i, 0) = dot > 0 ? (1ll << D) : 0;
+        }
+        perm.resize(n);
+        std::iota(perm.begin(), perm.end(), 0);
+        for (u64 i = n; i > 1; --i) std::swap(perm[i - 1], perm[xorshift(x) % i]);
+    }
+    void setup(PartyCtx& p) override {
+        sX[p.idx].resize(n, d);
+        sY[p.idx].resize(n, 1);
+        sW[p.idx].resize(d, 1);
+        if (p.idx == 0) {
+            p.enc.localIntMatrix(p.rt, X, sX[0]).get();
+            p.enc.localIntMatrix(p.rt, Y, sY[0]).get();
+            p.enc.localIntMatrix(p.rt, w0, sW[0]).get();
+        } else {
+            p.enc.remoteIntMatrix(p.rt, sX[p.idx]).get();
+            p.enc.remoteIntMatrix(p.rt, sY[p.idx]).get();
+            p.enc.remoteIntMatrix(p.rt, sW[p.idx]).get();
+        }
+        ml[p.idx] = std::make_unique<aby3ML>(p.rt, p.enc, p.eval, D);
+    }
+    void step(PartyCtx& p) override {
+        const u64 start = (iter[p.idx]++ * B) % (n - B + 1);
+        std::vector<u32> idx(perm.begin() + start, perm.begin() + start + B);
+        sgdLogisticStep(*ml[p.idx], sX[p.idx], sY[p.idx], sW[p.idx], idx, aB, st[p.idx]);
+    }
+    bool check(PartyCtx& p) override {
+        i64Matrix r;
+        p.enc.revealAll(p.rt, sW[p.idx], r).get();
+        if (p.idx != 0) return true;
+        for (auto v : r.mData)
+            if (std::abs(fromFixed(v, D)) > 1e6) return false;
+        return true;
+    }
+    void info(double* o) override { o[ABY3H_INFO_MULTS_PER_STEP] = 2.0 * B * d; }
+};
+
+// ---- C5: one compare-exchange layer of the merge network ------------------
+struct MergeLayerJob : Job {
+    u64 keys;
+    i64Matrix k;
+    sbMatrix S[3], X[3], Y[3], Mn[3], Mx[3];
+    CircuitLibrary lib;
+    std::vector<u32> xi, yi;
+    explicit MergeLayerJob(u64 n) : keys(n) {
+        k.resize(keys, 1);
+        u64 x = 7;
+        for (u64 i = 0; i < keys; ++i) k(i, 0) = (i64)(((xorshift(x) % (1ull << 43)) << 20) | i);
+        for (u64 i = 0; i + 1 < keys; i += 2) {
+            xi.push_back((u32)i);
+            yi.push_back((u32)(i + 1));
+        }
+    }
+    void setup(PartyCtx& p) override {
+        S[p.idx].resize(keys, 64);
+        if (p.idx == 0)
+            p.enc.localBinMatrix(p.rt, k, S[0]).get();
+        else
+            p.enc.remoteBinMatrix(p.rt, S[p.idx]).get();
+    }
+    void step(PartyCtx& p) override {
+        Gpu& g = p.rt.gpu();
+        const u64 m = xi.size();
+        DeviceBuffer dx(g, m * 4), dy(g, m * 4);
+        toDevice(dx.data(), xi.data(), m * 4, g);
+        toDevice(dy.data(), yi.data(), m * 4, g);
+        sbMatrix &s = S[p.idx], &x = X[p.idx], &y = Y[p.idx];
+        x.resize(m, 64);
+        y.resize(m, 64);
+        for (int sh = 0; sh < 2; ++sh) {
+            GPU_CALL(aby3g_u64_gather(m, dx.as<u32>(), (const u64*)s.share(sh), (u64*)x.share(sh), g.stream()));
+            GPU_CALL(aby3g_u64_gather(m, dy.as<u32>(), (const u64*)s.share(sh), (u64*)y.share(sh), g.stream()));
+        }
+        bool_cipher_max_min_split(p.idx, x, y, Mx[p.idx], Mn[p.idx], p.eval, p.rt);
+        for (int sh = 0; sh < 2; ++sh) {
+            GPU_CALL(aby3g_u64_scatter(m, dx.as<u32>(), (const u64*)Mn[p.idx].share(sh), (u64*)s.share(sh), g.stream()));
+            GPU_CALL(aby3g_u64_scatter(m, dy.as<u32>(), (const u64*)Mx[p.idx].share(sh), (u64*)s.share(sh), g.stream()));
+        }
+    }
+    void info(double* o) override {
+        BetaCircuit* c = lib.cmp_swap(64);
+        const u64 m = keys / 2;
+        const double words = std::ceil(m / 64.0), padded = 32.0 * ((m + 2047) / 2048);
+        o[ABY3H_INFO_MULTS_PER_STEP] = c->mAndCount * words;
+        o[ABY3H_INFO_AND_WORDS] = c->mAndCount * words;
+        o[ABY3H_INFO_GATE_WORDS] = c->mGates.size() * words;
+        o[ABY3H_INFO_GATE_BYTES] = gateBytes(*c) * padded;
+    }
+};
+
+}  // namespace
+
+struct Session {
+    std::unique_ptr<Job> job;
+    std::thread th[3];
+    std::mutex mu;
+    std::condition_variable cv, done;
+    // command: 0 idle, 1 run, 2 stop, 3 probe read, 4 probe reset, 5 check
+    int cmd = 0;
+    u64 gen = 0, steps = 0;
+    int finished = 0;
+    std::string err;
+    double probeMs[8] = {0};
+    u64 probeN[8] = {0};
+    int probeFamily = 0;
+    bool checkOk = true;
+    std::vector<CommPkg> comms;
+
+    void worker(int i, int device, bool probe) {
+        PartyCtx p;
+        u64 seen = 0;
+        try {
+            p.idx = i;
+            p.rt.init(i, comms[i], device);
+            p.enc.init(i, toBlock(0, i), toBlock(0, (i + 1) % 3));
+            p.eval.init(i, toBlock(1, i), toBlock(1, (i + 1) % 3));
+            if (probe) GPU_CALL(aby3g_probe_enable(1));
+            job->setup(p);
+            p.rt.gpu().sync();
+        } catch (const std::exception& e) {
+            std::lock_guard<std::mutex> lk(mu);
+            err = std::string("party ") + std::to_string(i) + " setup: " + e.what();
+        }
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            ++finished;
+            done.notify_all();
+        }
+        for (;;) {
+            int c;
+            u64 n;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return gen != seen; });
+                seen = gen;
+                c = cmd;
+                n = steps;
+            }
+            if (c == 2) return;
+            try {
+                if (!err.empty()) throw std::runtime_error("session failed earlier");
+                if (c == 1) {
+                    for (u64 s = 0; s < n; ++s) job->step(p);
+                    p.rt.gpu().sync();
+                } else if (c == 3) {
+                    double ms = 0;
+                    uint64_t cnt = 0;
+                    GPU_CALL(aby3g_probe_read(probeFamily, &ms, &cnt));
+                    std::lock_guard<std::mutex> lk(mu);
+                    probeMs[0] += ms;
+                    probeN[0] += cnt;
+                } else if (c == 4) {
+                    GPU_CALL(aby3g_probe_reset());
+                } else if (c == 5) {
+                    bool ok = job->check(p);
+                    p.rt.gpu().sync();
+                    std::lock_guard<std::mutex> lk(mu);
+                    checkOk = checkOk && ok;
+                }
+            } catch (const std::exception& e) {
+                std::lock_guard<std::mutex> lk(mu);
+                if (err.empty()) err = std::string("party ") + std::to_string(i) + ": " + e.what();
+            }
+            std::lock_guard<std::mutex> lk(mu);
+            ++finished;
+            done.notify_all();
+        }
+    }
+
+    void command(int c, u64 n = 0) {
+        std::unique_lock<std::mutex> lk(mu);
+        cmd = c;
+        steps = n;
+        finished = 0;
+        ++gen;
+        cv.notify_all();
+        done.wait(lk, [&] { return finished == 3; });
+    }
+};
+
+}  // namespace aby3
+
+using namespace aby3;
+
+struct aby3h_session {
+    Session s;
+};
+
+extern "C" {
+
+const char* aby3h_last_error(void) { return t_err.c_str(); }
+
+aby3h_session* aby3h_session_create(int job, const uint64_t* params, int nparams, const int* devices, int probe) {
+    try {
+        auto P = [&](int i, u64 def) { return i < nparams ? params[i] : def; };
+        auto* h = new aby3h_session;
+        Session& s = h->s;
+        switch (job) {
+            case ABY3H_JOB_MUL_TRUNC:
+                s.job = std::make_unique<MulJob>(P(0, 1024), P(1, 1024), P(2, 1024), P(3, 16),
+                                                 P(4, 1) ? MulMode::Gemm : MulMode::Hadamard, true);
+                break;
+            case ABY3H_JOB_MUL:
+                s.job = std::make_unique<MulJob>(P(0, 128), P(1, 128), P(2, 128), 0,
+                                                 P(3, 0) ? MulMode::Gemm : MulMode::Hadamard, false);
+                break;
+            case ABY3H_JOB_MSB: s.job = std::make_unique<MsbJob>(P(0, 1 << 20)); break;
+            case ABY3H_JOB_LR:
+                s.job = std::make_unique<LrJob>(P(0, 1000000), P(1, 128), P(2, 256), P(3, 16), P(4, 11));
+                break;
+            case ABY3H_JOB_MERGE_LAYER: s.job = std::make_unique<MergeLayerJob>(P(0, 1 << 20)); break;
+            default: throw std::runtime_error("unknown job");
+        }
+        s.comms = makeLocalRing();
+        {
+            std::unique_lock<std::mutex> lk(s.mu);
+            s.finished = 0;
+        }
+        for (int i = 0; i < 3; ++i) s.th[i] = std::thread([&s, i, devices, probe] {
+            s.worker(i, devices ? devices[i] : 0, probe != 0);
+        });
+        {
+            std::unique_lock<std::mutex> lk(s.mu);
+            s.done.wait(lk, [&] { return s.finished == 3; });
+        }
+        if (!s.err.empty()) {
+            std::string e = s.err;
+            aby3h_session_destroy(h);
+            throw std::runtime_error(e);
+        }
+        return h;
+    } catch (const std::exception& e) {
+        t_err = e.what();
+        return nullptr;
+    }
+}
+
+int aby3h_session_run(aby3h_session* h, uint64_t steps) {
+    h->s.command(1, steps);
+    if (!h->s.err.empty()) {
+        t_err = h->s.err;
+        return 1;
+    }
+    return 0;
+}
+
+int aby3h_session_probe(aby3h_session* h, int family, double* ms, uint64_t* launches) {
+    Session& s = h->s;
+    s.probeFamily = family;
+    s.probeMs[0] = 0;
+    s.probeN[0] = 0;
+    s.command(3);
+    *ms = s.probeMs[0];
+    *launches = s.probeN[0];
+    if (!s.err.empty()) {
+        t_err = s.err;
+        return 1;
+    }
+    return 0;
+}
+
+int aby3h_session_probe_reset(aby3h_session* h) {
+    h->s.command(4);
+    return h->s.err.empty() ? 0 : 1;
+}
+
+int aby3h_session_info(aby3h_session* h, double* out, int n) {
+    double tmp[ABY3H_INFO_COUNT] = {0};
+    h->s.job->info(tmp);
+    for (int i = 0; i < n && i < ABY3H_INFO_COUNT; ++i) out[i] = tmp[i];
+    return 0;
+}
+
+int aby3h_session_check(aby3h_session* h) {
+    Session& s = h->s;
+    s.checkOk = true;
+    s.command(5);
+    if (!s.err.empty()) {
+        t_err = s.err;
+        return 2;
+    }
+    return s.checkOk ? 0 : 1;
+}
+
+void aby3h_session_destroy(aby3h_session* h) {
+    if (!h) return;
+    Session& s = h->s;
+    {
+        std::lock_guard<std::mutex> lk(s.mu);
+        s.cmd = 2;
+        ++s.gen;
+        s.cv.notify_all();
+    }
+    for (auto& t : s.th)
+        if (t.joinable()) t.join();
+    delete h;
+}
+
+int aby3h_circuit(const char* name, uint64_t size, uint64_t param, uint64_t counts[6], uint32_t* gates,
+                  uint32_t* level_counts, uint32_t* in_sizes, uint32_t* in_wires, uint32_t* out_sizes,
+                  uint32_t* out_wires) {
+    try {
+        CircuitLibrary lib;
+        std::string n(name);
+        BetaCircuit* c = nullptr;
+        if (n == "int_comp_helper") c = lib.int_comp_helper(size);
+        else if (n == "int_int_lt") c = lib.int_int_lt(size);
+        else if (n == "int_eq") c = lib.int_eq(size);
+        else if (n == "int_int_add") c = lib.int_int_add(size);
+        else if (n == "int_int_sub") c = lib.int_int_sub(size);
+        else if (n == "int_int_bitwiseAnd") c = lib.int_int_bitwiseAnd(size);
+        else if (n == "int_int_bitwiseOr") c = lib.int_int_bitwiseOr(size);
+        else if (n == "bits_nor_helper") c = lib.bits_nor_helper(size);
+        else if (n == "cmp_swap") c = lib.cmp_swap(size);
+        else if (n == "int_Sh3Piecewise_helper") c = lib.int_Sh3Piecewise_helper(size, param);
+        else throw std::runtime_error("unknown circuit " + n);
+        u64 inW = 0, outW = 0;
+        for (auto& b : c->mInputs) inW += b.size();
+        for (auto& b : c->mOutputs) outW += b.size();
+        counts[0] = c->mWireCount;
+        counts[1] = c->mLevelGates.size();
+        counts[2] = c->mLevelCounts.size();
+        counts[3] = c->mInputs.size();
+        counts[4] = c->mOutputs.size();
+        counts[5] = inW + outW;
+        if (gates)
+            for (size_t i = 0; i < c->mLevelGates.size(); ++i) {
+                const auto& g = c->mLevelGates[i];
+                gates[4 * i] = g.in0;
+                gates[4 * i + 1] = g.in1;
+                gates[4 * i + 2] = g.out;
+                gates[4 * i + 3] = (u32)g.type;
+            }
+        if (level_counts) std::copy(c->mLevelCounts.begin(), c->mLevelCounts.end(), level_counts);
+        u64 o = 0;
+        for (size_t b = 0; b < c->mInputs.size(); ++b) {
+            if (in_sizes) in_sizes[b] = (u32)c->mInputs[b].size();
+            if (in_wires) std::copy(c->mInputs[b].begin(), c->mInputs[b].end(), in_wires + o);
+            o += c->mInputs[b].size();
+        }
+        o = 0;
+        for (size_t b = 0; b < c->mOutputs.size(); ++b) {
+            if (out_sizes) out_sizes[b] = (u32)c->mOutputs[b].size();
+            if (out_wires) std::copy(c->mOutputs[b].begin(), c->mOutputs[b].end(), out_wires + o);
+            o += c->mOutputs[b].size();
+        }
+        return 0;
+    } catch (const std::exception& e) {
+        t_err = e.what();
+        return 1;
+    }
+}
+
+}  // extern "C"

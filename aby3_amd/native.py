@@ -23,7 +23,7 @@ c_u8p = POINTER(ctypes.c_uint8)
 MUL_HADAMARD, MUL_GEMM = 0, 1
 DRAW_ARITH, DRAW_BIN, DRAW_RANDPAIR = 0, 1, 2
 GATE = dict(XOR=0, NXOR=1, AND=2, OR=3, NOR=4, NA_AND=5, COPY=6, INV=7)
-PROBE_GEMM, PROBE_EPILOGUE, PROBE_BINARY, PROBE_AES, PROBE_OTHER = range(5)
+PROBE_GEMM, PROBE_EPILOGUE, PROBE_BINARY, PROBE_AES, PROBE_OTHER, PROBE_DIGITS = range(6)
 
 
 class ZeroShare(ctypes.Structure):
@@ -104,6 +104,8 @@ _SIGS = {
     "aby3g_wires_to_bits": (c_int, [c_void_p, c_void_p, c_uint32, c_uint64, c_void_p, c_uint64, c_void_p]),
     "aby3g_i64_lincomb": (c_int, [c_uint64, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
     "aby3g_u64_bitop": (c_int, [c_int, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "aby3g_i64_gather_rows": (c_int, [c_void_p, c_uint64, c_uint64, c_void_p, c_uint64, c_void_p, c_void_p]),
+    "aby3g_i64_transpose": (c_int, [c_void_p, c_uint64, c_uint64, c_void_p, c_void_p]),
     "aby3g_u64_gather": (c_int, [c_uint64, c_void_p, c_void_p, c_void_p, c_void_p]),
     "aby3g_u64_scatter": (c_int, [c_uint64, c_void_p, c_void_p, c_void_p, c_void_p]),
 }
@@ -140,6 +142,117 @@ class _Lib:
             return rc
 
         return call
+
+
+JOB_MUL_TRUNC, JOB_MUL, JOB_MSB, JOB_LR, JOB_MERGE_LAYER = range(5)
+INFO = dict(mults_per_step=0, gemm_int8_ops=1, and_words=2, gate_words=3, gate_bytes=4, bytes_sent=5)
+
+_HOST_SIGS = {
+    "aby3h_last_error": (c_char_p, []),
+    "aby3h_session_create": (c_void_p, [c_int, POINTER(c_uint64), c_int, POINTER(c_int), c_int]),
+    "aby3h_session_run": (c_int, [c_void_p, c_uint64]),
+    "aby3h_session_probe": (c_int, [c_void_p, c_int, POINTER(c_double), POINTER(c_uint64)]),
+    "aby3h_session_probe_reset": (c_int, [c_void_p]),
+    "aby3h_session_info": (c_int, [c_void_p, POINTER(c_double), c_int]),
+    "aby3h_session_check": (c_int, [c_void_p]),
+    "aby3h_session_destroy": (None, [c_void_p]),
+    "aby3h_circuit": (c_int, [c_char_p, c_uint64, c_uint64, POINTER(c_uint64), c_void_p, c_void_p, c_void_p,
+                              c_void_p, c_void_p, c_void_p]),
+}
+
+_host = None
+
+
+def host():
+    """The C++ host runtime (include/aby3.h)."""
+    global _host
+    if _host is None:
+        lib()  # the GPU library must load first (libaby3.so links it)
+        if not os.path.exists(HOST_LIB):
+            raise NativeError(f"{HOST_LIB} missing: run `make`")
+        d = ctypes.CDLL(HOST_LIB)
+        for name, (res, args) in _HOST_SIGS.items():
+            fn = getattr(d, name)
+            fn.restype = res
+            fn.argtypes = args
+        _host = d
+    return _host
+
+
+class Session:
+    """Three in-process parties running one job of the hot path (include/aby3.h)."""
+
+    def __init__(self, job: int, params, devices=(0, 0, 0), probe: bool = True):
+        h = host()
+        p = (c_uint64 * len(params))(*params)
+        dv = (c_int * 3)(*devices)
+        self._h = h.aby3h_session_create(job, p, len(params), dv, int(probe))
+        if not self._h:
+            raise NativeError("aby3h_session_create: " + h.aby3h_last_error().decode())
+        self.host = h
+
+    def run(self, steps: int):
+        if self.host.aby3h_session_run(self._h, steps) != 0:
+            raise NativeError("aby3h_session_run: " + self.host.aby3h_last_error().decode())
+
+    def probe(self, family: int):
+        ms, n = c_double(), c_uint64()
+        if self.host.aby3h_session_probe(self._h, family, ctypes.byref(ms), ctypes.byref(n)) != 0:
+            raise NativeError("aby3h_session_probe: " + self.host.aby3h_last_error().decode())
+        return ms.value, n.value
+
+    def probe_reset(self):
+        self.host.aby3h_session_probe_reset(self._h)
+
+    def info(self) -> dict:
+        out = (c_double * 6)()
+        self.host.aby3h_session_info(self._h, out, 6)
+        return {k: out[v] for k, v in INFO.items()}
+
+    def check(self) -> bool:
+        rc = self.host.aby3h_session_check(self._h)
+        if rc == 2:
+            raise NativeError("aby3h_session_check: " + self.host.aby3h_last_error().decode())
+        return rc == 0
+
+    def close(self):
+        if self._h:
+            self.host.aby3h_session_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def circuit(name: str, size: int = 64, param: int = 0) -> dict:
+    """A library circuit as flat arrays (levelized gate list), CPU only."""
+    import numpy as np
+
+    h = host()
+    counts = (c_uint64 * 6)()
+    if h.aby3h_circuit(name.encode(), size, param, counts, None, None, None, None, None, None) != 0:
+        raise NativeError(h.aby3h_last_error().decode())
+    wires, ngates, nlev, nin, nout, _ = list(counts)
+    gates = np.zeros(4 * ngates, dtype=np.uint32)
+    levels = np.zeros(nlev, dtype=np.uint32)
+    insz = np.zeros(nin, dtype=np.uint32)
+    outsz = np.zeros(nout, dtype=np.uint32)
+    inw = np.zeros(counts[5], dtype=np.uint32)
+    outw = np.zeros(counts[5], dtype=np.uint32)
+    P = lambda a: a.ctypes.data_as(c_void_p)
+    h.aby3h_circuit(name.encode(), size, param, counts, P(gates), P(levels), P(insz), P(inw), P(outsz), P(outw))
+    ins, outs, o = [], [], 0
+    for s in insz:
+        ins.append(inw[o:o + s].tolist())
+        o += s
+    o = 0
+    for s in outsz:
+        outs.append(outw[o:o + s].tolist())
+        o += s
+    return dict(wires=int(wires), gates=gates.reshape(-1, 4), levels=levels, inputs=ins, outputs=outs)
 
 
 _lib = None

@@ -1,0 +1,235 @@
+#!/usr/bin/env python3
+"""Benchmark of the ABY3 replicated-secret-sharing hot path on MI355X.
+
+Workload (BASELINE.json configs[1]): Sh3Evaluator::asyncMul on 1024x1024
+sf64Matrix shares with truncation (D16), upstream GEMM semantics, three
+parties. On each GPU the three parties run co-located (three host threads,
+three HIP streams, device-to-device channels); with --gpus N every rank runs
+its own independent 3-party job on its own GPU (weak scaling, no data-path
+collective: each rank's multiplications are independent units of work).
+
+One step = one complete 3-party asyncMul + truncation: every party's digit
+split + int8-MFMA share GEMM, truncation pair (AES-CTR on device), the z
+messages to P0/P1 and the finalize. `value` = secret-shared 64-bit mults
+(M*N*K product terms per multiplication) completed per second by the whole
+job; the metric is quoted "per party" because every party takes part in
+every multiplication.
+
+The JSON line also carries:
+  roofline      -- the share-GEMM kernel: int8 MFMA ops per launch
+                   (144*M*N*K) / its average launch time,
+                   measured with HIP events on the party streams, vs the
+                   gfx950 dense int8 peak; `traffic` from the committed PMC
+                   profile when one matches (profiles/pmc_*.json);
+  binary        -- the binary-AND side of the metric (config C3): cipher_gt
+                   (reshare + MSB(a+b) circuit) over 2^20 rows, AND
+                   word-gates/s and the gate-kernel HBM roofline;
+  cpu_baseline  -- the CPU restatement (oracle/, kind "port") of the same
+                   multiplication on this host, 3 party threads.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_INT8_TOPS = 256 * 4 * 2048 * 2.4e9 / 1e12  # 256 CU x 4 SIMD x 2048 int8 op/clk x 2.4 GHz = 5033 TOP/s
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--m", type=int, default=1024)
+    ap.add_argument("--k", type=int, default=1024)
+    ap.add_argument("--n", type=int, default=1024)
+    ap.add_argument("--decimal", type=int, default=16)
+    ap.add_argument("--binary-rows", type=int, default=1 << 20)
+    ap.add_argument("--binary-steps", type=int, default=5)
+    ap.add_argument("--no-binary", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-reps", type=int, default=4)
+    return ap.parse_args()
+
+
+def dist_setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # control plane only (barrier, max over ranks): no data crosses ranks
+        dist.init_process_group(backend="gloo")
+        pg = dist
+    return world, rank, local, pg
+
+
+def barrier(pg):
+    if pg is not None:
+        pg.barrier()
+
+
+def allmax(pg, x: float) -> float:
+    if pg is None:
+        return x
+    import torch
+
+    t = torch.tensor([x], dtype=torch.float64)
+    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    return float(t.item())
+
+
+def load_pmc(kind: str, cfg: dict):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary, if it matches."""
+    import glob
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        e = d.get(kind)
+        if e and e.get("config") == cfg:
+            best = e.get("hbm_bytes_per_launch")
+    return best
+
+
+def main():
+    args = parse()
+    world, rank, local, pg = dist_setup()
+    from aby3_amd import native as nt
+
+    dev = local
+    M, K, N, D = args.m, args.k, args.n, args.decimal
+    sess = nt.Session(nt.JOB_MUL_TRUNC, [M, K, N, D, 1], devices=(dev, dev, dev), probe=True)
+    sess.run(args.warmup)
+    if not sess.check():
+        raise SystemExit("bench: revealed product does not match the plaintext")
+    sess.probe_reset()
+    barrier(pg)
+    t0 = time.perf_counter()
+    sess.run(args.steps)  # returns after every party stream drained
+    t1 = time.perf_counter()
+    barrier(pg)
+    dt = allmax(pg, t1 - t0)
+    info = sess.info()
+    gemm_ms, gemm_n = sess.probe(nt.PROBE_GEMM)
+    dig_ms, _ = sess.probe(nt.PROBE_DIGITS)
+    epi_ms, _ = sess.probe(nt.PROBE_EPILOGUE)
+    sess.close()
+
+    mults = info["mults_per_step"]
+    value = world * args.steps * mults / dt
+    gemm_avg_s = gemm_ms / max(gemm_n, 1) / 1e3
+    achieved_tops = info["gemm_int8_ops"] / gemm_avg_s / 1e12 if gemm_avg_s > 0 else 0.0
+    cfg = {"m": M, "k": K, "n": N}
+    traffic = load_pmc("share_gemm", cfg)
+    out = {
+        "metric": "secret-shared 64-bit mults/sec (matmul + binary-AND) per party, 3 parties on 3 MI355X",
+        "value": value,
+        "unit": "mults/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic: fixed-point operands round(U[-8,8) * 2^16), shared by party 0",
+        "config": {
+            "workload": f"sf64Matrix asyncMul + truncation {M}x{K} . {K}x{N} (D{D}), upstream GEMM semantics, "
+                        "3 parties co-located per GPU",
+            "parties_per_gpu": 3,
+            "global_batch": world,
+            "parallelism": f"replicas{world}",
+        },
+        "roofline": {
+            "bound": "mfma",
+            "kernel": "k_share_gemm (int8 MFMA 32x32x32, 36 digit-pair planes)",
+            "achieved": achieved_tops,
+            "peak": PEAK_INT8_TOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved_tops / PEAK_INT8_TOPS,
+            "traffic": traffic,
+            "launch_ms": gemm_avg_s * 1e3,
+            "ops_per_launch": info["gemm_int8_ops"],
+        },
+        "kernel_ms_per_step": {
+            "share_gemm": gemm_ms / args.steps,
+            "digit_planes": dig_ms / args.steps,
+            "trunc_epilogue": epi_ms / args.steps,
+        },
+    }
+
+    if not args.no_binary:
+        bs = nt.Session(nt.JOB_MSB, [args.binary_rows], devices=(dev, dev, dev), probe=True)
+        bs.run(1)
+        if not bs.check():
+            raise SystemExit("bench: binary MSB result does not match the plaintext")
+        bs.probe_reset()
+        barrier(pg)
+        b0 = time.perf_counter()
+        bs.run(args.binary_steps)
+        b1 = time.perf_counter()
+        barrier(pg)
+        bdt = allmax(pg, b1 - b0)
+        binfo = bs.info()
+        gate_ms, gate_n = bs.probe(nt.PROBE_BINARY)
+        bs.close()
+        gate_s = gate_ms / 3 / args.binary_steps / 1e3  # per party per step
+        gbs = binfo["gate_bytes"] / gate_s / 1e9 if gate_s > 0 else 0.0
+        out["binary"] = {
+            "workload": f"cipher_gt / fetch_msb over {args.binary_rows} rows (MSB(a+b) circuit), 3 parties",
+            "value": world * args.binary_steps * binfo["and_words"] / bdt,
+            "unit": "AND word-gates/s (1 AND-type gate on one 64-row word)",
+            "ms_per_step": bdt / args.binary_steps * 1e3,
+            "and_words_per_step": binfo["and_words"],
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_bin_gates + k_bin_unpack",
+                "achieved": gbs,
+                "peak": PEAK_HBM_GBS,
+                "unit": "GB/s",
+                "frac": gbs / PEAK_HBM_GBS,
+                "traffic": load_pmc("bin_gates", {"rows": args.binary_rows}),
+                "bytes_per_step_per_party": binfo["gate_bytes"],
+            },
+        }
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import ctypes
+
+        orc = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "liborc.so"))
+        orc.orc_bench_mul_trunc.restype = ctypes.c_double
+        reps = args.cpu_reps
+        secs = orc.orc_bench_mul_trunc(1, M, K, N, D, reps)
+        out["cpu_baseline"] = {
+            "value": reps * M * N * K / secs,
+            "unit": "mults/s",
+            "cores": 3,
+            "kind": "port",
+            "sample": f"{reps} x asyncMul+trunc {M}x{K}x{N}: three scalar i64 GEMMs (Eigen-style, "
+                      "reference Release flags) + AES-NI truncation pair per party, 3 party threads",
+            "cpu": open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].strip(": \t")
+            if os.path.exists("/proc/cpuinfo") else "unknown",
+        }
+        out["speedup_vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
+
+    if rank == 0:
+        print(json.dumps(out))
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

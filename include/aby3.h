@@ -1,0 +1,82 @@
+/*
+ * aby3.h -- C entry points of the host runtime (aby3_amd/lib/libaby3.so),
+ * for drivers that are not C++ (bench.py, the Python tests, a cgo/ctypes
+ * binding). The C++ API itself is aby3_amd/host/*.h (namespace aby3),
+ * mirroring the reference's Sh3Runtime / Sh3Encryptor / Sh3Evaluator /
+ * Sh3BinaryEvaluator / Sh3Piecewise classes.
+ *
+ * A session runs the three ABY3 parties as three persistent host threads of
+ * this process, each with its own Sh3Runtime, HIP stream and device (party i
+ * on devices[i]; all three may share one GPU), connected by in-process
+ * device channels. aby3h_session_run(s, k) executes k protocol steps of the
+ * session's job on all parties and returns when every party's stream has
+ * drained, so the caller can bracket exactly k steps with its own clock.
+ */
+#ifndef ABY3_H
+#define ABY3_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct aby3h_session aby3h_session;
+
+enum {
+    /* params: M, K, N, D, mode (1 GEMM, 0 Hadamard). One step = one
+     * Sh3Evaluator::asyncMul(A, B, C, D) with truncation (Sh3Evaluator.cpp:651-730). */
+    ABY3H_JOB_MUL_TRUNC = 0,
+    /* params: M, K, N, mode. One step = asyncMul without truncation (:92-116). */
+    ABY3H_JOB_MUL = 1,
+    /* params: rows. One step = cipher_gt / fetch_msb over `rows` 64-bit
+     * values: reshare + MSB(a+b) circuit (BuildingBlocks.cpp:464-532). */
+    ABY3H_JOB_MSB = 2,
+    /* params: rows (dataset), dim, batch, D, lr_log2. One step = one
+     * SGD_Logistic iteration (aby3-ML/Regression.h:249-293): xw = X_B w,
+     * sigmoid (Sh3Piecewise), err = f - Y_B, w -= X_B^T err >> (D + aB). */
+    ABY3H_JOB_LR = 3,
+    /* params: keys. One step = one compare-exchange layer of keys/2 pairs
+     * of the merge network (Sort.cpp:366-398, fused cmp_swap circuit). */
+    ABY3H_JOB_MERGE_LAYER = 4
+};
+
+/* info slots returned by aby3h_session_info */
+enum {
+    ABY3H_INFO_MULTS_PER_STEP = 0,    /* secret-shared 64-bit mults per step (metric unit) */
+    ABY3H_INFO_GEMM_INT8_OPS = 1,     /* int8 MFMA ops per GEMM launch (144 M N K) */
+    ABY3H_INFO_AND_WORDS = 2,         /* AND-type gates x 64-row words per step */
+    ABY3H_INFO_GATE_WORDS = 3,        /* all gates x words per step */
+    ABY3H_INFO_GATE_BYTES = 4,        /* algorithmic HBM bytes of the gate kernels per step */
+    ABY3H_INFO_BYTES_SENT = 5,        /* bytes sent by party 0 per step */
+    ABY3H_INFO_COUNT = 6
+};
+
+const char* aby3h_last_error(void);
+
+aby3h_session* aby3h_session_create(int job, const uint64_t* params, int nparams, const int* devices, int probe);
+int aby3h_session_run(aby3h_session* s, uint64_t steps);
+/* kernel time (ms) and launches of a probe family (aby3gpu.h), summed over parties */
+int aby3h_session_probe(aby3h_session* s, int family, double* ms, uint64_t* launches);
+int aby3h_session_probe_reset(aby3h_session* s);
+int aby3h_session_info(aby3h_session* s, double* out, int n);
+/* reveals the last step's result and checks it against plaintext; 0 = ok */
+int aby3h_session_check(aby3h_session* s);
+void aby3h_session_destroy(aby3h_session* s);
+
+/* A library circuit, levelized, as flat arrays (for CPU tests and external
+ * evaluators). name: "int_comp_helper", "int_int_lt", "int_eq", "int_int_add",
+ * "int_int_sub", "int_int_bitwiseAnd", "int_int_bitwiseOr", "bits_nor_helper",
+ * "cmp_swap", "int_Sh3Piecewise_helper" (param = thresholds).
+ * Call with NULL buffers to get the sizes (counts[0..5] = wires, gates,
+ * levels, input bundles, output bundles, total bundle wires); gates are
+ * 4 x u32 {in0, in1, out, type} in evaluation order. */
+int aby3h_circuit(const char* name, uint64_t size, uint64_t param, uint64_t counts[6], uint32_t* gates,
+                  uint32_t* level_counts, uint32_t* in_sizes, uint32_t* in_wires, uint32_t* out_sizes,
+                  uint32_t* out_wires);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ABY3_H */

@@ -241,6 +241,13 @@ int aby3g_i64_lincomb(uint64_t n, int64_t ca, const int64_t* a, int64_t cb, cons
 /* Bitwise ops on u64 vectors: 0 xor, 1 and, 2 not(a), 3 lsb-to-mask (-(a&1)),
  * 4 copy. b may be NULL for unary ops. */
 int aby3g_u64_bitop(int op, uint64_t n, const uint64_t* a, const uint64_t* b, uint64_t* out, aby3g_stream stream);
+/* Row gather of a [2][rows][cols] share matrix: dst[s][i][:] = src[s][idx[i]][:]
+ * (extractBatch, aby3-ML/Regression.h:42-58); dst is [2][n][cols]. */
+int aby3g_i64_gather_rows(const int64_t* src, uint64_t rows, uint64_t cols, const uint32_t* idx, uint64_t n,
+                          int64_t* dst, aby3g_stream stream);
+/* Transpose of both shares: dst[s] = src[s]^T, src [2][rows][cols] -> dst [2][cols][rows]
+ * (sMatrix::transpose / transposeInPlace, Sh3Types.h:198-271). */
+int aby3g_i64_transpose(const int64_t* src, uint64_t rows, uint64_t cols, int64_t* dst, aby3g_stream stream);
 /* dst[i] = src[idx[i]] (gather) and dst[idx[i]] = src[i] (scatter), u64. */
 int aby3g_u64_gather(uint64_t n, const uint32_t* idx, const uint64_t* src, uint64_t* dst, aby3g_stream stream);
 int aby3g_u64_scatter(uint64_t n, const uint32_t* idx, const uint64_t* src, uint64_t* dst, aby3g_stream stream);

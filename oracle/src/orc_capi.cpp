@@ -3,6 +3,8 @@
 #include "orc_core.h"
 #include <cstring>
 #include <string>
+#include <chrono>
+#include <thread>
 
 using namespace orc;
 
@@ -280,6 +282,51 @@ int orc_sim_fetch_msb(uint32_t wires, const uint32_t* gates, uint64_t ngates, co
         Mat m = revealBin(r);
         memcpy(out_plain, m.v.data(), 8 * n);
     });
+}
+
+// CPU baseline of asyncMul + truncation (bench.py cpu_baseline): the three
+// parties' round-1 local compute (three scalar i64 GEMMs as Eigen evaluates
+// A0*B0 + A0*B1 + A1*B0, Sh3Evaluator.cpp:662-665, plus the truncation tuple
+// from AES-NI PRNG streams) run concurrently, one thread per party like the
+// reference's one compute thread per party process, followed by the round-2
+// finalize of P0/P1. Returns wall seconds for `reps` multiplications.
+double orc_bench_mul_trunc(int mode, uint64_t M, uint64_t K, uint64_t N, uint64_t d, int reps) {
+    try {
+        auto ev = makeEvaluators(1);
+        std::array<SMat, 3> A, B;
+        u64 x = 42;
+        auto rnd = [&](SMat& m, u64 r, u64 c) {
+            m = SMat(r, c);
+            for (int s = 0; s < 2; ++s)
+                for (auto& v : m.s[s].v) {
+                    x ^= x << 13;
+                    x ^= x >> 7;
+                    x ^= x << 17;
+                    v = (i64)x;
+                }
+        };
+        for (int p = 0; p < 3; ++p) {
+            rnd(A[p], M, K);
+            rnd(B[p], mode == MUL_GEMM ? K : M, mode == MUL_GEMM ? N : K);
+        }
+        auto t0 = std::chrono::steady_clock::now();
+        for (int r = 0; r < reps; ++r) {
+            std::array<Mat, 3> z;
+            std::array<SMat, 3> C;
+            std::vector<std::thread> th;
+            for (int p = 0; p < 3; ++p)
+                th.emplace_back([&, p] { mulTruncLocal(ev[p], (MulMode)mode, A[p], B[p], d, z[p], C[p]); });
+            for (auto& t : th) t.join();
+            Mat s = z[0];
+            for (u64 k = 0; k < s.size(); ++k) s.v[k] = (i64)((u64)z[0].v[k] + (u64)z[1].v[k] + (u64)z[2].v[k]);
+            for (int p = 0; p < 2; ++p) truncFinalize(p, s, d, C[p]);
+        }
+        auto t1 = std::chrono::steady_clock::now();
+        return std::chrono::duration<double>(t1 - t0).count();
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return -1;
+    }
 }
 
 }  // extern "C"

@@ -1,0 +1,87 @@
+"""The product's circuit library (exported by libaby3.so, CPU) evaluated by
+the oracle's 3-party binary engine: revealed semantics of every circuit the
+hot path uses, plus piecewise and fetch_msb at the revealed level.
+Anchors: Sh3BinaryEvaluatorTests.cpp:333-424, CircuitTests.cpp:16-81,
+Sh3PiecewiseTests.cpp:13-83, BuildingBlocks.cpp:464-532. CPU only."""
+import numpy as np
+import pytest
+
+import oracle as orc
+from aby3_amd import native as nt
+
+
+def _vals(n, seed, bits=64):
+    rng = np.random.default_rng(seed)
+    v = rng.integers(-(2**63), 2**63 - 1, size=n, dtype=np.int64, endpoint=True)
+    v[:6] = [0, -1, 2**63 - 1, -(2**63), 1, 5]
+    if bits < 64:
+        v &= (1 << bits) - 1
+    return v
+
+
+CASES = [
+    ("int_comp_helper", 64, lambda a, b: ((a.view(np.uint64) + b.view(np.uint64)) >> np.uint64(63)).view(np.int64)),
+    ("int_int_lt", 64, lambda a, b: (a < b).astype(np.int64)),
+    ("int_eq", 64, lambda a, b: (a == b).astype(np.int64)),
+    ("int_int_add", 64, lambda a, b: (a.view(np.uint64) + b.view(np.uint64)).view(np.int64)),
+    ("int_int_sub", 64, lambda a, b: (a.view(np.uint64) - b.view(np.uint64)).view(np.int64)),
+    ("int_int_bitwiseAnd", 64, lambda a, b: a & b),
+    ("int_int_bitwiseOr", 64, lambda a, b: a | b),
+    ("int_int_add", 8, lambda a, b: (a + b) & 0xFF),
+    ("int_int_bitwiseAnd", 8, lambda a, b: a & b),
+]
+
+
+@pytest.mark.parametrize("name,bits,f", CASES)
+@pytest.mark.parametrize("rows", [1, 256, 2100])
+def test_circuit_revealed(name, bits, f, rows):
+    cir = nt.circuit(name, bits)
+    a, b = _vals(rows, 1, bits), _vals(rows, 2, bits)
+    if rows > 5:
+        b[5] = a[5]  # an equal pair
+    out = orc.sim_circuit(cir, rows, [a, b])
+    assert np.array_equal(out[0][:, 0], f(a, b))
+
+
+def test_cmp_swap_revealed():
+    cir = nt.circuit("cmp_swap", 64)
+    a, b = _vals(300, 3), _vals(300, 4)
+    mn, mx = orc.sim_circuit(cir, 300, [a, b])
+    assert np.array_equal(mn[:, 0], np.minimum(a, b))
+    assert np.array_equal(mx[:, 0], np.maximum(a, b))
+
+
+def test_levels_and_masks_consistent():
+    # every AND-type gate consumes one z row; level counts cover the gate list
+    cir = nt.circuit("int_comp_helper", 64)
+    assert int(cir["levels"].sum()) == len(cir["gates"])
+    n_and = int(np.isin(cir["gates"][:, 3], [2, 3, 4, 5]).sum())
+    assert n_and > 0
+
+
+@pytest.mark.parametrize("D", [8, 16])
+def test_piecewise_sigmoid(D):
+    cir = nt.circuit("int_Sh3Piecewise_helper", 64, 2)
+    x = np.linspace(-2.0, 2.0, 257)
+    xf = (x * (1 << D)).astype(np.int64)
+    _, plain = orc.sim_piecewise(0, cir, xf, D)
+    got = plain / float(1 << D)
+    exp = np.where(x < -0.5, 0.0, np.where(x < 0.5, 0.5 + xf / float(1 << D), 1.0))
+    assert np.max(np.abs(got - exp)) <= 2.0**-D
+
+
+def test_piecewise_relu():
+    cir = nt.circuit("int_Sh3Piecewise_helper", 64, 1)
+    D = 16
+    xf = np.arange(-300, 300, 7, dtype=np.int64) * 1000
+    _, plain = orc.sim_piecewise(1, cir, xf, D)
+    assert np.array_equal(plain, np.maximum(xf, 0))
+
+
+def test_fetch_msb_cipher_gt():
+    cir = nt.circuit("int_comp_helper", 64)
+    n = 16
+    a = np.arange(n, dtype=np.int64)
+    b = n - a
+    gt = orc.sim_fetch_msb(cir, a, b)  # Test.cpp:74-191 res_gt = i > 16 - i
+    assert np.array_equal(gt & 1, (a > b).astype(np.int64))

@@ -1,0 +1,35 @@
+"""Runs the C++ test programs (built by `make tests`): the scheduler contract
+and the circuit library on CPU; the 3-party protocol parity suites on GPU."""
+import os
+import subprocess
+
+import pytest
+
+BUILD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "cpp", "build")
+
+
+def _run(name, timeout):
+    exe = os.path.join(BUILD, name)
+    assert os.path.exists(exe), f"{exe} missing: run `make tests`"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=timeout)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "FAIL" not in r.stdout
+
+
+def test_runtime_schedule():
+    _run("test_runtime", 60)
+
+
+def test_circuit_library_plaintext():
+    _run("test_circuits", 120)
+
+
+@pytest.mark.gpu
+def test_arith_protocols_gpu():
+    _run("test_arith", 600)
+
+
+@pytest.mark.gpu
+def test_binary_protocols_gpu():
+    _run("test_binary", 600)

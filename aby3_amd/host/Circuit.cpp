@@ -335,4 +335,18 @@ BetaCircuit* CircuitLibrary::cmp_swap(u64 size) {
     });
 }
 
+BetaCircuit* CircuitLibrary::byName(const std::string& n, u64 size, u64 param) {
+    if (n == "int_comp_helper") return int_comp_helper(size);
+    if (n == "int_int_lt") return int_int_lt(size);
+    if (n == "int_eq") return int_eq(size);
+    if (n == "int_int_add") return int_int_add(size);
+    if (n == "int_int_sub") return int_int_sub(size);
+    if (n == "int_int_bitwiseAnd") return int_int_bitwiseAnd(size);
+    if (n == "int_int_bitwiseOr") return int_int_bitwiseOr(size);
+    if (n == "bits_nor_helper") return bits_nor_helper(size);
+    if (n == "cmp_swap") return cmp_swap(size);
+    if (n == "int_Sh3Piecewise_helper") return int_Sh3Piecewise_helper(size, param);
+    throw std::runtime_error("unknown circuit " + n);
+}
+
 }  // namespace aby3

@@ -90,6 +90,10 @@ public:
     // (bool_cipher_max_min_split, BoolBasic.cpp:275-312, fused into one circuit)
     BetaCircuit* cmp_swap(u64 size);
 
+    // any of the above by its name (param = thresholds for the piecewise helper);
+    // throws std::runtime_error for an unknown name
+    BetaCircuit* byName(const std::string& name, u64 size, u64 param = 0);
+
 private:
     std::map<std::pair<std::string, u64>, std::unique_ptr<BetaCircuit>> mCirMap;
     BetaCircuit* get(const std::string& name, u64 key);

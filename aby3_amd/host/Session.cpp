@@ -1,6 +1,7 @@
 // C entry points (include/aby3.h): three persistent party threads running a
 // job of the hot path, for bench.py and the Python tests.
 #include <aby3.h>
+#include <algorithm>
 #include <atomic>
 #include <cmath>
 #include <condition_variable>
@@ -212,12 +213,36 @@ struct LrJob : Job {
         std::vector<u32> idx(perm.begin() + start, perm.begin() + start + B);
         sgdLogisticStep(*ml[p.idx], sX[p.idx], sY[p.idx], sW[p.idx], idx, aB, st[p.idx]);
     }
+    // plaintext fixed-point restatement of the same iterations (floor shifts as
+    // Sh3FixedPoint.h:200-210, the sigmoid of aby3ML.h:121-139); the protocol's
+    // truncation error is a few ulps per product, so the revealed model must
+    // agree to 2^-10 per iteration
     bool check(PartyCtx& p) override {
         i64Matrix r;
         p.enc.revealAll(p.rt, sW[p.idx], r).get();
         if (p.idx != 0) return true;
-        for (auto v : r.mData)
-            if (std::abs(fromFixed(v, D)) > 1e6) return false;
+        std::vector<i64> w(w0.mData);
+        const i64 half = 1ll << (D - 1), one = 1ll << D;
+        for (u64 t = 0; t < iter[0]; ++t) {
+            const u64 start = (t * B) % (n - B + 1);
+            std::vector<i64> err(B);
+            for (u64 i = 0; i < B; ++i) {
+                const u64 row = perm[start + i];
+                i64 xw = 0;
+                for (u64 j = 0; j < d; ++j) xw += X(row, j) * w[j];
+                xw >>= D;
+                const i64 f = xw < -half ? 0 : (xw < half ? half + xw : one);
+                err[i] = f - Y(row, 0);
+            }
+            for (u64 j = 0; j < d; ++j) {
+                i64 u = 0;
+                for (u64 i = 0; i < B; ++i) u += X(perm[start + i], j) * err[i];
+                w[j] -= u >> (D + aB);
+            }
+        }
+        const double tol = (double)(iter[0] + 1) / 1024.0;
+        for (u64 j = 0; j < d; ++j)
+            if (std::abs(fromFixed(r.mData[j], D) - fromFixed(w[j], D)) > tol) return false;
         return true;
     }
     void info(double* o) override { o[ABY3H_INFO_MULTS_PER_STEP] = 2.0 * B * d; }
@@ -230,6 +255,7 @@ struct MergeLayerJob : Job {
     sbMatrix S[3], X[3], Y[3], Mn[3], Mx[3];
     CircuitLibrary lib;
     std::vector<u32> xi, yi;
+    DeviceBuffer dx[3], dy[3];
     explicit MergeLayerJob(u64 n) : keys(n) {
         k.resize(keys, 1);
         u64 x = 7;
@@ -245,13 +271,18 @@ struct MergeLayerJob : Job {
             p.enc.localBinMatrix(p.rt, k, S[0]).get();
         else
             p.enc.remoteBinMatrix(p.rt, S[p.idx]).get();
+        Gpu& g = p.rt.gpu();
+        const u64 m = xi.size();
+        dx[p.idx].reset(g, m * 4);
+        dy[p.idx].reset(g, m * 4);
+        toDevice(dx[p.idx].data(), xi.data(), m * 4, g);
+        toDevice(dy[p.idx].data(), yi.data(), m * 4, g);
+        g.sync();
     }
     void step(PartyCtx& p) override {
         Gpu& g = p.rt.gpu();
         const u64 m = xi.size();
-        DeviceBuffer dx(g, m * 4), dy(g, m * 4);
-        toDevice(dx.data(), xi.data(), m * 4, g);
-        toDevice(dy.data(), yi.data(), m * 4, g);
+        DeviceBuffer &dx = this->dx[p.idx], &dy = this->dy[p.idx];
         sbMatrix &s = S[p.idx], &x = X[p.idx], &y = Y[p.idx];
         x.resize(m, 64);
         y.resize(m, 64);
@@ -264,6 +295,19 @@ struct MergeLayerJob : Job {
             GPU_CALL(aby3g_u64_scatter(m, dx.as<u32>(), (const u64*)Mn[p.idx].share(sh), (u64*)s.share(sh), g.stream()));
             GPU_CALL(aby3g_u64_scatter(m, dy.as<u32>(), (const u64*)Mx[p.idx].share(sh), (u64*)s.share(sh), g.stream()));
         }
+    }
+    // after any number of layers over the same pairs: every pair ordered
+    // (signed), and the keys a permutation of the input (the layer is idempotent)
+    bool check(PartyCtx& p) override {
+        i64Matrix r;
+        p.enc.revealAll(p.rt, S[p.idx], r).get();
+        if (p.idx != 0) return true;
+        for (u64 i = 0; i < xi.size(); ++i)
+            if (r(xi[i], 0) > r(yi[i], 0)) return false;
+        std::vector<i64> a(r.mData), b(k.mData);
+        std::sort(a.begin(), a.end());
+        std::sort(b.begin(), b.end());
+        return a == b;
     }
     void info(double* o) override {
         BetaCircuit* c = lib.cmp_swap(64);
@@ -489,19 +533,7 @@ int aby3h_circuit(const char* name, uint64_t size, uint64_t param, uint64_t coun
                   uint32_t* out_wires) {
     try {
         CircuitLibrary lib;
-        std::string n(name);
-        BetaCircuit* c = nullptr;
-        if (n == "int_comp_helper") c = lib.int_comp_helper(size);
-        else if (n == "int_int_lt") c = lib.int_int_lt(size);
-        else if (n == "int_eq") c = lib.int_eq(size);
-        else if (n == "int_int_add") c = lib.int_int_add(size);
-        else if (n == "int_int_sub") c = lib.int_int_sub(size);
-        else if (n == "int_int_bitwiseAnd") c = lib.int_int_bitwiseAnd(size);
-        else if (n == "int_int_bitwiseOr") c = lib.int_int_bitwiseOr(size);
-        else if (n == "bits_nor_helper") c = lib.bits_nor_helper(size);
-        else if (n == "cmp_swap") c = lib.cmp_swap(size);
-        else if (n == "int_Sh3Piecewise_helper") c = lib.int_Sh3Piecewise_helper(size, param);
-        else throw std::runtime_error("unknown circuit " + n);
+        BetaCircuit* c = lib.byName(name, size, param);
         u64 inW = 0, outW = 0;
         for (auto& b : c->mInputs) inW += b.size();
         for (auto& b : c->mOutputs) outW += b.size();

@@ -95,6 +95,25 @@ void Sh3BinaryEvaluator::setInput(u64 i, const sbMatrix& in) {
     mLevel = 0;
 }
 
+void Sh3BinaryEvaluator::setReplicatedInput(u64 i, const sbMatrix& in) {
+    if (!mCir) throw RTE_LOC;
+    if (i >= mCir->mInputs.size()) throw std::invalid_argument("input index out of bounds");
+    const auto& wires = mCir->mInputs[i];
+    if (in.bitCount() != wires.size()) throw std::invalid_argument("input data wrong size");
+    if (in.rows() != 1) throw std::invalid_argument("incorrect number of simd rows");
+    Gpu& g = *mGpu;
+    const u64 W = mCir->mWireCount;
+    for (int s = 0; s < 2; ++s) {
+        // every row of wire j takes bit j of the single input row: all-zero or all-one words
+        const std::vector<i64> row = in.shareToHost(s);
+        for (size_t j = 0; j < wires.size(); ++j) {
+            const int v = ((u64)row[j / 64] >> (j % 64)) & 1 ? 0xff : 0;
+            GPU_CALL(aby3g_memset(mMem.as<u64>() + ((u64)s * W + wires[j]) * mWords, v, mWords * 8, g.stream()));
+        }
+    }
+    mLevel = 0;
+}
+
 void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
     if (mLevel > mCir->mLevelCounts.size())
         throw std::runtime_error("evaluateRound() was called but no rounds remain... " LOCATION);

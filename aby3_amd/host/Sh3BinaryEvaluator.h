@@ -24,6 +24,8 @@ public:
     void setCir(BetaCircuit* cir, u64 width, Sh3ShareGen& gen);
     void setCir(BetaCircuit* cir, u64 width, block prevSeed, block nextSeed);
     void setInput(u64 i, const sbMatrix& in);
+    // a one-row shared input broadcast to every row (Sh3BinaryEvaluator.cpp:105-138)
+    void setReplicatedInput(u64 i, const sbMatrix& in);
     Sh3Task asyncEvaluate(Sh3Task dep);
     Sh3Task asyncEvaluate(Sh3Task dep, BetaCircuit* cir, Sh3ShareGen& gen, std::vector<const sbMatrix*> inputs,
                           std::vector<sbMatrix*> outputs);

@@ -1,0 +1,249 @@
+// aby3h_sim_* (include/aby3.h): one protocol call run by three in-process
+// parties on one GPU, in the topology and with the seeds of the reference's
+// unit tests (Sh3EvaluatorTests.cpp:23-131: encryptor toBlock(0, i),
+// evaluator toBlock(1, i)), party 0 owning the inputs. Every party's two
+// shares and the revealed result come back to the host, so a test can hold
+// them against committed fixtures share by share.
+#include <aby3.h>
+#include <cstring>
+#include <exception>
+#include <thread>
+#include "Basic.h"
+#include "Sh3Piecewise.h"
+
+namespace aby3 {
+namespace {
+
+thread_local std::string t_simErr;
+
+struct SimParty {
+    int idx = 0;
+    Sh3Runtime rt;
+    Sh3Encryptor enc;
+    Sh3Evaluator eval;
+};
+
+void run3(int device, const std::function<void(SimParty&)>& f) {
+    auto comms = makeLocalRing();
+    std::exception_ptr err[3];
+    std::thread th[3];
+    for (int i = 0; i < 3; ++i)
+        th[i] = std::thread([&, i] {
+            try {
+                SimParty p;
+                p.idx = i;
+                p.rt.init(i, comms[i], device);
+                p.enc.init(i, toBlock(0, i), toBlock(0, (i + 1) % 3));
+                p.eval.init(i, toBlock(1, i), toBlock(1, (i + 1) % 3));
+                f(p);
+                p.rt.gpu().sync();
+            } catch (...) {
+                err[i] = std::current_exception();
+            }
+        });
+    for (auto& t : th) t.join();
+    for (auto& e : err)
+        if (e) std::rethrow_exception(e);
+}
+
+i64Matrix hostMat(const int64_t* p, u64 r, u64 c) {
+    i64Matrix m(r, c);
+    std::memcpy(m.mData.data(), p, 8 * r * c);
+    return m;
+}
+
+// out layout [party][share][n], as the oracle's putShared
+void putShares(int party, const SharedMat& m, int64_t* out) {
+    if (!out) return;
+    const u64 n = m.size();
+    for (int s = 0; s < 2; ++s) {
+        auto v = m.shareToHost(s);
+        std::memcpy(out + (2 * party + s) * n, v.data(), 8 * n);
+    }
+}
+
+template <class T>
+void shareIn(SimParty& p, const i64Matrix& m, T& dest) {
+    if (p.idx == 0)
+        p.enc.localIntMatrix(p.rt, m, dest).get();
+    else
+        p.enc.remoteIntMatrix(p.rt, dest).get();
+}
+void shareBinIn(SimParty& p, const i64Matrix& m, sbMatrix& dest) {
+    if (p.idx == 0)
+        p.enc.localBinMatrix(p.rt, m, dest).get();
+    else
+        p.enc.remoteBinMatrix(p.rt, dest).get();
+}
+
+template <class F>
+int guarded(F&& f) {
+    try {
+        f();
+        return 0;
+    } catch (const std::exception& e) {
+        t_simErr = e.what();
+        return 1;
+    }
+}
+
+}  // namespace
+}  // namespace aby3
+
+using namespace aby3;
+
+extern "C" {
+
+const char* aby3h_sim_last_error(void) { return t_simErr.c_str(); }
+
+int aby3h_sim_mul(int device, int mode, int trunc, uint64_t d, const int64_t* a, const int64_t* b, uint64_t M,
+                  uint64_t K, uint64_t N, int64_t* out_shares, int64_t* out_plain) {
+    return guarded([&] {
+        const MulMode mm = mode == 1 ? MulMode::Gemm : MulMode::Hadamard;
+        const u64 br = mode == 1 ? K : M, bc = mode == 1 ? N : K;
+        i64Matrix am = hostMat(a, M, K), bm = hostMat(b, br, bc);
+        run3(device, [&](SimParty& p) {
+            si64Matrix A(M, K), B(br, bc), C;
+            shareIn(p, am, A);
+            shareIn(p, bm, B);
+            if (trunc)
+                p.eval.asyncMul(p.rt, A, B, C, d, mm).get();
+            else
+                p.eval.asyncMul(p.rt, A, B, C, mm).get();
+            putShares(p.idx, C, out_shares);
+            i64Matrix r;
+            p.enc.revealAll(p.rt, C, r).get();
+            if (p.idx == 0 && out_plain) std::memcpy(out_plain, r.mData.data(), 8 * r.size());
+        });
+    });
+}
+
+int aby3h_sim_mul_bit(int device, int kind, const int64_t* a, int64_t apub, const int64_t* bits, uint64_t n,
+                      int64_t* out_shares, int64_t* out_plain) {
+    return guarded([&] {
+        i64Matrix bm = hostMat(bits, n, 1);
+        i64Matrix am = kind == 0 ? hostMat(a, n, 1) : i64Matrix();
+        run3(device, [&](SimParty& p) {
+            si64Matrix A(n, 1), C;
+            sbMatrix B(n, 1);
+            shareBinIn(p, bm, B);  // the oracle shares the bits first
+            if (kind == 0) {
+                shareIn(p, am, A);
+                p.eval.asyncMul(p.rt, A, B, C).get();
+            } else {
+                p.eval.asyncMul(p.rt, apub, B, C).get();
+            }
+            putShares(p.idx, C, out_shares);
+            i64Matrix r;
+            p.enc.revealAll(p.rt, C, r).get();
+            if (p.idx == 0 && out_plain) std::memcpy(out_plain, r.mData.data(), 8 * n);
+        });
+    });
+}
+
+int aby3h_sim_circuit(int device, const char* name, uint64_t size, uint64_t param, uint64_t rows, const int64_t* ins,
+                      int64_t* outs, int64_t* out_shares) {
+    return guarded([&] {
+        CircuitLibrary lib;
+        BetaCircuit* cir = lib.byName(name, size, param);
+        std::vector<i64Matrix> inM;
+        u64 off = 0;
+        for (auto& b : cir->mInputs) {
+            const u64 cols = (b.size() + 63) / 64;
+            inM.push_back(hostMat(ins + off, rows, cols));
+            off += rows * cols;
+        }
+        run3(device, [&](SimParty& p) {
+            std::vector<sbMatrix> in(cir->mInputs.size()), out(cir->mOutputs.size());
+            std::vector<const sbMatrix*> ip;
+            std::vector<sbMatrix*> op;
+            for (size_t b = 0; b < in.size(); ++b) {
+                in[b].resize(rows, cir->mInputs[b].size());
+                shareBinIn(p, inM[b], in[b]);
+                ip.push_back(&in[b]);
+            }
+            for (auto& o : out) op.push_back(&o);
+            CircuitLibrary local;
+            evalCircuit(local.byName(name, size, param), ip, op, p.eval, p.rt);
+            u64 o = 0, so = 0;
+            for (auto& m : out) {
+                if (out_shares) putShares(p.idx, m, out_shares + so);
+                i64Matrix r;
+                p.enc.revealAll(p.rt, m, r).get();
+                if (p.idx == 0 && outs) std::memcpy(outs + o, r.mData.data(), 8 * r.size());
+                o += m.size();
+                so += 6 * m.size();
+            }
+        });
+    });
+}
+
+int aby3h_sim_piecewise(int device, int kind, const int64_t* x, uint64_t n, uint64_t D, int64_t* out_shares,
+                        int64_t* out_plain) {
+    return guarded([&] {
+        i64Matrix xm = hostMat(x, n, 1);
+        run3(device, [&](SimParty& p) {
+            si64Matrix X(n, 1), Y;
+            shareIn(p, xm, X);
+            Sh3Piecewise pw;
+            if (kind == 0) {  // the reference's sigmoid (aby3ML.h:121-139)
+                pw.mThresholds = {Sh3Piecewise::Coef(-0.5), Sh3Piecewise::Coef(0.5)};
+                pw.mCoefficients.resize(3);
+                pw.mCoefficients[1] = {Sh3Piecewise::Coef(0.5), Sh3Piecewise::Coef(1)};
+                pw.mCoefficients[2] = {Sh3Piecewise::Coef(1)};
+            } else {  // ReLU
+                pw.mThresholds = {Sh3Piecewise::Coef(0)};
+                pw.mCoefficients.resize(2);
+                pw.mCoefficients[1] = {Sh3Piecewise::Coef(0), Sh3Piecewise::Coef(1)};
+            }
+            pw.eval(p.rt, X, Y, D, p.eval).get();
+            putShares(p.idx, Y, out_shares);
+            i64Matrix r;
+            p.enc.revealAll(p.rt, Y, r).get();
+            if (p.idx == 0 && out_plain) std::memcpy(out_plain, r.mData.data(), 8 * n);
+        });
+    });
+}
+
+int aby3h_sim_cipher_gt(int device, const int64_t* a, const int64_t* b, uint64_t n, int64_t* out_plain,
+                        int64_t* out_shares) {
+    return guarded([&] {
+        i64Matrix am = hostMat(a, n, 1), bm = hostMat(b, n, 1);
+        run3(device, [&](SimParty& p) {
+            si64Matrix A(n, 1), B(n, 1);
+            shareIn(p, am, A);
+            shareIn(p, bm, B);
+            sbMatrix g;
+            cipher_gt(p.idx, A, B, g, p.eval, p.rt);
+            putShares(p.idx, g, out_shares);
+            i64Matrix r;
+            p.enc.revealAll(p.rt, g, r).get();
+            if (p.idx == 0 && out_plain) std::memcpy(out_plain, r.mData.data(), 8 * n);
+        });
+    });
+}
+
+int aby3h_sim_merge(int device, const uint64_t* lens, uint64_t nlists, const int64_t* keys, int64_t* out_sorted) {
+    return guarded([&] {
+        std::vector<i64Matrix> lists;
+        u64 off = 0;
+        for (u64 k = 0; k < nlists; ++k) {
+            lists.push_back(hostMat(keys + off, lens[k], 1));
+            off += lens[k];
+        }
+        run3(device, [&](SimParty& p) {
+            std::vector<sbMatrix> data(nlists);
+            for (u64 k = 0; k < nlists; ++k) {
+                data[k].resize(lens[k], 64);
+                shareBinIn(p, lists[k], data[k]);
+            }
+            sbMatrix sorted;
+            odd_even_multi_merge(data, sorted, p.idx, p.eval, p.rt);
+            i64Matrix r;
+            p.enc.revealAll(p.rt, sorted, r).get();
+            if (p.idx == 0 && out_sorted) std::memcpy(out_sorted, r.mData.data(), 8 * r.size());
+        });
+    });
+}
+
+}  // extern "C"

@@ -158,6 +158,14 @@ _HOST_SIGS = {
     "aby3h_session_destroy": (None, [c_void_p]),
     "aby3h_circuit": (c_int, [c_char_p, c_uint64, c_uint64, POINTER(c_uint64), c_void_p, c_void_p, c_void_p,
                               c_void_p, c_void_p, c_void_p]),
+    "aby3h_sim_last_error": (c_char_p, []),
+    "aby3h_sim_mul": (c_int, [c_int, c_int, c_int, c_uint64, c_void_p, c_void_p, c_uint64, c_uint64, c_uint64,
+                              c_void_p, c_void_p]),
+    "aby3h_sim_mul_bit": (c_int, [c_int, c_int, c_void_p, c_int64, c_void_p, c_uint64, c_void_p, c_void_p]),
+    "aby3h_sim_circuit": (c_int, [c_int, c_char_p, c_uint64, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p]),
+    "aby3h_sim_piecewise": (c_int, [c_int, c_int, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p]),
+    "aby3h_sim_cipher_gt": (c_int, [c_int, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p]),
+    "aby3h_sim_merge": (c_int, [c_int, c_void_p, c_uint64, c_void_p, c_void_p]),
 }
 
 _host = None
@@ -253,6 +261,95 @@ def circuit(name: str, size: int = 64, param: int = 0) -> dict:
         outs.append(outw[o:o + s].tolist())
         o += s
     return dict(wires=int(wires), gates=gates.reshape(-1, 4), levels=levels, inputs=ins, outputs=outs)
+
+
+class sim:
+    """One protocol call by three in-process parties on one GPU, with the
+    reference unit tests' seeds (include/aby3.h aby3h_sim_*). Each returns
+    (shares[3][2][n], revealed) as numpy int64, in the oracle's layout."""
+
+    @staticmethod
+    def _np():
+        import numpy as np
+
+        return np
+
+    @staticmethod
+    def _call(fn, *args):
+        h = host()
+        if getattr(h, fn)(*args) != 0:
+            raise NativeError(f"{fn}: " + h.aby3h_sim_last_error().decode())
+
+    @staticmethod
+    def _p(a):
+        return a.ctypes.data_as(c_void_p)
+
+    @classmethod
+    def mul(cls, mode, trunc, d, a, b, M, K, N, device=0):
+        np = cls._np()
+        a, b = np.ascontiguousarray(a, np.int64), np.ascontiguousarray(b, np.int64)
+        n = M * N if mode == 1 else M * K  # Hadamard: a, b and C are M x K
+        if a.size != M * K or b.size != (K * N if mode == 1 else M * K):
+            raise ValueError("sim.mul: operand sizes do not match M, K, N")
+        sh, plain = np.zeros(6 * n, np.int64), np.zeros(n, np.int64)
+        cls._call("aby3h_sim_mul", device, mode, int(trunc), d, cls._p(a), cls._p(b), M, K, N, cls._p(sh),
+                  cls._p(plain))
+        return sh.reshape(3, 2, -1), plain
+
+    @classmethod
+    def mul_bit(cls, kind, a, apub, bits, device=0):
+        np = cls._np()
+        n = len(bits)
+        a = np.ascontiguousarray(a if a is not None else np.zeros(n), np.int64)
+        bits = np.ascontiguousarray(bits, np.int64)
+        sh, plain = np.zeros(6 * n, np.int64), np.zeros(n, np.int64)
+        cls._call("aby3h_sim_mul_bit", device, kind, cls._p(a), apub, cls._p(bits), n, cls._p(sh), cls._p(plain))
+        return sh.reshape(3, 2, -1), plain
+
+    @classmethod
+    def circuit(cls, name, size, param, rows, inputs, device=0):
+        """inputs: one [rows, ceil(bits/64)] int64 array per input bundle;
+        returns (shares per output bundle, revealed per output bundle)."""
+        np = cls._np()
+        cir = circuit(name, size, param)
+        ins = np.ascontiguousarray(np.concatenate([np.asarray(x, np.int64).reshape(-1) for x in inputs]))
+        cols = [(len(o) + 63) // 64 for o in cir["outputs"]]
+        outs, sh = np.zeros(rows * sum(cols), np.int64), np.zeros(6 * rows * sum(cols), np.int64)
+        cls._call("aby3h_sim_circuit", device, name.encode(), size, param, rows, cls._p(ins), cls._p(outs),
+                  cls._p(sh))
+        res, shs, o = [], [], 0
+        for c in cols:
+            res.append(outs[o:o + rows * c].reshape(rows, c))
+            shs.append(sh[6 * o:6 * (o + rows * c)].reshape(3, 2, rows * c))
+            o += rows * c
+        return shs, res
+
+    @classmethod
+    def piecewise(cls, kind, x, D, device=0):
+        np = cls._np()
+        x = np.ascontiguousarray(x, np.int64)
+        n = len(x)
+        sh, plain = np.zeros(6 * n, np.int64), np.zeros(n, np.int64)
+        cls._call("aby3h_sim_piecewise", device, kind, cls._p(x), n, D, cls._p(sh), cls._p(plain))
+        return sh.reshape(3, 2, -1), plain
+
+    @classmethod
+    def cipher_gt(cls, a, b, device=0):
+        np = cls._np()
+        a, b = np.ascontiguousarray(a, np.int64), np.ascontiguousarray(b, np.int64)
+        n = len(a)
+        sh, plain = np.zeros(6 * n, np.int64), np.zeros(n, np.int64)
+        cls._call("aby3h_sim_cipher_gt", device, cls._p(a), cls._p(b), n, cls._p(plain), cls._p(sh))
+        return sh.reshape(3, 2, -1), plain
+
+    @classmethod
+    def merge(cls, lists, device=0):
+        np = cls._np()
+        lens = np.asarray([len(x) for x in lists], np.uint64)
+        keys = np.ascontiguousarray(np.concatenate([np.asarray(x, np.int64) for x in lists]))
+        out = np.zeros(len(keys), np.int64)
+        cls._call("aby3h_sim_merge", device, cls._p(lens), len(lists), cls._p(keys), cls._p(out))
+        return out
 
 
 _lib = None

@@ -43,8 +43,8 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--m", type=int, default=1024)
     ap.add_argument("--k", type=int, default=1024)
     ap.add_argument("--n", type=int, default=1024)
@@ -53,7 +53,9 @@ def parse():
     ap.add_argument("--binary-steps", type=int, default=5)
     ap.add_argument("--no-binary", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-reps", type=int, default=4)
+    ap.add_argument("--cpu-reps", type=int, default=10)
+    ap.add_argument("--no-extras", action="store_true", help="skip the LR-iteration and merge-layer lines")
+    ap.add_argument("--lr-rows", type=int, default=1000000)
     return ap.parse_args()
 
 
@@ -101,6 +103,44 @@ def load_pmc(kind: str, cfg: dict):
         if e and e.get("config") == cfg:
             best = e.get("hbm_bytes_per_launch")
     return best
+
+
+def timed(sess, steps, pg):
+    barrier(pg)
+    t0 = time.perf_counter()
+    sess.run(steps)
+    t1 = time.perf_counter()
+    barrier(pg)
+    return allmax(pg, t1 - t0)
+
+
+def extras(args, nt, dev, world, pg):
+    """C4 (one SGD_Logistic iteration, 10^6 x 128, B=256, D16) and C5 (one
+    compare-exchange layer of the 2^20-key merge network), each checked."""
+    res = {}
+    with nt.Session(nt.JOB_LR, [args.lr_rows, 128, 256, 16, 11], devices=(dev,) * 3, probe=False) as s:
+        s.run(5)
+        dt = timed(s, 50, pg)
+        if not s.check():
+            raise SystemExit("bench: LR model differs from the plaintext fixed-point restatement")
+        res["lr_iteration"] = {
+            "workload": f"SGD_Logistic iteration, {args.lr_rows}x128, batch 256, D16, lr 2^-11 (sigmoid piecewise)",
+            "ms_per_iteration": dt / 50 * 1e3,
+            "iterations_per_s": world * 50 / dt,
+        }
+    with nt.Session(nt.JOB_MERGE_LAYER, [1 << 20], devices=(dev,) * 3, probe=False) as s:
+        s.run(2)
+        dt = timed(s, 10, pg)
+        if not s.check():
+            raise SystemExit("bench: merge layer not ordered")
+        info = s.info()
+        res["merge_layer"] = {
+            "workload": "one odd-even merge layer: cmp_swap on 2^19 pairs of 64-bit keys (gather, circuit, scatter)",
+            "ms_per_layer": dt / 10 * 1e3,
+            "and_word_gates_per_s": world * 10 * info["and_words"] / dt,
+            "est_full_merge_s": dt / 10 * 210,
+        }
+    return res
 
 
 def main():
@@ -205,6 +245,9 @@ def main():
                 "bytes_per_step_per_party": binfo["gate_bytes"],
             },
         }
+
+    if not args.no_extras:
+        out["extras"] = extras(args, nt, dev, world, pg)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         import ctypes

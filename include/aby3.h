@@ -76,6 +76,38 @@ int aby3h_circuit(const char* name, uint64_t size, uint64_t param, uint64_t coun
                   uint32_t* level_counts, uint32_t* in_sizes, uint32_t* in_wires, uint32_t* out_sizes,
                   uint32_t* out_wires);
 
+/* ---- one protocol call by three in-process parties ---------------------
+ * The topology and seeds of the reference's unit tests
+ * (Sh3EvaluatorTests.cpp:23-131): encryptor seeds toBlock(0, i) /
+ * toBlock(0, i+1), evaluator seeds toBlock(1, i) / toBlock(1, i+1), all on
+ * `device`; party 0 shares the inputs (Sh3Encryptor::localIntMatrix /
+ * localBinMatrix, inputs shared in argument order). out_shares receives
+ * every party's two shares as [party][share][n] i64 (n = result elements),
+ * out_plain the result revealed by revealAll. Any output pointer may be
+ * NULL. Returns 0, or 1 with aby3h_sim_last_error() set. */
+const char* aby3h_sim_last_error(void);
+/* asyncMul(A, B, C [, d]) (Sh3Evaluator.cpp:92-116, :651-730); mode 1 GEMM
+ * (a M x K, b K x N), 0 Hadamard (a, b M x K) */
+int aby3h_sim_mul(int device, int mode, int trunc, uint64_t d, const int64_t* a, const int64_t* b, uint64_t M,
+                  uint64_t K, uint64_t N, int64_t* out_shares, int64_t* out_plain);
+/* kind 0: asyncMul(si64 a, sb bits) (:119-263); 1: asyncMul(i64 apub, sb bits) (:418-501); bits shared first */
+int aby3h_sim_mul_bit(int device, int kind, const int64_t* a, int64_t apub, const int64_t* bits, uint64_t n,
+                      int64_t* out_shares, int64_t* out_plain);
+/* a library circuit (aby3h_circuit names) on binary-shared inputs: ins is
+ * [input bundle][rows][ceil(bits/64)] i64; outs / out_shares the same per output bundle */
+int aby3h_sim_circuit(int device, const char* name, uint64_t size, uint64_t param, uint64_t rows, const int64_t* ins,
+                      int64_t* outs, int64_t* out_shares);
+/* Sh3Piecewise::eval on an n x 1 shared input (Sh3Piecewise.cpp:184-378):
+ * kind 0 the logistic sigmoid of aby3ML.h:121-139, kind 1 ReLU */
+int aby3h_sim_piecewise(int device, int kind, const int64_t* x, uint64_t n, uint64_t D, int64_t* out_shares,
+                        int64_t* out_plain);
+/* cipher_gt(A, B) = MSB(B - A) (BuildingBlocks.cpp:525-532), 1-bit result */
+int aby3h_sim_cipher_gt(int device, const int64_t* a, const int64_t* b, uint64_t n, int64_t* out_plain,
+                        int64_t* out_shares);
+/* odd_even_multi_merge of nlists sorted lists (Sort.cpp:327-437); keys
+ * concatenated, out_sorted receives the revealed merged list */
+int aby3h_sim_merge(int device, const uint64_t* lens, uint64_t nlists, const int64_t* keys, int64_t* out_sorted);
+
 #ifdef __cplusplus
 }
 #endif

@@ -265,7 +265,7 @@ int orc_sim_piecewise(int kind, uint32_t wires, const uint32_t* gates, uint64_t 
 int orc_sim_fetch_msb(uint32_t wires, const uint32_t* gates, uint64_t ngates, const uint32_t* levels,
                       uint64_t nlevels, const uint32_t* inWires, const uint32_t* inSizes, uint64_t nin,
                       const uint32_t* outWires, const uint32_t* outSizes, uint64_t nout, const int64_t* a,
-                      const int64_t* b, uint64_t n, int64_t* out_plain) {
+                      const int64_t* b, uint64_t n, int64_t* out_plain, int64_t* out_shares) {
     return guard([&] {
         Circuit c = toCircuit(wires, gates, ngates, levels, nlevels, inWires, inSizes, nin, outWires, outSizes, nout);
         auto enc = makeEncryptors(0);
@@ -279,6 +279,7 @@ int orc_sim_fetch_msb(uint32_t wires, const uint32_t* gates, uint64_t ngates, co
                 for (u64 k = 0; k < n; ++k)
                     diff[p].s[s].v[k] = (i64)((u64)B[p].s[s].v[k] - (u64)A[p].s[s].v[k]);
         Shared r = fetchMsb(ev, c, diff);
+        if (out_shares) putShared(r, out_shares);
         Mat m = revealBin(r);
         memcpy(out_plain, m.v.data(), 8 * n);
     });

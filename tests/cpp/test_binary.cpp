@@ -267,6 +267,35 @@ static void mergeTest(std::vector<u64> lens, u64 seed) {
     check(revealed == all, "merged order");
 }
 
+static void replicatedInput() {
+    // setReplicatedInput (Sh3BinaryEvaluator.cpp:105-138): a one-row shared
+    // constant broadcast to every row; a & c over 300 rows
+    const u64 rows = 300;
+    i64Matrix a = randMat(rows, 1, 41), c(1, 1);
+    c(0, 0) = (i64)0xF0F0F0F00FF00FF0ull;
+    std::vector<i64> revealed;
+    run3([&](harness::Party& p) {
+        sbMatrix A(rows, 64), C(1, 64), out;
+        if (p.idx == 0) {
+            p.enc.localBinMatrix(p.rt, a, A).get();
+            p.enc.localBinMatrix(p.rt, c, C).get();
+        } else {
+            p.enc.remoteBinMatrix(p.rt, A).get();
+            p.enc.remoteBinMatrix(p.rt, C).get();
+        }
+        CircuitLibrary lib;
+        Sh3BinaryEvaluator eng;
+        eng.setCir(lib.int_int_bitwiseAnd(64), rows, p.eval.mShareGen);
+        eng.setInput(0, A);
+        eng.setReplicatedInput(1, C);
+        eng.asyncEvaluate(p.rt.noDependencies()).then([&](Sh3Task&) { eng.getOutput(0, out); }).get();
+        i64Matrix r;
+        p.enc.revealAll(p.rt, out, r).get();
+        if (p.idx == 0) revealed = r.mData;
+    });
+    for (u64 i = 0; i < rows; ++i) check(revealed[i] == (a(i, 0) & c(0, 0)), "a & replicated c");
+}
+
 int main() {
     auto msb = [](u64 a, u64 b) { return (a + b) >> 63; };
     test("bin_msb_64_rows256 (Sh3_BinaryEngine_add_msb_test)",
@@ -300,6 +329,7 @@ int main() {
     test("arith_compare_16 (Test.cpp gt/ge/eq/mul_ab)", arithCompare16);
     test("cipher_gt_parity_1000", [] { fetchMsbParity(1000); });
     test("piecewise_sigmoid_256_D16", [] { piecewiseParity(256, 16); });
+    test("setReplicatedInput_and_300", replicatedInput);
     test("odd_even_merge_2x8 (SortTest.cpp)", [] { mergeTest({8, 8}, 1); });
     test("odd_even_multi_merge_4 (SortTest.cpp)", [] { mergeTest({5, 7, 8, 3}, 2); });
     test("odd_even_multi_merge_8x64", [] { mergeTest({64, 64, 64, 64, 64, 64, 64, 64}, 3); });

@@ -96,7 +96,7 @@ def trunc_tuple(next_seed: bytes, next_off: int, prev_seed: bytes, prev_off: int
 
 
 def sim_mul(mode: int, trunc: bool, d: int, a: np.ndarray, b: np.ndarray, M: int, K: int, N: int):
-    n = M * N
+    n = M * N if mode == 1 else M * K  # Hadamard: C is M x K
     shares = np.zeros(6 * n, dtype=np.int64)
     plain = np.zeros(n, dtype=np.int64)
     a = np.ascontiguousarray(a, dtype=np.int64)
@@ -160,11 +160,13 @@ def sim_piecewise(kind: int, cir, x: np.ndarray, D: int):
     return shares.reshape(3, 2, n), plain
 
 
-def sim_fetch_msb(cir, a: np.ndarray, b: np.ndarray):
+def sim_fetch_msb(cir, a: np.ndarray, b: np.ndarray, with_shares: bool = False):
+    """cipher_gt(a, b) = MSB(b - a) through fetch_msb (BuildingBlocks.cpp:464-532)."""
     args, keep = _cir_args(cir)
     n = len(a)
     a = np.ascontiguousarray(a, dtype=np.int64)
     b = np.ascontiguousarray(b, dtype=np.int64)
     out = np.zeros(n, dtype=np.int64)
-    _check(dll().orc_sim_fetch_msb(*args, _p(a), _p(b), c_uint64(n), _p(out)))
-    return out
+    sh = np.zeros(6 * n, dtype=np.int64)
+    _check(dll().orc_sim_fetch_msb(*args, _p(a), _p(b), c_uint64(n), _p(out), _p(sh)))
+    return (out, sh.reshape(3, 2, n)) if with_shares else out

@@ -13,7 +13,8 @@ from aby3_amd import native as nt
 def _vals(n, seed, bits=64):
     rng = np.random.default_rng(seed)
     v = rng.integers(-(2**63), 2**63 - 1, size=n, dtype=np.int64, endpoint=True)
-    v[:6] = [0, -1, 2**63 - 1, -(2**63), 1, 5]
+    edge = np.array([0, -1, 2**63 - 1, -(2**63), 1, 5], dtype=np.int64)[:n]
+    v[:len(edge)] = edge
     if bits < 64:
         v &= (1 << bits) - 1
     return v

@@ -103,7 +103,7 @@ def _rand(n, seed, bound=None):
     return rng.integers(-bound, bound, size=n, dtype=np.int64)
 
 
-@pytest.mark.parametrize("mode,M,K,N", [(1, 10, 10, 10), (1, 7, 13, 5), (0, 10, 10, 10)])
+@pytest.mark.parametrize("mode,M,K,N", [(1, 10, 10, 10), (1, 7, 13, 5), (0, 10, 10, 10), (0, 31, 9, 1)])
 def test_sim_mul_reveals_product(mode, M, K, N):
     # Sh3_Evaluator_mul_test (GEMM, :594-690) / the fork's Hadamard (Test.cpp:116)
     a = _rand(M * K, 1)

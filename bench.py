@@ -89,8 +89,9 @@ def allmax(pg, x: float) -> float:
     return float(t.item())
 
 
-def load_pmc(kind: str, cfg: dict):
-    """HBM bytes per launch from a committed rocprofv3 PMC summary, if it matches."""
+def load_pmc(kind: str, cfg: dict, field: str = "hbm_bytes_per_launch"):
+    """HBM bytes (per launch, or the named field) from a committed rocprofv3
+    PMC summary (profiles/pmc_*.json, scripts/pmc_summary.py), if its config matches."""
     import glob
 
     best = None
@@ -101,7 +102,7 @@ def load_pmc(kind: str, cfg: dict):
             continue
         e = d.get(kind)
         if e and e.get("config") == cfg:
-            best = e.get("hbm_bytes_per_launch")
+            best = e.get(field)
     return best
 
 
@@ -112,6 +113,23 @@ def timed(sess, steps, pg):
     t1 = time.perf_counter()
     barrier(pg)
     return allmax(pg, t1 - t0)
+
+
+def cpu_lr_ms(nt, iters):
+    """The oracle's LR iteration on this host (cpu_baseline leg only)."""
+    import ctypes
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle as orc
+
+    args, keep = orc._cir_args(nt.circuit("int_Sh3Piecewise_helper", 64, 2))
+    f = orc.dll().orc_bench_lr
+    f.restype = ctypes.c_double
+    u = ctypes.c_uint64
+    secs = f(*args, u(65536), u(128), u(256), u(16), u(11), iters)
+    if secs < 0:
+        raise SystemExit("bench: oracle LR baseline failed: " + orc.dll().orc_last_error().decode())
+    return secs / iters * 1e3
 
 
 def extras(args, nt, dev, world, pg):
@@ -128,6 +146,14 @@ def extras(args, nt, dev, world, pg):
             "ms_per_iteration": dt / 50 * 1e3,
             "iterations_per_s": world * 50 / dt,
         }
+        if world == 1 and not args.no_cpu_baseline:
+            cpu_ms = cpu_lr_ms(nt, iters=200)
+            res["lr_iteration"]["cpu_baseline"] = {
+                "value": cpu_ms, "unit": "ms/iteration", "cores": 1, "kind": "port",
+                "sample": "200 iterations of the oracle's SGD_Logistic restatement (65536x128 dataset, batch 256, "
+                          "D16, aB 11), the three parties simulated in sequence on one thread, no network",
+            }
+            res["lr_iteration"]["speedup_vs_cpu_baseline"] = cpu_ms / (dt / 50 * 1e3)
     with nt.Session(nt.JOB_MERGE_LAYER, [1 << 20], devices=(dev,) * 3, probe=False) as s:
         s.run(2)
         dt = timed(s, 10, pg)
@@ -201,6 +227,7 @@ def main():
             "unit": "TFLOP/s",
             "frac": achieved_tops / PEAK_INT8_TOPS,
             "traffic": traffic,
+            "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_*.json)",
             "launch_ms": gemm_avg_s * 1e3,
             "ops_per_launch": info["gemm_int8_ops"],
         },
@@ -241,7 +268,8 @@ def main():
                 "peak": PEAK_HBM_GBS,
                 "unit": "GB/s",
                 "frac": gbs / PEAK_HBM_GBS,
-                "traffic": load_pmc("bin_gates", {"rows": args.binary_rows}),
+                "traffic": load_pmc("bin_gates", {"rows": args.binary_rows}, "hbm_bytes_per_step_per_party"),
+                "traffic_unit": "HBM bytes per step per party (rocprofv3 FETCH_SIZE/WRITE_SIZE)",
                 "bytes_per_step_per_party": binfo["gate_bytes"],
             },
         }

@@ -41,12 +41,33 @@ struct SrcSlabs {
         return v;
     }
 };
+// GEMM product minus a subtrahend (z = product - R of the truncation pair).
+struct SrcSlabsMinus {
+    const i64* P;
+    u32 nsplit;
+    u64 stride;
+    const i64* sub;
+    __device__ u64 operator()(u64 i) const {
+        u64 v = 0;
+        for (u32 s = 0; s < nsplit; ++s) v += (u64)P[s * stride + i];
+        return v - (u64)sub[i];
+    }
+};
 // Hadamard: A0 B0 + A0 B1 + A1 B0 = A0 (B0 + B1) + A1 B0, mod 2^64.
 struct SrcHadamard {
     const i64 *A0, *A1, *B0, *B1;
     __device__ u64 operator()(u64 i) const {
         u64 a0 = (u64)A0[i], a1 = (u64)A1[i], b0 = (u64)B0[i], b1 = (u64)B1[i];
         return a0 * (b0 + b1) + a1 * b0;
+    }
+};
+
+// Hadamard product minus a subtrahend.
+struct SrcHadamardMinus {
+    const i64 *A0, *A1, *B0, *B1, *sub;
+    __device__ u64 operator()(u64 i) const {
+        u64 a0 = (u64)A0[i], a1 = (u64)A1[i], b0 = (u64)B0[i], b1 = (u64)B1[i];
+        return a0 * (b0 + b1) + a1 * b0 - (u64)sub[i];
     }
 };
 

@@ -18,6 +18,8 @@
 // row r is stored at slot g ^ (r & 15): the 16 lanes of each ds_read_b128
 // lane group read 16 different rows at the same chunk and land on 16
 // different bank slots.
+#include <map>
+#include <mutex>
 #include "epilogue.h"
 
 namespace aby3g {
@@ -66,77 +68,85 @@ GemmPlan plan_gemm(u64 M, u64 K, u64 N) {
     return p;
 }
 
-// Balanced base-256 digits of 16 consecutive K' values, written as one
-// 16-byte chunk per plane.
-__device__ __forceinline__ void digits16(const u64 (&x)[16], v4i (&planes)[8]) {
-    u32 carry[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) carry[j] = 0;
-#pragma unroll
-    for (int p = 0; p < 8; ++p) {
-        u32 w[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            u32 b = (u32)((x[j] >> (8 * p)) & 0xff) + carry[j];  // 0..256
-            carry[j] = b >= 128 ? 1u : 0u;
-            u32 d = b & 0xff;  // two's complement byte of b - 256*carry
-            w[j >> 2] |= d << (8 * (j & 3));
-        }
-        planes[p] = v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
-    }
-}
+// Balanced base-256 digits. With y = x + 0x8080...80 (mod 2^64), byte p of
+// y is b_p + 128 + carry_p (mod 256) and the carry out of byte p is exactly
+// the balanced-digit borrow, so digit p = byte p of y minus 128, i.e. the
+// int8 whose bits are (byte p of y) ^ 0x80:  x = sum_p d_p 2^(8p) mod 2^64.
+constexpr u64 kDigitBias = 0x8080808080808080ull;
 
-// Ad[m][K'/32][8][32] from A0 | A1 (row m, K' = [0, Kp) <- A0, [Kp, 2Kp) <- A1).
-__global__ void __launch_bounds__(256) k_digits_A(const i64* __restrict__ A0, const i64* __restrict__ A1, u64 M,
-                                                  u64 K, u64 Kp, u64 Mp, u8* __restrict__ Ad) {
-    const u64 chunks = 2 * Kp / 16;
-    const u64 total = Mp * chunks;
-    for (u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (u64)gridDim.x * blockDim.x) {
-        const u64 m = t / chunks, ch = t % chunks;
-        const u64 k0 = ch * 16;
-        u64 x[16];
-        const bool second = k0 >= Kp;
-        const i64* src = second ? A1 : A0;
-        const u64 kb = second ? k0 - Kp : k0;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            u64 k = kb + j;
-            x[j] = (m < M && k < K) ? (u64)src[m * K + k] : 0;
-        }
-        v4i planes[8];
-        digits16(x, planes);
-        u8* rec = Ad + (m * (2 * Kp / BK) + k0 / BK) * kRec + (k0 % BK);
-#pragma unroll
-        for (int p = 0; p < 8; ++p) *reinterpret_cast<v4i*>(rec + p * 32) = planes[p];
-    }
-}
+// One launch builds both digit operands. A workgroup stages a 64 x 32 tile
+// of i64 (A: 64 rows x 32 K'; B': 32 K' x 64 columns, B0 + B1 summed for the
+// first half of K') in LDS with coalesced loads, then writes the tile's 64
+// records: 16 lanes per 256-byte record, lane (plane p, half h) packs digit
+// p of the 16 values of K' half h into one 16-byte store, so every record is
+// written by one contiguous 256-byte burst.
+constexpr u32 kDigitTile = 64;   // rows (A) or columns (B) per workgroup
+constexpr u32 kLdsPitch = 33;    // i64 per staged row: 32 + 1 pad (bank spread)
 
-// Bd[n][K'/32][8][32] from B' = [[B0 + B1]; [B0]] (column n).
-__global__ void __launch_bounds__(256) k_digits_B(const i64* __restrict__ B0, const i64* __restrict__ B1, u64 K,
-                                                  u64 N, u64 Kp, u64 Np, u8* __restrict__ Bd) {
-    const u64 chunks = 2 * Kp / 16;
-    for (u64 ch = blockIdx.y; ch < chunks; ch += gridDim.y) {
-        const u64 k0 = ch * 16;
-        const bool second = k0 >= Kp;
-        const u64 kb = second ? k0 - Kp : k0;
-        for (u64 n = (u64)blockIdx.x * blockDim.x + threadIdx.x; n < Np; n += (u64)gridDim.x * blockDim.x) {
-            u64 x[16];
+__global__ void __launch_bounds__(256) k_digits(const i64* __restrict__ A0, const i64* __restrict__ A1,
+                                                const i64* __restrict__ B0, const i64* __restrict__ B1, u64 M,
+                                                u64 K, u64 N, u64 Kp, u64 aTiles, u64 stages, u8* __restrict__ Ad,
+                                                u8* __restrict__ Bd) {
+    __shared__ u64 tile[kDigitTile * kLdsPitch];  // [row or column][32 K'] + pad
+    const u32 t = threadIdx.x;
+    const bool isA = blockIdx.x < aTiles;
+    const u64 tix = isA ? blockIdx.x : blockIdx.x - aTiles;
+    const u64 r0 = (tix / stages) * kDigitTile;  // first row (A) / column (B)
+    const u64 st = tix % stages;                 // 32-wide stage of K'
+    const u64 kc0 = st * BK;
+    if (isA) {
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                u64 k = kb + j;
-                u64 v = 0;
-                if (n < N && k < K) {
-                    v = (u64)B0[k * N + n];
-                    if (!second) v += (u64)B1[k * N + n];
+        for (int j = 0; j < 8; ++j) {
+            const u32 q = t + 256 * j;
+            const u32 r = q >> 5, kk = q & 31;
+            const u64 m = r0 + r, kc = kc0 + kk;
+            u64 v = 0;
+            if (m < M) {
+                if (kc < Kp) {
+                    if (kc < K) v = (u64)A0[m * K + kc];
+                } else if (kc - Kp < K) {
+                    v = (u64)A1[m * K + (kc - Kp)];
                 }
-                x[j] = v;
             }
-            v4i planes[8];
-            digits16(x, planes);
-            u8* rec = Bd + (n * (2 * Kp / BK) + k0 / BK) * kRec + (k0 % BK);
-#pragma unroll
-            for (int p = 0; p < 8; ++p) *reinterpret_cast<v4i*>(rec + p * 32) = planes[p];
+            tile[r * kLdsPitch + kk] = v;
         }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const u32 q = t + 256 * j;
+            const u32 kk = q >> 6, c = q & 63;
+            const u64 n = r0 + c, kc = kc0 + kk;
+            u64 v = 0;
+            if (n < N) {
+                if (kc < Kp) {
+                    if (kc < K) v = (u64)B0[kc * N + n] + (u64)B1[kc * N + n];
+                } else if (kc - Kp < K) {
+                    v = (u64)B0[(kc - Kp) * N + n];
+                }
+            }
+            tile[c * kLdsPitch + kk] = v;
+        }
+    }
+    __syncthreads();
+    u8* out = isA ? Ad : Bd;
+    const u32 lane16 = t & 15, p = lane16 >> 1, h = lane16 & 1;
+#pragma unroll
+    for (int pass = 0; pass < 4; ++pass) {
+        const u32 r = pass * 16 + (t >> 4);  // record (row / column) within the tile
+        const u64* src = tile + r * kLdsPitch + 16 * h;
+        u32 w[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            u32 acc = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const u64 y = src[4 * q + e] + kDigitBias;
+                acc |= ((u32)(y >> (8 * p)) & 0xffu) << (8 * e);
+            }
+            w[q] = acc ^ 0x80808080u;
+        }
+        u8* rec = out + ((r0 + r) * stages + st) * kRec + p * 32 + h * 16;
+        *reinterpret_cast<v4i*>(rec) = v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
     }
 }
 
@@ -223,6 +233,48 @@ __global__ void __launch_bounds__(kThreads, 2) k_share_gemm(const u8* __restrict
     }
 }
 
+// Share-GEMM launches on one device run one at a time, in issue order,
+// whichever stream issues them: co-located parties' GEMMs all want the whole
+// chip's matrix cores, so overlapping them only stretches each launch, while
+// the parties' AES, copy and finalize kernels (VALU/LDS/HBM) keep running
+// beside whichever GEMM holds the turn. The turn is a device-wide event chain
+// (stream waits on the previous GEMM's completion event; no host sync).
+class MfmaTurn {
+public:
+    explicit MfmaTurn(hipStream_t s) : s_(s) {
+        int dev = 0;
+        ABY3G_CHECK_HIP(hipGetDevice(&dev));
+        dev_ = dev;
+        mu().lock();
+        hipEvent_t& last = events()[dev_];
+        if (last) {
+            hipError_t e = hipStreamWaitEvent(s_, last, 0);
+            if (e != hipSuccess) {
+                mu().unlock();
+                ABY3G_CHECK_HIP(e);
+            }
+        }
+    }
+    ~MfmaTurn() {
+        hipEvent_t& last = events()[dev_];
+        if (!last) (void)hipEventCreateWithFlags(&last, hipEventDisableTiming);
+        if (last) (void)hipEventRecord(last, s_);
+        mu().unlock();
+    }
+
+private:
+    static std::mutex& mu() {
+        static std::mutex m;
+        return m;
+    }
+    static std::map<int, hipEvent_t>& events() {
+        static std::map<int, hipEvent_t> e;
+        return e;
+    }
+    hipStream_t s_;
+    int dev_ = 0;
+};
+
 struct Workspace {
     u8* Ad;
     u8* Bd;
@@ -244,13 +296,11 @@ void run_gemm(const GemmPlan& p, const i64* A, const i64* B, const Workspace& w,
     const i64* A1 = A + p.M * p.K;
     const i64* B0 = B;
     const i64* B1 = B + p.K * p.N;
-    const u64 chunks = p.Kc / 16;
-    u64 ga = (p.Mp * chunks + 255) / 256;
-    launch(PROBE_DIGITS, k_digits_A, dim3((u32)min(ga, (u64)8192)), dim3(256), 0, s, A0, A1, p.M, p.K, p.Kp, p.Mp, w.Ad);
-    u32 gbx = (u32)((p.Np + 255) / 256);
-    u32 gby = (u32)min(chunks, (u64)1024);
-    launch(PROBE_DIGITS, k_digits_B, dim3(gbx, gby), dim3(256), 0, s, B0, B1, p.K, p.N, p.Kp, p.Np, w.Bd);
     const u64 stages = p.Kc / BK;
+    const u64 aTiles = (p.Mp / kDigitTile) * stages, bTiles = (p.Np / kDigitTile) * stages;
+    launch(PROBE_DIGITS, k_digits, dim3((u32)(aTiles + bTiles)), dim3(256), 0, s, A0, A1, B0, B1, p.M, p.K, p.N, p.Kp,
+           aTiles, stages, w.Ad, w.Bd);
+    MfmaTurn turn(s);
     launch(PROBE_GEMM, k_share_gemm, dim3((u32)(p.Mp / BM), (u32)(p.Np / BN), p.splits), dim3(kThreads), 0, s,
            (const u8*)w.Ad, (const u8*)w.Bd, p.M, p.N, stages, p.kPerSplit / BK, w.P);
 }
@@ -317,6 +367,28 @@ int aby3g_mul_trunc_local(int mode, const int64_t* A, const int64_t* B, uint64_t
         run_gemm(p, A, B, w, S(stream));
         SrcSlabs src{w.P, p.splits, n};
         launch_finish_trunc(src, *ts, n, d, nullptr, C, C + n, z, S(stream));
+    });
+}
+
+int aby3g_mul_sub_local(int mode, const int64_t* A, const int64_t* B, const int64_t* sub, aby3g_event sub_ready,
+                        int64_t* out, uint64_t M, uint64_t K, uint64_t N, void* workspace, size_t workspace_bytes,
+                        aby3g_stream stream) {
+    return guarded([&] {
+        ABY3G_REQUIRE(mode == ABY3G_MUL_HADAMARD || mode == ABY3G_MUL_GEMM, "bad mode");
+        ABY3G_REQUIRE(sub != nullptr && out != nullptr, "null operand");
+        const u64 n = M * N;
+        if (!n) return;
+        if (mode == ABY3G_MUL_HADAMARD) {
+            if (sub_ready) ABY3G_CHECK_HIP(hipStreamWaitEvent(S(stream), (hipEvent_t)sub_ready, 0));
+            launch_finish_plain(SrcHadamardMinus{A, A + n, B, B + n, sub}, n, out, S(stream));
+            return;
+        }
+        GemmPlan p = plan_gemm(M, K, N);
+        check_ws(p, workspace, workspace_bytes);
+        Workspace w = carve(p, workspace);
+        run_gemm(p, A, B, w, S(stream));
+        if (sub_ready) ABY3G_CHECK_HIP(hipStreamWaitEvent(S(stream), (hipEvent_t)sub_ready, 0));
+        launch_finish_plain(SrcSlabsMinus{w.P, p.splits, n, sub}, n, out, S(stream));
     });
 }
 

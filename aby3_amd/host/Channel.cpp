@@ -18,6 +18,8 @@ struct Msg {
     std::vector<u8> host;
     Slot* slot = nullptr;
     size_t bytes = 0;
+    std::shared_ptr<DeviceBuffer> shared;  // zero-copy payload
+    std::shared_ptr<Event> ready;          // recorded on the sender's stream
 };
 }  // namespace
 
@@ -80,16 +82,23 @@ struct RecvFuture::State {
     void* dst = nullptr;
     size_t bytes = 0;
     Gpu* gpu = nullptr;  // null: host payload
+    bool shared = false;
+    std::shared_ptr<DeviceBuffer> out;
     bool done = false;
     std::mutex mu;
 };
 
 void RecvFuture::get() const {
     if (!mState) throw std::runtime_error("RecvFuture::get on an empty future");
+    if (mState->shared) {
+        getShared();
+        return;
+    }
     State& st = *mState;
     std::lock_guard<std::mutex> lk(st.mu);
     if (st.done) return;
     Msg m = st.pipe->pop(st.ticket);
+    if (m.shared) throw std::runtime_error("channel: zero-copy payload received by a copying receive");
     if (m.bytes != st.bytes)
         throw std::runtime_error("channel: message size mismatch (expected " + std::to_string(st.bytes) + ", got " +
                                  std::to_string(m.bytes) + ")");
@@ -111,6 +120,43 @@ void RecvFuture::get() const {
         st.pipe->releaseSlot(s);
     }
     st.done = true;
+}
+
+std::shared_ptr<DeviceBuffer> RecvFuture::getShared() const {
+    if (!mState || !mState->shared) throw std::runtime_error("RecvFuture::getShared on a non-shared receive");
+    State& st = *mState;
+    std::lock_guard<std::mutex> lk(st.mu);
+    if (st.done) return st.out;
+    Msg m = st.pipe->pop(st.ticket);
+    if (!m.shared) throw std::runtime_error("channel: expected a zero-copy device payload");
+    if (m.bytes != st.bytes)
+        throw std::runtime_error("channel: message size mismatch (expected " + std::to_string(st.bytes) + ", got " +
+                                 std::to_string(m.bytes) + ")");
+    GPU_CALL(aby3g_set_device(st.gpu->device()));
+    GPU_CALL(aby3g_stream_wait_event(st.gpu->stream(), m.ready->get()));
+    st.out = std::move(m.shared);
+    st.done = true;
+    return st.out;
+}
+
+void Channel::asyncSendShared(std::shared_ptr<DeviceBuffer> buf, size_t bytes, Gpu& gpu) {
+    if (!mOut) throw std::runtime_error("channel not connected");
+    if (!buf || buf->bytes() < bytes) throw std::runtime_error("asyncSendShared: buffer smaller than the message");
+    GPU_CALL(aby3g_set_device(gpu.device()));
+    Msg m;
+    m.device = true;
+    m.bytes = bytes;
+    m.shared = std::move(buf);
+    m.ready = std::make_shared<Event>();
+    m.ready->record(gpu.stream());
+    mOut->push(std::move(m));
+}
+
+RecvFuture Channel::asyncRecvShared(size_t bytes, Gpu& gpu) {
+    RecvFuture f = asyncRecv(nullptr, bytes);
+    f.mState->gpu = &gpu;
+    f.mState->shared = true;
+    return f;
 }
 
 void Channel::asyncSendCopy(const void* data, size_t bytes) {

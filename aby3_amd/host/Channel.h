@@ -31,6 +31,10 @@ public:
     // Waits for the message and makes its payload available at the
     // destination (device payload: ordered on the receiver's stream).
     void get() const;
+    // for asyncRecvShared: waits (on the receiver's stream) for the message
+    // and returns the sender's buffer itself. After enqueueing its last read
+    // of it, the receiver calls buffer->fence(its stream).
+    std::shared_ptr<DeviceBuffer> getShared() const;
     bool valid() const { return (bool)mState; }
 
     struct State;
@@ -59,6 +63,12 @@ public:
     // device payloads, enqueued on / delivered to `gpu`'s stream
     void asyncSendDevice(const void* src, size_t bytes, Gpu& gpu);
     RecvFuture asyncRecvDevice(void* dst, size_t bytes, Gpu& gpu);
+    // zero-copy device payloads: the message is the sender's buffer (the same
+    // buffer may go to several receivers); readiness is an event recorded on
+    // the sender's stream at send time. The receiver reads it in place (over
+    // xGMI when on another GPU) and fences it when done.
+    void asyncSendShared(std::shared_ptr<DeviceBuffer> buf, size_t bytes, Gpu& gpu);
+    RecvFuture asyncRecvShared(size_t bytes, Gpu& gpu);
 
     u64 bytesSent() const;
     u64 bytesRecv() const;

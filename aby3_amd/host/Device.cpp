@@ -29,12 +29,24 @@ void Event::sync() { GPU_CALL(aby3g_event_sync(mEv)); }
 Gpu::Gpu(int device) : mDevice(device) {
     GPU_CALL(aby3g_set_device(device));
     GPU_CALL(aby3g_stream_create(&mStream));
+    mPool = std::make_shared<Pool>();
+    mPool->device = device;
+    mPool->stream = mStream;
 }
 
 Gpu::~Gpu() {
     aby3g_set_device(mDevice);
     aby3g_stream_sync(mStream);
+    if (mAux) aby3g_stream_sync(mAux);
     trim();
+    {
+        // buffers still alive elsewhere now free straight to the driver
+        std::lock_guard<std::mutex> lk(mPool->mu);
+        mPool->stream = nullptr;
+    }
+    mForkEv.reset();
+    mAuxEv.reset();
+    if (mAux) aby3g_stream_destroy(mAux);
     aby3g_stream_destroy(mStream);
     if (t_current == this) t_current = nullptr;
 }
@@ -44,45 +56,85 @@ void Gpu::bind() {
     t_current = this;
 }
 
-void Gpu::sync() { GPU_CALL(aby3g_stream_sync(mStream)); }
+void Gpu::sync() {
+    GPU_CALL(aby3g_stream_sync(mStream));
+    if (mAux) GPU_CALL(aby3g_stream_sync(mAux));
+}
+
+aby3g_stream Gpu::aux() {
+    if (!mAux) {
+        GPU_CALL(aby3g_set_device(mDevice));
+        GPU_CALL(aby3g_stream_create(&mAux));
+        mForkEv = std::make_unique<Event>();
+        mAuxEv = std::make_unique<Event>();
+    }
+    return mAux;
+}
+
+void Gpu::forkAux() {
+    aby3g_stream a = aux();
+    mForkEv->record(mStream);
+    GPU_CALL(aby3g_stream_wait_event(a, mForkEv->get()));
+}
+
+aby3g_event Gpu::recordAux() {
+    aux();
+    mAuxEv->record(mAux);
+    return mAuxEv->get();
+}
+
+void Gpu::joinAux() { GPU_CALL(aby3g_stream_wait_event(mStream, recordAux())); }
 
 void* Gpu::alloc(size_t bytes) {
     size_t cls = sizeClass(bytes);
-    std::lock_guard<std::mutex> lk(mMu);
-    auto it = mFree.find(cls);
-    if (it != mFree.end()) {
-        void* p = it->second;
-        mFree.erase(it);
-        mCached -= cls;
-        return p;
+    {
+        std::lock_guard<std::mutex> lk(mPool->mu);
+        auto it = mPool->free.find(cls);
+        if (it != mPool->free.end()) {
+            void* p = it->second.ptr;
+            for (auto& ev : it->second.fences) GPU_CALL(aby3g_stream_wait_event(mStream, ev->get()));
+            mPool->free.erase(it);
+            mPool->cached -= cls;
+            return p;
+        }
     }
     void* p = nullptr;
     GPU_CALL(aby3g_set_device(mDevice));
     int rc = aby3g_malloc(&p, cls);
     if (rc != 0) {
-        // out of memory: drop the cache (after the stream drains) and retry once
+        // out of memory: drop the cache (after the streams drain) and retry once
         sync();
-        for (auto& kv : mFree) aby3g_free(kv.second);
-        mFree.clear();
-        mCached = 0;
+        trim();
         GPU_CALL(aby3g_malloc(&p, cls));
     }
     return p;
 }
 
-void Gpu::release(void* p, size_t bytes) {
+void Gpu::Pool::release(void* p, size_t bytes, std::vector<std::unique_ptr<Event>>&& fences) {
     if (!p) return;
-    size_t cls = sizeClass(bytes);
-    std::lock_guard<std::mutex> lk(mMu);
-    mFree.emplace(cls, p);
-    mCached += cls;
+    const size_t cls = sizeClass(bytes);
+    std::unique_lock<std::mutex> lk(mu);
+    if (stream) {
+        free.emplace(cls, FreeBlock{p, std::move(fences)});
+        cached += cls;
+        return;
+    }
+    lk.unlock();
+    // the owner is gone: wait for the other streams' last uses, then free
+    for (auto& ev : fences) ev->sync();
+    aby3g_set_device(device);
+    aby3g_device_sync();
+    aby3g_free(p);
 }
 
 void Gpu::trim() {
-    std::lock_guard<std::mutex> lk(mMu);
-    for (auto& kv : mFree) aby3g_free(kv.second);
-    mFree.clear();
-    mCached = 0;
+    std::lock_guard<std::mutex> lk(mPool->mu);
+    bool fenced = false;
+    for (auto& kv : mPool->free) fenced = fenced || !kv.second.fences.empty();
+    if (fenced) aby3g_device_sync();  // fenced blocks may still be read by other streams
+    for (auto& kv : mPool->free) aby3g_free(kv.second.ptr);
+    mPool->free.clear();
+    mPool->cached = 0;
 }
 
 Gpu& Gpu::current() {
@@ -94,12 +146,28 @@ bool Gpu::hasCurrent() { return t_current != nullptr; }
 void DeviceBuffer::reset(Gpu& gpu, size_t bytes) {
     free();
     mGpu = &gpu;
+    mPool = gpu.pool();
     mBytes = bytes;
     mPtr = gpu.alloc(bytes ? bytes : 8);
+    mFences = std::make_unique<Fences>();  // created here: fence() may race from several consumer threads
+}
+
+void DeviceBuffer::fence(aby3g_stream s) {
+    if (!mPtr) return;
+    auto ev = std::make_unique<Event>();
+    ev->record(s);
+    std::lock_guard<std::mutex> lk(mFences->mu);
+    mFences->events.push_back(std::move(ev));
 }
 
 void DeviceBuffer::free() {
-    if (mPtr && mGpu) mGpu->release(mPtr, mBytes ? mBytes : 8);
+    if (mPtr && mPool) {
+        std::vector<std::unique_ptr<Event>> fences;
+        if (mFences) fences = std::move(mFences->events);
+        mPool->release(mPtr, mBytes ? mBytes : 8, std::move(fences));
+    }
+    mFences.reset();
+    mPool.reset();
     mPtr = nullptr;
     mGpu = nullptr;
     mBytes = 0;

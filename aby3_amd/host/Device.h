@@ -32,6 +32,10 @@ private:
 // One party's device context. Allocations are cached per size class and
 // reused in stream order: a block freed after work was enqueued on this
 // party's stream can be handed out again to later work on the same stream.
+// The cache (Pool) is shared with every buffer drawn from it, so a buffer
+// that outlives its Gpu (a matrix declared outside the party's scope, a
+// zero-copy message held by another party) is still freed correctly: after
+// the Gpu is gone it goes straight back to the driver.
 class Gpu {
 public:
     explicit Gpu(int device = 0);
@@ -42,11 +46,32 @@ public:
     int device() const { return mDevice; }
     aby3g_stream stream() const { return mStream; }
     void bind();  // makes this the calling thread's current device/Gpu
-    void sync();
+    void sync();  // drains the main and the auxiliary stream
+
+    // A second in-order stream of this party for work that overlaps the main
+    // stream (e.g. the truncation pair's AES beside the share GEMM).
+    aby3g_stream aux();
+    void forkAux();             // aux waits for all work enqueued so far on the main stream
+    aby3g_event recordAux();    // event: all work enqueued so far on aux
+    void joinAux();             // main waits for all work enqueued so far on aux
+
+    struct FreeBlock {
+        void* ptr;
+        std::vector<std::unique_ptr<Event>> fences;  // other streams' last uses
+    };
+    struct Pool {
+        std::mutex mu;
+        int device = 0;
+        aby3g_stream stream = nullptr;  // owner's stream; null once the Gpu is gone
+        std::multimap<size_t, FreeBlock> free;
+        size_t cached = 0;
+        // returns a block: cached while the owner lives, else freed at once
+        void release(void* p, size_t bytes, std::vector<std::unique_ptr<Event>>&& fences);
+    };
 
     void* alloc(size_t bytes);
-    void release(void* p, size_t bytes);
-    size_t cachedBytes() const { return mCached; }
+    const std::shared_ptr<Pool>& pool() const { return mPool; }
+    size_t cachedBytes() const { return mPool->cached; }
     void trim();  // return cached blocks to the driver
 
     // thread-local current Gpu (set by bind(), e.g. by Sh3Runtime::init)
@@ -56,12 +81,15 @@ public:
 private:
     int mDevice;
     aby3g_stream mStream = nullptr;
-    std::mutex mMu;
-    std::multimap<size_t, void*> mFree;
-    size_t mCached = 0;
+    aby3g_stream mAux = nullptr;
+    std::unique_ptr<Event> mForkEv, mAuxEv;
+    std::shared_ptr<Pool> mPool;
 };
 
-// Owning device allocation from a party's pool (move-only).
+// Owning device allocation from a party's pool (move-only). A buffer handed
+// to another party's stream (zero-copy messages) is fenced by each consumer
+// after it enqueued its last use; the block returns to the owner's pool
+// behind those fences.
 class DeviceBuffer {
 public:
     DeviceBuffer() = default;
@@ -73,8 +101,10 @@ public:
         if (this != &o) {
             free();
             mGpu = o.mGpu;
+            mPool = std::move(o.mPool);
             mPtr = o.mPtr;
             mBytes = o.mBytes;
+            mFences = std::move(o.mFences);
             o.mGpu = nullptr;
             o.mPtr = nullptr;
             o.mBytes = 0;
@@ -90,12 +120,20 @@ public:
     template <class T>
     T* as() const { return static_cast<T*>(mPtr); }
     size_t bytes() const { return mBytes; }
-    Gpu* gpu() const { return mGpu; }
+    Gpu* gpu() const { return mGpu; }  // valid while the allocating Gpu lives
+    // records "stream s is done with this buffer as of now" (thread-safe)
+    void fence(aby3g_stream s);
 
 private:
-    Gpu* mGpu = nullptr;
+    struct Fences {
+        std::mutex mu;
+        std::vector<std::unique_ptr<Event>> events;
+    };
+    Gpu* mGpu = nullptr;  // the allocating party (informational; may be gone)
+    std::shared_ptr<Gpu::Pool> mPool;
     void* mPtr = nullptr;
     size_t mBytes = 0;
+    std::unique_ptr<Fences> mFences;
 };
 
 // Convenience copies on the current Gpu's stream.

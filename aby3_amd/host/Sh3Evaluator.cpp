@@ -100,45 +100,52 @@ Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, const si64Matrix& A, const si64Matri
             shape(mode, A, B, M, K, N);
             const u64 n = M * N, bytes = n * sizeof(i64);
             C.resize(M, N);
-            struct State {
-                DeviceBuffer z, zNext, zPrev;
-            };
-            auto st = std::make_shared<State>();
-            st->z.reset(g, bytes);
+            // z = product - r is revealed to P0 and P1 zero-copy: the buffer
+            // itself is the message (Channel::asyncSendShared)
+            auto z = std::make_shared<DeviceBuffer>(g, bytes);
             size_t wsBytes = 0;
             void* ws = workspace(mode, M, K, N, wsBytes, g);
             if (DEBUG_disable_randomization) {
                 // zero truncation pair: z = product, C = 0
-                GPU_CALL(aby3g_mul_local((int)mode, A.data(), B.data(), st->z.as<i64>(), M, K, N, nullptr, ws, wsBytes,
+                GPU_CALL(aby3g_mul_local((int)mode, A.data(), B.data(), z->as<i64>(), M, K, N, nullptr, ws, wsBytes,
                                          g.stream()));
                 C.setZero();
             } else {
-                // round 1 (Sh3Evaluator.cpp:658-673): z = product - r, C = r/2^d shares
+                // round 1 (Sh3Evaluator.cpp:658-673): the truncation pair
+                // (AES-CTR of both streams) on the auxiliary stream, beside
+                // the share product on the main stream; z = product - r
                 aby3g_trunc_streams ts;
                 std::memcpy(ts.next_seed, mShareGen.mNextSeed.data(), 16);
                 std::memcpy(ts.prev_seed, mShareGen.mPrevSeed.data(), 16);
                 ts.next_off = mShareGen.takeNext(8 * n);
                 ts.prev_off = mShareGen.takePrev(8 * n);
-                GPU_CALL(aby3g_mul_trunc_local((int)mode, A.data(), B.data(), M, K, N, (unsigned)shift, &ts,
-                                               st->z.as<i64>(), C.data(), ws, wsBytes, g.stream()));
+                DeviceBuffer r(g, bytes);
+                g.forkAux();
+                GPU_CALL(aby3g_trunc_tuple(&ts, n, (unsigned)shift, r.as<i64>(), C.data(), g.aux()));
+                aby3g_event rReady = g.recordAux();
+                GPU_CALL(aby3g_mul_sub_local((int)mode, A.data(), B.data(), r.as<i64>(), rReady, z->as<i64>(), M, K,
+                                             N, ws, wsBytes, g.stream()));
+                // r and C's RT were written on aux; the main stream has waited for
+                // them (rReady) before the pass that reads r, so freeing r into
+                // the main stream's pool and later uses of C are ordered
             }
             // reveal z to parties 0 and 1 (:681-684)
             const u64 p = self.getRuntime().mPartyIdx;
             const u64 next = (p + 1) % 3, prev = (p + 2) % 3;
-            if (next < 2) comm.mNext.asyncSendDevice(st->z.data(), bytes, g);
-            if (prev < 2) comm.mPrev.asyncSendDevice(st->z.data(), bytes, g);
+            if (next < 2) comm.mNext.asyncSendShared(z, bytes, g);
+            if (prev < 2) comm.mPrev.asyncSendShared(z, bytes, g);
             if (p < 2) {
-                st->zNext.reset(g, bytes);
-                st->zPrev.reset(g, bytes);
-                auto fu0 = comm.mNext.asyncRecvDevice(st->zNext.data(), bytes, g);
-                auto fu1 = comm.mPrev.asyncRecvDevice(st->zPrev.data(), bytes, g);
+                auto fu0 = comm.mNext.asyncRecvShared(bytes, g);
+                auto fu1 = comm.mPrev.asyncRecvShared(bytes, g);
                 // round 2 (:703-719): C[p] += (z0 + z1 + z2) >> d
-                self.then([st, fu0, fu1, &C, shift, p, n](CommPkg&, Sh3Task& self2) {
-                    fu0.get();
-                    fu1.get();
+                self.then([z, fu0, fu1, &C, shift, p, n](CommPkg&, Sh3Task& self2) {
                     Gpu& g2 = self2.getRuntime().gpu();
-                    GPU_CALL(aby3g_trunc_finalize((int)p, st->zNext.as<i64>(), st->zPrev.as<i64>(), st->z.as<i64>(),
-                                                  (unsigned)shift, C.data(), n, g2.stream()));
+                    auto zn = fu0.getShared();
+                    auto zp = fu1.getShared();
+                    GPU_CALL(aby3g_trunc_finalize((int)p, zn->as<i64>(), zp->as<i64>(), z->as<i64>(), (unsigned)shift,
+                                                  C.data(), n, g2.stream()));
+                    zn->fence(g2.stream());
+                    zp->fence(g2.stream());
                 });
             }
         })

@@ -85,6 +85,8 @@ _SIGS = {
     "aby3g_mul_local": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64, c_uint64,
                                 POINTER(ZeroShare), c_void_p, c_size_t, c_void_p]),
     "aby3g_trunc_tuple": (c_int, [POINTER(TruncStreams), c_uint64, ctypes.c_uint, c_void_p, c_void_p, c_void_p]),
+    "aby3g_mul_sub_local": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64,
+                                    c_uint64, c_void_p, c_size_t, c_void_p]),
     "aby3g_mul_trunc_local": (c_int, [c_int, c_void_p, c_void_p, c_uint64, c_uint64, c_uint64, ctypes.c_uint,
                                       POINTER(TruncStreams), c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "aby3g_trunc_finalize": (c_int, [c_int, c_void_p, c_void_p, c_void_p, ctypes.c_uint, c_void_p, c_uint64,

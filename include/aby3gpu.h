@@ -151,6 +151,15 @@ int aby3g_mul_trunc_local(int mode, const int64_t* A, const int64_t* B, uint64_t
                           const aby3g_trunc_streams* ts, int64_t* z, int64_t* C, void* workspace,
                           size_t workspace_bytes, aby3g_stream stream);
 
+/* The same round-1 z split for overlap (Sh3Evaluator.cpp:667-673):
+ * out = share product - sub, where sub = R of aby3g_trunc_tuple, which the
+ * caller may produce concurrently on another stream. The product kernels
+ * are enqueued at once; the stream waits for `sub_ready` (NULL: no wait)
+ * only before the final pass that reads `sub`. */
+int aby3g_mul_sub_local(int mode, const int64_t* A, const int64_t* B, const int64_t* sub, aby3g_event sub_ready,
+                        int64_t* out, uint64_t M, uint64_t K, uint64_t N, void* workspace, size_t workspace_bytes,
+                        aby3g_stream stream);
+
 /* Round-2 continuation (Sh3Evaluator.cpp:703-719), parties 0 and 1:
  * C[party] += (z_a + z_b + z_own) >> d  over n elements ([2][n] layout). */
 int aby3g_trunc_finalize(int party, const int64_t* z_a, const int64_t* z_b, const int64_t* z_own, unsigned d,

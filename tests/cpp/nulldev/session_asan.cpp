@@ -1,0 +1,44 @@
+// Host-runtime memory-safety driver: sessions of every job created, stepped,
+// checked and destroyed back to back, plus the three-party sim entry points,
+// linked against the null device (gen_nulldev.py) and built with
+// -fsanitize=address by tests/test_host_asan.py. Compute results are
+// meaningless here; only the host code's memory behaviour is under test.
+#include <aby3.h>
+#include <cstdio>
+#include <vector>
+
+static int fail(const char* what) {
+    std::printf("FAIL %s: %s\n", what, aby3h_last_error());
+    return 1;
+}
+
+int main() {
+    const int dev[3] = {0, 0, 0};
+    struct J {
+        int job;
+        std::vector<uint64_t> p;
+        int steps;
+    } jobs[] = {
+        {ABY3H_JOB_MUL_TRUNC, {64, 48, 80, 16, 1}, 3}, {ABY3H_JOB_MUL_TRUNC, {64, 64, 64, 8, 0}, 3},
+        {ABY3H_JOB_MUL, {32, 32, 32, 0}, 3},           {ABY3H_JOB_MUL, {32, 16, 8, 1}, 3},
+        {ABY3H_JOB_MSB, {3000}, 2},                    {ABY3H_JOB_LR, {2048, 16, 64, 16, 11}, 3},
+        {ABY3H_JOB_MERGE_LAYER, {4096}, 2},            {ABY3H_JOB_MUL_TRUNC, {64, 48, 80, 16, 1}, 2},
+    };
+    for (int round = 0; round < 2; ++round)
+        for (auto& j : jobs) {
+            aby3h_session* s = aby3h_session_create(j.job, j.p.data(), (int)j.p.size(), dev, round);
+            if (!s) return fail("create");
+            if (aby3h_session_run(s, j.steps)) return fail("run");
+            if (aby3h_session_check(s) == 2) return fail("check");
+            double ms;
+            uint64_t n;
+            aby3h_session_probe(s, 0, &ms, &n);
+            aby3h_session_destroy(s);
+        }
+    std::vector<int64_t> a(64 * 48, 3), b(48 * 80, 5), sh(6 * 64 * 80), pl(64 * 80);
+    if (aby3h_sim_mul(0, 1, 1, 16, a.data(), b.data(), 64, 48, 80, sh.data(), pl.data())) return fail("sim_mul");
+    std::vector<int64_t> x(300, 1), y(300, 2), o(300), osh(6 * 300);
+    if (aby3h_sim_cipher_gt(0, x.data(), y.data(), 300, o.data(), osh.data())) return fail("sim_cipher_gt");
+    std::printf("session_asan: ok\n");
+    return 0;
+}

@@ -29,14 +29,24 @@ namespace {
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
-constexpr u32 BM = 64, BN = 64, BK = 32;  // output tile, K' per stage
-constexpr u32 kThreads = 256;             // 4 waves, 2 x 2
-constexpr u32 kRec = 256;                 // bytes per (row, stage) record
+constexpr u32 BN = 64, BK = 32;  // output tile width, K' per stage
+constexpr u32 kRec = 256;        // bytes per (row, stage) record
+
+// Tile height of the share GEMM: 128 (8 waves, two per SIMD) by default,
+// 64 (4 waves, one per SIMD) with ABY3G_GEMM_TBM=64 -- kept for A/B runs.
+inline u32 gemm_tbm() {
+    static const u32 v = [] {
+        const char* e = getenv("ABY3G_GEMM_TBM");
+        return (e && atoi(e) == 64) ? 64u : 128u;
+    }();
+    return v;
+}
 
 inline u64 roundup(u64 x, u64 m) { return (x + m - 1) / m * m; }
 
 struct GemmPlan {
     u64 M, K, N;
+    u32 tbm;             // tile height (64 or 128)
     u64 Mp, Np, Kp, Kc;  // padded sizes; Kc = K' = 2*Kp
     u32 splits;          // split-K factor
     u64 kPerSplit;       // K' per split (multiple of BK)
@@ -48,16 +58,17 @@ GemmPlan plan_gemm(u64 M, u64 K, u64 N) {
     p.M = M;
     p.K = K;
     p.N = N;
-    p.Mp = roundup(M ? M : 1, BM);
+    p.tbm = gemm_tbm();
+    p.Mp = roundup(M ? M : 1, p.tbm);
     p.Np = roundup(N ? N : 1, BN);
     p.Kp = roundup(K ? K : 1, 16);
     p.Kc = 2 * p.Kp;
     const u64 stages = p.Kc / BK;
-    const u64 tiles = (p.Mp / BM) * (p.Np / BN);
-    // Enough workgroups for two per CU, at least 8 stages per split, and
+    const u64 tiles = (p.Mp / p.tbm) * (p.Np / BN);
+    // Enough workgroups for one per CU, at least 8 stages per split, and
     // K' per split <= 8192 so every i32 plane stays exact.
     u32 s = 1;
-    while (tiles * s < 512 && stages / (2 * s) >= 8) s *= 2;
+    while (tiles * s < 256 && stages / (2 * s) >= 8) s *= 2;
     while ((stages + s - 1) / s * BK > 8192) s *= 2;
     p.splits = s;
     p.kPerSplit = (stages + s - 1) / s * BK;
@@ -151,41 +162,94 @@ __global__ void __launch_bounds__(256) k_digits(const i64* __restrict__ A0, cons
 }
 
 // One 64x64 output tile over K' range [kBegin, kBegin + kLen) of split z.
-__global__ void __launch_bounds__(kThreads, 2) k_share_gemm(const u8* __restrict__ Ad, const u8* __restrict__ Bd,
-                                                            u64 M, u64 N, u64 stagesTotal, u64 stagesPerSplit,
-                                                            i64* __restrict__ P) {
-    __shared__ __attribute__((aligned(16))) u8 lds[2][2][BM * kRec];  // [buf][A|B][row][256 B]
+// XCD-aware tile order. Workgroup ids are dealt round-robin to the 8 XCDs
+// (id % 8), each with its own 4 MiB L2. Remap so every XCD gets one
+// contiguous range of the tile order, and order tiles split-major, then in
+// groups of 8 row-panels, column-major within a group: an XCD's range is then
+// a compact block of tiles (2 splits x 16 x 16 tiles: one split, 8 x 8 tiles
+// per XCD) and reads 8 A and 8 B digit panels instead of all 16 B panels.
+struct TileCoord {
+    u32 tm, tn, split;
+};
+__device__ __forceinline__ TileCoord tile_of(u32 pid, u32 TM, u32 TN, u32 splits) {
+    const u32 T = TM * TN * splits;
+    const u32 per = (T + 7) / 8;
+    const u32 xcd = pid % 8, idx = pid / 8;
+    // a bijection when T is a multiple of 8; otherwise keep the launch order
+    const u32 np = (per * 8 == T) ? xcd * per + idx : pid;
+    const u32 tilesPerSplit = TM * TN;
+    TileCoord c;
+    c.split = np / tilesPerSplit;
+    const u32 rem = np % tilesPerSplit;
+    constexpr u32 G = 8;
+    const u32 group = rem / (G * TN), first = group * G;
+    const u32 gm = min(G, TM - first);
+    const u32 inGroup = rem % (G * TN);
+    c.tm = first + inGroup % gm;
+    c.tn = inGroup / gm;
+    return c;
+}
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+
+// One TBM x 64 output tile over the K' stages [s0, s1) of its split;
+// TBM / 32 x 2 waves, each a 32 x 32 tile with 8 digit-plane accumulators.
+//
+// Staging: LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction)
+// into an NBUF-deep ring of stages. The LDS image is lane-linear, so the bank
+// swizzle (chunk g of row r at slot g ^ (r&15)) is applied on the per-lane
+// SOURCE address. Stage i + NBUF - 1 is issued right after the barrier of
+// stage i; the wait is a counted vmcnt (the pieces of the later stages stay
+// in flight) and the barrier a raw s_barrier, so the DMA is not drained by
+// it. Variants: TBM 64 / NBUF 3 (4 waves, one per SIMD) and TBM 128 / NBUF 2
+// (8 waves, two per SIMD: a second wave to issue MFMAs while one waits).
+//
+// Epilogue: recombine the 8 planes in i64; one split -> out = product (-
+// sub), several -> the split's slab of P.
+template <u32 TBM, u32 NBUF>
+__global__ void __launch_bounds__(TBM / 32 * 2 * 64, 1)
+    k_share_gemm(const u8* __restrict__ Ad, const u8* __restrict__ Bd, u64 M, u64 N, u64 stagesTotal,
+                 u64 stagesPerSplit, u32 TM, u32 TN, u32 splits, i64* __restrict__ P, const i64* __restrict__ sub) {
+    constexpr u32 kWaves = TBM / 32 * 2, kT = kWaves * 64;
+    constexpr u32 kStageA = TBM * kRec, kStageB = BN * kRec, kStage = kStageA + kStageB;
+    constexpr u32 kPiecesA = TBM / 4, kPieces = kPiecesA + BN / 4, kPerWave = kPieces / kWaves;
+    static_assert(kPieces % kWaves == 0, "pieces must split evenly over waves");
+    __shared__ __attribute__((aligned(16))) u8 lds[NBUF * kStage];  // [buf][A rows | B rows][256 B]
     const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const u64 m0 = (u64)blockIdx.x * BM, n0 = (u64)blockIdx.y * BN;
-    const u64 s0 = (u64)blockIdx.z * stagesPerSplit;
+    const TileCoord tc = tile_of(blockIdx.x, TM, TN, splits);
+    const u64 m0 = (u64)tc.tm * TBM, n0 = (u64)tc.tn * BN;
+    const u64 s0 = (u64)tc.split * stagesPerSplit;
     const u64 s1 = min(stagesTotal, s0 + stagesPerSplit);
+    i64* dst = P + (splits > 1 ? (u64)tc.split * M * N : 0);
     if (s0 >= s1) {
         // empty split: still define its slab
-        for (u32 i = tid; i < BM * BN; i += kThreads) {
+        for (u32 i = tid; i < TBM * BN; i += kT) {
             u64 m = m0 + i / BN, n = n0 + i % BN;
-            if (m < M && n < N) P[(u64)blockIdx.z * M * N + m * N + n] = 0;
+            if (m < M && n < N) dst[m * N + n] = 0;
         }
         return;
     }
+    const u32 nst = (u32)(s1 - s0);
 
-    // global -> LDS staging: 1024 chunks of 16 B per operand tile, 4 per thread
-    v4i ra[4], rb[4];
-    auto gload = [&](u64 st) {
+    // this wave's DMA pieces: piece q covers 4 records (A rows, then B rows)
+    const u32 lrow = lane >> 4, lslot = lane & 15;
+    const u8* src[kPerWave];
+    u32 ldsOff[kPerWave];
 #pragma unroll
-        for (int it = 0; it < 4; ++it) {
-            const u32 q = it * kThreads + tid;
-            const u32 row = q >> 4, slot = q & 15, g = slot ^ (row & 15);
-            ra[it] = *reinterpret_cast<const v4i*>(Ad + ((m0 + row) * stagesTotal + st) * kRec + g * 16);
-            rb[it] = *reinterpret_cast<const v4i*>(Bd + ((n0 + row) * stagesTotal + st) * kRec + g * 16);
-        }
-    };
-    auto lstore = [&](int buf) {
+    for (u32 j = 0; j < kPerWave; ++j) {
+        const u32 q = wave * kPerWave + j;
+        const bool isA = q < kPiecesA;
+        const u32 r = 4 * (isA ? q : q - kPiecesA) + lrow;
+        const u32 g = lslot ^ (r & 15);
+        src[j] = (isA ? Ad + (m0 + r) * stagesTotal * kRec : Bd + (n0 + r) * stagesTotal * kRec) + g * 16;
+        ldsOff[j] = (isA ? 0 : kStageA) + 4 * (isA ? q : q - kPiecesA) * kRec;
+    }
+    auto issue = [&](u64 st, u32 buf) {
 #pragma unroll
-        for (int it = 0; it < 4; ++it) {
-            const u32 q = it * kThreads + tid;
-            *reinterpret_cast<v4i*>(&lds[buf][0][q * 16]) = ra[it];
-            *reinterpret_cast<v4i*>(&lds[buf][1][q * 16]) = rb[it];
-        }
+        for (u32 j = 0; j < kPerWave; ++j)
+            __builtin_amdgcn_global_load_lds((glb_void*)(src[j] + st * kRec), (lds_void*)(lds + buf * kStage + ldsOff[j]),
+                                             16, 0, 0);
     };
 
     v16i acc[8];
@@ -195,33 +259,42 @@ __global__ void __launch_bounds__(kThreads, 2) k_share_gemm(const u8* __restrict
     const u32 wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
     const u32 fr = lane & 31, fh = lane >> 5;
     const u32 rowA = wr + fr, rowB = wc + fr;
+    u32 offRA[8], offRB[8];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+        const u32 g = 2 * p + fh;
+        offRA[p] = rowA * kRec + ((g ^ (rowA & 15)) * 16);
+        offRB[p] = kStageA + rowB * kRec + ((g ^ (rowB & 15)) * 16);
+    }
 
-    gload(s0);
-    lstore(0);
-    __syncthreads();
-    int buf = 0;
-    for (u64 st = s0; st < s1; ++st) {
-        const bool more = st + 1 < s1;
-        if (more) gload(st + 1);
+#pragma unroll
+    for (u32 k = 0; k + 1 < NBUF; ++k)
+        if (k < nst) issue(s0 + k, k);
+    u32 buf = 0;
+    for (u32 i = 0; i < nst; ++i) {
+        // stage i landed: leave the pieces of the stages issued after it in flight
+        if (NBUF == 3 && i + 1 < nst)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPerWave) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (i + NBUF - 1 < nst) issue(s0 + i + NBUF - 1, (buf + NBUF - 1) % NBUF);
+        const u8* ls = lds + buf * kStage;
         v4i a[8], b[8];
 #pragma unroll
         for (int p = 0; p < 8; ++p) {
-            const u32 g = 2 * p + fh;
-            a[p] = *reinterpret_cast<const v4i*>(&lds[buf][0][rowA * kRec + ((g ^ (rowA & 15)) * 16)]);
-            b[p] = *reinterpret_cast<const v4i*>(&lds[buf][1][rowB * kRec + ((g ^ (rowB & 15)) * 16)]);
+            a[p] = *reinterpret_cast<const v4i*>(ls + offRA[p]);
+            b[p] = *reinterpret_cast<const v4i*>(ls + offRB[p]);
         }
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
 #pragma unroll
             for (int p = 0; p <= s; ++p) acc[s] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[p], b[s - p], acc[s], 0, 0, 0);
         }
-        if (more) lstore(buf ^ 1);
-        __syncthreads();
-        buf ^= 1;
+        buf = buf + 1 == NBUF ? 0 : buf + 1;
     }
 
-    // recombine planes in i64 and store the split's slab
-    i64* slab = P + (u64)blockIdx.z * M * N;
+    // recombine planes in i64 and store
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         u64 v = 0;
@@ -229,7 +302,11 @@ __global__ void __launch_bounds__(kThreads, 2) k_share_gemm(const u8* __restrict
         for (int s = 0; s < 8; ++s) v += (u64)(i64)acc[s][r] << (8 * s);
         const u64 m = m0 + wr + (r & 3) + 8 * (r >> 2) + 4 * fh;
         const u64 n = n0 + wc + fr;
-        if (m < M && n < N) slab[m * N + n] = (i64)v;
+        if (m < M && n < N) {
+            const u64 i = m * N + n;
+            if (sub) v -= (u64)sub[i];
+            dst[i] = (i64)v;
+        }
     }
 }
 
@@ -290,8 +367,11 @@ Workspace carve(const GemmPlan& p, void* ws) {
     return w;
 }
 
-// Runs the digit split and the MFMA GEMM; leaves `splits` partial slabs in w.P.
-void run_gemm(const GemmPlan& p, const i64* A, const i64* B, const Workspace& w, hipStream_t s) {
+// Runs the digit split and the MFMA GEMM. One split: the GEMM writes the
+// product (minus `sub`, when given) straight to `out`; several: `splits`
+// partial slabs in w.P (the caller reduces them).
+void run_gemm(const GemmPlan& p, const i64* A, const i64* B, const Workspace& w, hipStream_t s, i64* out = nullptr,
+              const i64* sub = nullptr, hipEvent_t subReady = nullptr) {
     const i64* A0 = A;
     const i64* A1 = A + p.M * p.K;
     const i64* B0 = B;
@@ -300,9 +380,18 @@ void run_gemm(const GemmPlan& p, const i64* A, const i64* B, const Workspace& w,
     const u64 aTiles = (p.Mp / kDigitTile) * stages, bTiles = (p.Np / kDigitTile) * stages;
     launch(PROBE_DIGITS, k_digits, dim3((u32)(aTiles + bTiles)), dim3(256), 0, s, A0, A1, B0, B1, p.M, p.K, p.N, p.Kp,
            aTiles, stages, w.Ad, w.Bd);
+    const u32 TM = (u32)(p.Mp / p.tbm), TN = (u32)(p.Np / BN);
+    const bool direct = p.splits == 1 && out != nullptr;
+    if (direct && sub && subReady) ABY3G_CHECK_HIP(hipStreamWaitEvent(s, subReady, 0));
     MfmaTurn turn(s);
-    launch(PROBE_GEMM, k_share_gemm, dim3((u32)(p.Mp / BM), (u32)(p.Np / BN), p.splits), dim3(kThreads), 0, s,
-           (const u8*)w.Ad, (const u8*)w.Bd, p.M, p.N, stages, p.kPerSplit / BK, w.P);
+    i64* dst = direct ? out : w.P;
+    const i64* sb = direct ? sub : nullptr;
+    if (p.tbm == 64)
+        launch(PROBE_GEMM, k_share_gemm<64, 3>, dim3(TM * TN * p.splits), dim3(256), 0, s, (const u8*)w.Ad,
+               (const u8*)w.Bd, p.M, p.N, stages, p.kPerSplit / BK, TM, TN, p.splits, dst, sb);
+    else
+        launch(PROBE_GEMM, k_share_gemm<128, 2>, dim3(TM * TN * p.splits), dim3(512), 0, s, (const u8*)w.Ad,
+               (const u8*)w.Bd, p.M, p.N, stages, p.kPerSplit / BK, TM, TN, p.splits, dst, sb);
 }
 
 void check_ws(const GemmPlan& p, void* ws, size_t bytes) {
@@ -339,6 +428,12 @@ int aby3g_mul_local(int mode, const int64_t* A, const int64_t* B, int64_t* C0, u
         GemmPlan p = plan_gemm(M, K, N);
         check_ws(p, workspace, workspace_bytes);
         Workspace w = carve(p, workspace);
+        if (p.splits == 1) {
+            // the GEMM writes the product into C0; the zero-share is added in place
+            run_gemm(p, A, B, w, S(stream), C0);
+            if (zs) launch_finish_zero_share(SrcSlabs{C0, 1, n}, n, *zs, C0, S(stream));
+            return;
+        }
         run_gemm(p, A, B, w, S(stream));
         SrcSlabs src{w.P, p.splits, n};
         if (zs)
@@ -364,6 +459,11 @@ int aby3g_mul_trunc_local(int mode, const int64_t* A, const int64_t* B, uint64_t
         GemmPlan p = plan_gemm(M, K, N);
         check_ws(p, workspace, workspace_bytes);
         Workspace w = carve(p, workspace);
+        if (p.splits == 1) {
+            run_gemm(p, A, B, w, S(stream), z);  // product into z, then z -= r in place
+            launch_finish_trunc(SrcSlabs{z, 1, n}, *ts, n, d, nullptr, C, C + n, z, S(stream));
+            return;
+        }
         run_gemm(p, A, B, w, S(stream));
         SrcSlabs src{w.P, p.splits, n};
         launch_finish_trunc(src, *ts, n, d, nullptr, C, C + n, z, S(stream));
@@ -386,6 +486,11 @@ int aby3g_mul_sub_local(int mode, const int64_t* A, const int64_t* B, const int6
         GemmPlan p = plan_gemm(M, K, N);
         check_ws(p, workspace, workspace_bytes);
         Workspace w = carve(p, workspace);
+        if (p.splits == 1) {
+            // out = product - sub in the GEMM's epilogue (waits for sub_ready before the GEMM)
+            run_gemm(p, A, B, w, S(stream), out, sub, (hipEvent_t)sub_ready);
+            return;
+        }
         run_gemm(p, A, B, w, S(stream));
         if (sub_ready) ABY3G_CHECK_HIP(hipStreamWaitEvent(S(stream), (hipEvent_t)sub_ready, 0));
         launch_finish_plain(SrcSlabsMinus{w.P, p.splits, n, sub}, n, out, S(stream));

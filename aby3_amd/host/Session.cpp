@@ -170,6 +170,7 @@ struct LrJob : Job {
     std::unique_ptr<aby3ML> ml[3];
     SgdState st[3];
     std::vector<u32> perm;
+    DeviceBuffer dperm[3];  // the permutation, resident per party
     u64 iter[3] = {0, 0, 0};
     LrJob(u64 n_, u64 d_, u64 b_, u64 D_, u64 aB_) : n(n_), d(d_), B(b_), D(D_), aB(aB_) {
         // synthetic LogisticModelGen-shaped data (main-logistic.cpp:82-100):
@@ -207,11 +208,13 @@ struct LrJob : Job {
             p.enc.remoteIntMatrix(p.rt, sW[p.idx]).get();
         }
         ml[p.idx] = std::make_unique<aby3ML>(p.rt, p.enc, p.eval, D);
+        dperm[p.idx].reset(p.rt.gpu(), n * 4);
+        toDevice(dperm[p.idx].data(), perm.data(), n * 4, p.rt.gpu());
     }
     void step(PartyCtx& p) override {
         const u64 start = (iter[p.idx]++ * B) % (n - B + 1);
-        std::vector<u32> idx(perm.begin() + start, perm.begin() + start + B);
-        sgdLogisticStep(*ml[p.idx], sX[p.idx], sY[p.idx], sW[p.idx], idx, aB, st[p.idx]);
+        sgdLogisticStep(*ml[p.idx], sX[p.idx], sY[p.idx], sW[p.idx], dperm[p.idx].as<u32>() + start, B, aB,
+                        st[p.idx]);
     }
     // plaintext fixed-point restatement of the same iterations (floor shifts as
     // Sh3FixedPoint.h:200-210, the sigmoid of aby3ML.h:121-139); the protocol's

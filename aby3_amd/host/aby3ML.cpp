@@ -20,19 +20,15 @@ void aby3ML::logisticFunc(const si64Matrix& Y, si64Matrix& out) {
     mLogistic.eval(mRt.noDependencies(), Y, out, mD, mEval).get();
 }
 
-void sgdLogisticStep(aby3ML& ml, const si64Matrix& X, const si64Matrix& Y, si64Matrix& w,
-                     const std::vector<u32>& batchIdx, u64 aB, SgdState& st) {
+void sgdLogisticStep(aby3ML& ml, const si64Matrix& X, const si64Matrix& Y, si64Matrix& w, const u32* batchIdx,
+                     u64 B, u64 aB, SgdState& st) {
     Gpu& g = ml.mRt.gpu();
-    const u64 B = batchIdx.size(), d = X.cols();
-    if (st.idx.bytes() < B * 4) st.idx.reset(g, B * 4);
-    GPU_CALL(aby3g_memcpy(st.idx.data(), batchIdx.data(), B * 4, 0, g.stream()));
+    const u64 d = X.cols();
     // extractBatch (Regression.h:42-58)
     st.XX.resize(B, d);
     st.YY.resize(B, 1);
-    GPU_CALL(aby3g_i64_gather_rows(X.data(), X.rows(), d, st.idx.as<u32>(), B, st.XX.data(), g.stream()));
-    GPU_CALL(aby3g_i64_gather_rows(Y.data(), Y.rows(), 1, st.idx.as<u32>(), B, st.YY.data(), g.stream()));
-    // the index upload reads host memory that the caller may reuse
-    g.sync();
+    GPU_CALL(aby3g_i64_gather_rows(X.data(), X.rows(), d, batchIdx, B, st.XX.data(), g.stream()));
+    GPU_CALL(aby3g_i64_gather_rows(Y.data(), Y.rows(), 1, batchIdx, B, st.YY.data(), g.stream()));
     ml.mul(st.XX, w, st.xw);                 // xw = XX * w
     ml.logisticFunc(st.xw, st.fxw);          // f(xw)
     st.err.resize(B, 1);                     // error = f - YY
@@ -41,6 +37,15 @@ void sgdLogisticStep(aby3ML& ml, const si64Matrix& X, const si64Matrix& Y, si64M
     GPU_CALL(aby3g_i64_transpose(st.XX.data(), B, d, st.XXt.data(), g.stream()));
     ml.mulTruncate(st.XXt, st.err, st.update, aB);  // update = XX^T err / 2^(D + aB)
     GPU_CALL(aby3g_i64_lincomb(2 * d, 1, w.data(), -1, st.update.data(), 0, w.data(), g.stream()));
+}
+
+void sgdLogisticStep(aby3ML& ml, const si64Matrix& X, const si64Matrix& Y, si64Matrix& w,
+                     const std::vector<u32>& batchIdx, u64 aB, SgdState& st) {
+    Gpu& g = ml.mRt.gpu();
+    const u64 B = batchIdx.size();
+    if (st.idx.bytes() < B * 4) st.idx.reset(g, B * 4);
+    toDevice(st.idx.data(), batchIdx.data(), B * 4, g);
+    sgdLogisticStep(ml, X, Y, w, st.idx.as<u32>(), B, aB, st);
 }
 
 }  // namespace aby3

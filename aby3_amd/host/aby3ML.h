@@ -30,10 +30,15 @@ struct SgdState {
     DeviceBuffer idx;
 };
 
-// One SGD_Logistic iteration on the batch `batchIdx` of (X, Y):
+// One SGD_Logistic iteration on the batch of B row indices at device pointer
+// `batchIdx` (e.g. a slice of a device-resident permutation, so no host
+// upload or stream sync sits in the iteration) of (X, Y):
 //   XX, YY = extractBatch; xw = mul(XX, w); fxw = logistic(xw);
 //   err = fxw - YY; update = mulTruncate(XX^T, err, aB); w = w - update
 // (Regression.h:252-287).
+void sgdLogisticStep(aby3ML& ml, const si64Matrix& X, const si64Matrix& Y, si64Matrix& w,
+                     const u32* batchIdx, u64 B, u64 aB, SgdState& st);
+// Host-index convenience form: uploads the indices (and waits for the upload).
 void sgdLogisticStep(aby3ML& ml, const si64Matrix& X, const si64Matrix& Y, si64Matrix& w,
                      const std::vector<u32>& batchIdx, u64 aB, SgdState& st);
 

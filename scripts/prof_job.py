@@ -9,13 +9,15 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from aby3_amd import native as nt  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--job", choices=["mul", "msb"], required=True)
+ap.add_argument("--job", choices=["mul", "msb", "lr"], required=True)
 ap.add_argument("--steps", type=int, default=4)
 a = ap.parse_args()
 if a.job == "mul":
     s = nt.Session(nt.JOB_MUL_TRUNC, [1024, 1024, 1024, 16, 1], probe=False)
-else:
+elif a.job == "msb":
     s = nt.Session(nt.JOB_MSB, [1 << 20], probe=False)
+else:
+    s = nt.Session(nt.JOB_LR, [100000, 128, 256, 16, 11], probe=False)
 s.run(a.steps)
 s.close()
 print("done", a.job, a.steps)

@@ -72,6 +72,78 @@ __global__ void __launch_bounds__(kGateBlock) k_bin_gates(const aby3g_gate* __re
     *reinterpret_cast<u64x2*>(s1 + g.out * words + w) = o1;
 }
 
+// One whole communication level per launch. A workgroup owns 32 consecutive
+// words (2048 rows) of every wire; its 256 threads are 8 gate slots x 32
+// word lanes. It first unpacks the previous level's received AND shares
+// into share 1, then runs the level's gate batches in order, the 8 slots
+// striding over a batch's (independent) gates, with a workgroup barrier
+// between batches: a gate only ever reads words of its own rows, so the
+// per-workgroup barrier orders every dependency of the level.
+constexpr u32 kLevelWords = 32;
+
+__device__ __forceinline__ void gate_word(const aby3g_gate& g, u64* s0, u64* s1, u64 words, u64 w,
+                                          const u64* __restrict__ z, u64* __restrict__ sendbuf) {
+    const u64 x0 = s0[g.in0 * words + w], x1 = s1[g.in0 * words + w];
+    u64 o0, o1;
+    switch (g.type) {
+        case ABY3G_GATE_COPY:
+            o0 = x0;
+            o1 = x1;
+            break;
+        case ABY3G_GATE_INV:
+            o0 = ~x0;
+            o1 = ~x1;
+            break;
+        default: {
+            const u64 y0 = s0[g.in1 * words + w], y1 = s1[g.in1 * words + w];
+            if (g.type == ABY3G_GATE_XOR) {
+                o0 = x0 ^ y0;
+                o1 = x1 ^ y1;
+                break;
+            }
+            if (g.type == ABY3G_GATE_NXOR) {
+                o0 = ~(x0 ^ y0);
+                o1 = ~(x1 ^ y1);
+                break;
+            }
+            u64 r;
+            if (g.type == ABY3G_GATE_AND)
+                r = (x0 & y0) ^ (x0 & y1) ^ (x1 & y0);
+            else if (g.type == ABY3G_GATE_OR)
+                r = (x0 & y0) ^ (x0 & y1) ^ (x1 & y0) ^ x0 ^ y0;
+            else if (g.type == ABY3G_GATE_NOR)
+                r = (~x0 & ~y0) ^ (~x0 & ~y1) ^ (~x1 & ~y0);
+            else /* NA_AND */
+                r = (~x0 & y0) ^ (~x0 & y1) ^ (~x1 & y0);
+            r ^= z[(u64)g.z_row * words + w];
+            s0[g.out * words + w] = r;
+            sendbuf[(u64)g.send_row * words + w] = r;
+            return;
+        }
+    }
+    s0[g.out * words + w] = o0;
+    s1[g.out * words + w] = o1;
+}
+
+__global__ void __launch_bounds__(256) k_bin_level(const aby3g_gate* __restrict__ gates,
+                                                   const u32* __restrict__ batch_ends, u32 nbatches,
+                                                   const u64* __restrict__ recv, const u32* __restrict__ unpack_wires,
+                                                   u32 nunpack, u64* __restrict__ mem, u64 wires, u64 words,
+                                                   const u64* __restrict__ z, u64* __restrict__ sendbuf) {
+    const u32 lane = threadIdx.x & 31, slot = threadIdx.x >> 5;
+    const u64 w = (u64)blockIdx.x * kLevelWords + lane;
+    u64* s0 = mem;
+    u64* s1 = mem + wires * words;
+    for (u32 j = slot; j < nunpack; j += 8) s1[(u64)unpack_wires[j] * words + w] = recv[(u64)j * words + w];
+    u32 begin = 0;
+    for (u32 b = 0; b < nbatches; ++b) {
+        __syncthreads();
+        const u32 end = batch_ends[b];
+        for (u32 gi = begin + slot; gi < end; gi += 8) gate_word(gates[gi], s0, s1, words, w, z, sendbuf);
+        begin = end;
+    }
+}
+
 __global__ void __launch_bounds__(kGateBlock) k_bin_unpack(const u64* __restrict__ recv, const u32* __restrict__ outw,
                                                            u64* __restrict__ mem, u64 wires, u64 words) {
     const u32 j = blockIdx.y;
@@ -84,8 +156,12 @@ __global__ void __launch_bounds__(kGateBlock) k_bin_unpack(const u64* __restrict
 
 // One wave per (64-row word w, 64-bit column c): lane r holds row 64w + r;
 // the ballot of bit b over the wave is word w of wire b (LSB = row 64w).
+// blockIdx.y = share: input share s at in + s * rows * cols64, its wire rows
+// at wrows + s * shareStride
 __global__ void __launch_bounds__(256) k_bits_to_wires(const i64* __restrict__ in, u64 rows, u64 cols64, u32 nbits,
-                                                       u64* __restrict__ wrows, u64 words) {
+                                                       u64* __restrict__ wrows, u64 shareStride, u64 words) {
+    in += (u64)blockIdx.y * rows * cols64;
+    wrows += (u64)blockIdx.y * shareStride;
     const u32 lane = threadIdx.x & 63;
     const u64 waveId = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const u64 nw = words * cols64;
@@ -103,11 +179,16 @@ __global__ void __launch_bounds__(256) k_bits_to_wires(const i64* __restrict__ i
     if (bit < nbits) wrows[bit * words + w] = mine;
 }
 
-__global__ void __launch_bounds__(256) k_wires_to_bits(const u64* __restrict__ mem, const u32* __restrict__ wires,
-                                                       u32 nbits, u64 words, i64* __restrict__ out, u64 rows) {
+// blockIdx.y = share: wire rows of share s at mem + s * shareStride, output
+// share s at out + s * rows * ceil(nbits / 64)
+__global__ void __launch_bounds__(256) k_wires_to_bits(const u64* __restrict__ mem, u64 shareStride,
+                                                       const u32* __restrict__ wires, u32 nbits, u64 words,
+                                                       i64* __restrict__ out, u64 rows) {
     const u32 lane = threadIdx.x & 63;
     const u64 waveId = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const u64 cols = (nbits + 63) / 64;
+    mem += (u64)blockIdx.y * shareStride;
+    out += (u64)blockIdx.y * rows * cols;
     const u64 nw = ((rows + 63) / 64) * cols;
     if (waveId >= nw) return;
     const u64 rw = (rows + 63) / 64;
@@ -142,6 +223,17 @@ int aby3g_bin_gates(const aby3g_gate* gates, uint32_t ngates, uint64_t* mem, uin
     });
 }
 
+int aby3g_bin_level(const aby3g_gate* gates, const uint32_t* batch_ends, uint32_t nbatches, const uint64_t* recvbuf,
+                    const uint32_t* unpack_wires, uint32_t nunpack, uint64_t* mem, uint64_t wires, uint64_t words,
+                    const uint64_t* z, uint64_t* sendbuf, aby3g_stream stream) {
+    return guarded([&] {
+        ABY3G_REQUIRE(words % kLevelWords == 0, "words must be padded to a multiple of 32 (2048 rows)");
+        if ((!nbatches && !nunpack) || !words) return;
+        launch(PROBE_BINARY, k_bin_level, dim3((u32)(words / kLevelWords)), dim3(256), 0, S(stream), gates, batch_ends,
+               nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf);
+    });
+}
+
 int aby3g_bin_unpack(const uint64_t* recvbuf, const uint32_t* out_wires, uint32_t n, uint64_t* mem, uint64_t wires,
                      uint64_t words, aby3g_stream stream) {
     return guarded([&] {
@@ -153,27 +245,43 @@ int aby3g_bin_unpack(const uint64_t* recvbuf, const uint32_t* out_wires, uint32_
     });
 }
 
+static void bits_to_wires(const int64_t* in, u64 rows, u64 cols64, u32 nbits, u64* wire_rows, u64 shareStride,
+                          u32 shares, u64 words, hipStream_t s) {
+    ABY3G_REQUIRE(nbits <= cols64 * 64, "nbits exceeds input columns");
+    ABY3G_REQUIRE(words * 64 >= rows, "words too small for rows");
+    if (!nbits || !words) return;
+    u64 waves = words * cols64;
+    launch(PROBE_OTHER, k_bits_to_wires, dim3((u32)((waves * 64 + 255) / 256), shares), dim3(256), 0, s, in, rows,
+           cols64, nbits, wire_rows, shareStride, words);
+}
+
+static void wires_to_bits(const u64* mem, u64 shareStride, u32 shares, const u32* wires, u32 nbits, u64 words,
+                          int64_t* out, u64 rows, hipStream_t s) {
+    ABY3G_REQUIRE(words * 64 >= rows, "words too small for rows");
+    if (!nbits || !rows) return;
+    u64 waves = ((rows + 63) / 64) * ((nbits + 63) / 64);
+    launch(PROBE_OTHER, k_wires_to_bits, dim3((u32)((waves * 64 + 255) / 256), shares), dim3(256), 0, s, mem,
+           shareStride, wires, nbits, words, out, rows);
+}
+
 int aby3g_bits_to_wires(const int64_t* in, uint64_t rows, uint64_t cols64, uint32_t nbits, uint64_t* wire_rows,
                         uint64_t words, aby3g_stream stream) {
-    return guarded([&] {
-        ABY3G_REQUIRE(nbits <= cols64 * 64, "nbits exceeds input columns");
-        ABY3G_REQUIRE(words * 64 >= rows, "words too small for rows");
-        if (!nbits || !words) return;
-        u64 waves = words * cols64;
-        launch(PROBE_OTHER, k_bits_to_wires, dim3((u32)((waves * 64 + 255) / 256)), dim3(256), 0, S(stream), in, rows,
-               cols64, nbits, wire_rows, words);
-    });
+    return guarded([&] { bits_to_wires(in, rows, cols64, nbits, wire_rows, 0, 1, words, S(stream)); });
+}
+
+int aby3g_bits_to_wires2(const int64_t* in, uint64_t rows, uint64_t cols64, uint32_t nbits, uint64_t* wire_rows,
+                         uint64_t share_stride, uint64_t words, aby3g_stream stream) {
+    return guarded([&] { bits_to_wires(in, rows, cols64, nbits, wire_rows, share_stride, 2, words, S(stream)); });
 }
 
 int aby3g_wires_to_bits(const uint64_t* mem_share, const uint32_t* wires, uint32_t nbits, uint64_t words, int64_t* out,
                         uint64_t rows, aby3g_stream stream) {
-    return guarded([&] {
-        ABY3G_REQUIRE(words * 64 >= rows, "words too small for rows");
-        if (!nbits || !rows) return;
-        u64 waves = ((rows + 63) / 64) * ((nbits + 63) / 64);
-        launch(PROBE_OTHER, k_wires_to_bits, dim3((u32)((waves * 64 + 255) / 256)), dim3(256), 0, S(stream),
-               mem_share, wires, nbits, words, out, rows);
-    });
+    return guarded([&] { wires_to_bits(mem_share, 0, 1, wires, nbits, words, out, rows, S(stream)); });
+}
+
+int aby3g_wires_to_bits2(const uint64_t* mem, uint64_t share_stride, const uint32_t* wires, uint32_t nbits,
+                         uint64_t words, int64_t* out, uint64_t rows, aby3g_stream stream) {
+    return guarded([&] { wires_to_bits(mem, share_stride, 2, wires, nbits, words, out, rows, S(stream)); });
 }
 
 }  // extern "C"

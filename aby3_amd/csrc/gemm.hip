@@ -44,6 +44,10 @@ inline u32 gemm_tbm() {
 
 inline u64 roundup(u64 x, u64 m) { return (x + m - 1) / m * m; }
 
+// GEMMs up to this many product terms run on the VALU in one fused kernel.
+constexpr u64 kSmallGemmTerms = 1ull << 23;
+inline bool small_gemm(u64 M, u64 K, u64 N) { return M * N * K <= kSmallGemmTerms; }
+
 struct GemmPlan {
     u64 M, K, N;
     u32 tbm;             // tile height (64 or 128)
@@ -406,8 +410,12 @@ using namespace aby3g;
 
 extern "C" {
 
+int aby3g_mul_prefers_fused(int mode, uint64_t M, uint64_t K, uint64_t N) {
+    return mode != ABY3G_MUL_GEMM || small_gemm(M, K, N);
+}
+
 size_t aby3g_mul_workspace_bytes(int mode, uint64_t M, uint64_t K, uint64_t N) {
-    if (mode != ABY3G_MUL_GEMM) return 0;
+    if (mode != ABY3G_MUL_GEMM || small_gemm(M, K, N)) return 0;
     return plan_gemm(M, K, N).total;
 }
 
@@ -419,6 +427,14 @@ int aby3g_mul_local(int mode, const int64_t* A, const int64_t* B, int64_t* C0, u
         if (!n) return;
         if (mode == ABY3G_MUL_HADAMARD) {
             SrcHadamard src{A, A + n, B, B + n};
+            if (zs)
+                launch_finish_zero_share(src, n, *zs, C0, S(stream));
+            else
+                launch_finish_plain(src, n, C0, S(stream));
+            return;
+        }
+        if (small_gemm(M, K, N)) {
+            SrcSmallGemm src{A, A + M * K, B, B + K * N, K, N};
             if (zs)
                 launch_finish_zero_share(src, n, *zs, C0, S(stream));
             else
@@ -456,6 +472,11 @@ int aby3g_mul_trunc_local(int mode, const int64_t* A, const int64_t* B, uint64_t
             launch_finish_trunc(src, *ts, n, d, nullptr, C, C + n, z, S(stream));
             return;
         }
+        if (small_gemm(M, K, N)) {
+            launch_finish_trunc(SrcSmallGemm{A, A + M * K, B, B + K * N, K, N}, *ts, n, d, nullptr, C, C + n, z,
+                                S(stream));
+            return;
+        }
         GemmPlan p = plan_gemm(M, K, N);
         check_ws(p, workspace, workspace_bytes);
         Workspace w = carve(p, workspace);
@@ -481,6 +502,11 @@ int aby3g_mul_sub_local(int mode, const int64_t* A, const int64_t* B, const int6
         if (mode == ABY3G_MUL_HADAMARD) {
             if (sub_ready) ABY3G_CHECK_HIP(hipStreamWaitEvent(S(stream), (hipEvent_t)sub_ready, 0));
             launch_finish_plain(SrcHadamardMinus{A, A + n, B, B + n, sub}, n, out, S(stream));
+            return;
+        }
+        if (small_gemm(M, K, N)) {
+            if (sub_ready) ABY3G_CHECK_HIP(hipStreamWaitEvent(S(stream), (hipEvent_t)sub_ready, 0));
+            launch_finish_plain(SrcSmallGemmMinus{{A, A + M * K, B, B + K * N, K, N}, sub}, n, out, S(stream));
             return;
         }
         GemmPlan p = plan_gemm(M, K, N);

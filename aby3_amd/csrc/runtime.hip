@@ -205,6 +205,13 @@ int aby3g_device_sync(void) {
 int aby3g_event_create(aby3g_event* ev) {
     return guarded([&] {
         hipEvent_t e;
+        ABY3G_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        *ev = e;
+    });
+}
+int aby3g_event_create_timed(aby3g_event* ev) {
+    return guarded([&] {
+        hipEvent_t e;
         ABY3G_CHECK_HIP(hipEventCreate(&e));
         *ev = e;
     });

@@ -25,6 +25,18 @@ void Sh3BinaryEvaluator::upload(Gpu& g) {
         d->gates.reset(g, gs.size() * sizeof(aby3g_gate));
         toDevice(d->gates.data(), gs.data(), gs.size() * sizeof(aby3g_gate), g);
     }
+    // per level: first gate and batch end offsets (relative) for aby3g_bin_level
+    std::vector<u32> ends;
+    for (const auto& batches : c.mLevelBatches) {
+        d->levelFirstGate.push_back(batches.empty() ? 0 : batches.front().begin);
+        d->levelBatchOffset.push_back((u32)ends.size());
+        d->levelBatches.push_back((u32)batches.size());
+        for (const auto& b : batches) ends.push_back(b.begin + b.count - d->levelFirstGate.back());
+    }
+    if (!ends.empty()) {
+        d->batchEnds.reset(g, ends.size() * 4);
+        toDevice(d->batchEnds.data(), ends.data(), ends.size() * 4, g);
+    }
     // per level, the AND outputs in level-list order = send/recv row order
     size_t gi = 0;
     d->hostOutWires.resize(c.mLevelCounts.size());
@@ -89,9 +101,8 @@ void Sh3BinaryEvaluator::setInput(u64 i, const sbMatrix& in) {
         if (wires[k] != wires[k - 1] + 1) throw std::runtime_error("expecting contiguous input wires. " LOCATION);
     Gpu& g = *mGpu;
     const u64 W = mCir->mWireCount;
-    for (int s = 0; s < 2; ++s)
-        GPU_CALL(aby3g_bits_to_wires(in.share(s), mRows, in.i64Cols(), (u32)wires.size(),
-                                     mMem.as<u64>() + ((u64)s * W + wires[0]) * mWords, mWords, g.stream()));
+    GPU_CALL(aby3g_bits_to_wires2(in.data(), mRows, in.i64Cols(), (u32)wires.size(), mMem.as<u64>() + wires[0] * mWords,
+                                  W * mWords, mWords, g.stream()));
     mLevel = 0;
 }
 
@@ -120,20 +131,27 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
     Gpu& g = task.getRuntime().gpu();
     const u64 W = mCir->mWireCount;
     const u64 rowBytes = mWords * 8;
+    // share 1 of last level's AND outputs arrived from prev (:555-573); they
+    // are unpacked by the same launch that runs this level's gates
+    u32 nUnpack = 0;
+    const u32* unpackWires = nullptr;
     if (mLevel) {
-        // share 1 of last level's AND outputs arrived from prev (:555-573)
-        const u32 nAnd = mCir->mLevelAndCounts[mLevel - 1];
-        if (nAnd) {
+        nUnpack = mCir->mLevelAndCounts[mLevel - 1];
+        if (nUnpack) {
             mRecvFutr.get();
-            GPU_CALL(aby3g_bin_unpack(mRecv.as<u64>(), mCur->outWires[mLevel - 1].as<u32>(), nAnd, mMem.as<u64>(), W,
-                                      mWords, g.stream()));
+            unpackWires = mCur->outWires[mLevel - 1].as<u32>();
         }
     }
-    if (mLevel < mCir->mLevelCounts.size()) {
-        DeviceBuffer& send = mSend[mLevel & 1];
-        for (const auto& b : mCir->mLevelBatches[mLevel])
-            GPU_CALL(aby3g_bin_gates(mCur->gates.as<aby3g_gate>() + b.begin, b.count, mMem.as<u64>(), W, mWords,
-                                     mZ.as<u64>(), send.as<u64>(), g.stream()));
+    const bool gatesHere = mLevel < mCir->mLevelCounts.size();
+    const u32 nb = gatesHere ? mCur->levelBatches[mLevel] : 0;
+    DeviceBuffer& send = mSend[mLevel & 1];
+    if (nb || nUnpack) {
+        const aby3g_gate* gl = nb ? mCur->gates.as<aby3g_gate>() + mCur->levelFirstGate[mLevel] : nullptr;
+        const u32* be = nb ? mCur->batchEnds.as<u32>() + mCur->levelBatchOffset[mLevel] : nullptr;
+        GPU_CALL(aby3g_bin_level(gl, be, nb, mRecv.as<u64>(), unpackWires, nUnpack, mMem.as<u64>(), W, mWords,
+                                 mZ.as<u64>(), send.as<u64>(), g.stream()));
+    }
+    if (gatesHere) {
         const u32 nAnd = mCir->mLevelAndCounts[mLevel];
         if (nAnd) {
             comm.mNext.asyncSendDevice(send.data(), nAnd * rowBytes, g);
@@ -175,9 +193,8 @@ void Sh3BinaryEvaluator::getOutput(u64 i, sbMatrix& out) {
     Gpu& g = *mGpu;
     const u64 W = mCir->mWireCount;
     const u32* dw = mCur->allOutputWires.as<u32>() + mCur->outputOffsets[i];
-    for (int s = 0; s < 2; ++s)
-        GPU_CALL(aby3g_wires_to_bits(mMem.as<u64>() + (u64)s * W * mWords, dw, (u32)wires.size(), mWords,
-                                     out.share(s), mRows, g.stream()));
+    GPU_CALL(aby3g_wires_to_bits2(mMem.as<u64>(), W * mWords, dw, (u32)wires.size(), mWords, out.data(), mRows,
+                                  g.stream()));
 }
 
 }  // namespace aby3

@@ -43,6 +43,8 @@ public:
 private:
     struct DevCircuit {
         DeviceBuffer gates;                 // aby3g_gate per batched gate
+        DeviceBuffer batchEnds;             // per level: batch end offsets, relative to the level's first gate
+        std::vector<u32> levelFirstGate, levelBatchOffset, levelBatches;
         std::vector<DeviceBuffer> outWires; // per level: AND output wires (unpack order)
         std::vector<std::vector<u32>> hostOutWires;
         DeviceBuffer allOutputWires;        // output bundles, concatenated

@@ -111,23 +111,29 @@ Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, const si64Matrix& A, const si64Matri
                                          g.stream()));
                 C.setZero();
             } else {
-                // round 1 (Sh3Evaluator.cpp:658-673): the truncation pair
-                // (AES-CTR of both streams) on the auxiliary stream, beside
-                // the share product on the main stream; z = product - r
+                // round 1 (Sh3Evaluator.cpp:658-673): z = product - r, C = RT
                 aby3g_trunc_streams ts;
                 std::memcpy(ts.next_seed, mShareGen.mNextSeed.data(), 16);
                 std::memcpy(ts.prev_seed, mShareGen.mPrevSeed.data(), 16);
                 ts.next_off = mShareGen.takeNext(8 * n);
                 ts.prev_off = mShareGen.takePrev(8 * n);
-                DeviceBuffer r(g, bytes);
-                g.forkAux();
-                GPU_CALL(aby3g_trunc_tuple(&ts, n, (unsigned)shift, r.as<i64>(), C.data(), g.aux()));
-                aby3g_event rReady = g.recordAux();
-                GPU_CALL(aby3g_mul_sub_local((int)mode, A.data(), B.data(), r.as<i64>(), rReady, z->as<i64>(), M, K,
-                                             N, ws, wsBytes, g.stream()));
-                // r and C's RT were written on aux; the main stream has waited for
-                // them (rReady) before the pass that reads r, so freeing r into
-                // the main stream's pool and later uses of C are ordered
+                if (aby3g_mul_prefers_fused((int)mode, M, K, N)) {
+                    // small or element-wise: product, truncation pair and z in one launch
+                    GPU_CALL(aby3g_mul_trunc_local((int)mode, A.data(), B.data(), M, K, N, (unsigned)shift, &ts,
+                                                   z->as<i64>(), C.data(), ws, wsBytes, g.stream()));
+                } else {
+                    // the truncation pair (AES-CTR of both streams) on the auxiliary
+                    // stream, beside the share GEMM on the main stream. r and C's RT
+                    // are written on aux; the main stream waits for them (rReady)
+                    // before the pass that reads r, so freeing r into the main
+                    // stream's pool and later uses of C are ordered.
+                    DeviceBuffer r(g, bytes);
+                    g.forkAux();
+                    GPU_CALL(aby3g_trunc_tuple(&ts, n, (unsigned)shift, r.as<i64>(), C.data(), g.aux()));
+                    aby3g_event rReady = g.recordAux();
+                    GPU_CALL(aby3g_mul_sub_local((int)mode, A.data(), B.data(), r.as<i64>(), rReady, z->as<i64>(), M,
+                                                 K, N, ws, wsBytes, g.stream()));
+                }
             }
             // reveal z to parties 0 and 1 (:681-684)
             const u64 p = self.getRuntime().mPartyIdx;

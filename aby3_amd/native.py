@@ -75,6 +75,7 @@ _SIGS = {
     "aby3g_stream_sync": (c_int, [c_void_p]),
     "aby3g_device_sync": (c_int, []),
     "aby3g_event_create": (c_int, [POINTER(c_void_p)]),
+    "aby3g_event_create_timed": (c_int, [POINTER(c_void_p)]),
     "aby3g_event_destroy": (c_int, [c_void_p]),
     "aby3g_event_record": (c_int, [c_void_p, c_void_p]),
     "aby3g_event_sync": (c_int, [c_void_p]),
@@ -91,6 +92,7 @@ _SIGS = {
     "aby3g_mul_local": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64, c_uint64,
                                 POINTER(ZeroShare), c_void_p, c_size_t, c_void_p]),
     "aby3g_trunc_tuple": (c_int, [POINTER(TruncStreams), c_uint64, ctypes.c_uint, c_void_p, c_void_p, c_void_p]),
+    "aby3g_mul_prefers_fused": (c_int, [c_int, c_uint64, c_uint64, c_uint64]),
     "aby3g_mul_sub_local": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64,
                                     c_uint64, c_void_p, c_size_t, c_void_p]),
     "aby3g_mul_trunc_local": (c_int, [c_int, c_void_p, c_void_p, c_uint64, c_uint64, c_uint64, ctypes.c_uint,
@@ -107,6 +109,12 @@ _SIGS = {
     "aby3g_pubmul_helper": (c_int, [c_void_p, c_uint64, POINTER(ZeroShare), c_u8p, c_uint64, c_void_p, c_void_p,
                                     c_void_p]),
     "aby3g_bin_gates": (c_int, [c_void_p, c_uint32, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p]),
+    "aby3g_bin_level": (c_int, [c_void_p, c_void_p, ctypes.c_uint32, c_void_p, c_void_p, ctypes.c_uint32, c_void_p,
+                                c_uint64, c_uint64, c_void_p, c_void_p, c_void_p]),
+    "aby3g_bits_to_wires2": (c_int, [c_void_p, c_uint64, c_uint64, ctypes.c_uint32, c_void_p, c_uint64, c_uint64,
+                                     c_void_p]),
+    "aby3g_wires_to_bits2": (c_int, [c_void_p, c_uint64, c_void_p, ctypes.c_uint32, c_uint64, c_void_p, c_uint64,
+                                     c_void_p]),
     "aby3g_bin_unpack": (c_int, [c_void_p, c_void_p, c_uint32, c_void_p, c_uint64, c_uint64, c_void_p]),
     "aby3g_bits_to_wires": (c_int, [c_void_p, c_uint64, c_uint64, c_uint32, c_void_p, c_uint64, c_void_p]),
     "aby3g_wires_to_bits": (c_int, [c_void_p, c_void_p, c_uint32, c_uint64, c_void_p, c_uint64, c_void_p]),

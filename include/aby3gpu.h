@@ -57,7 +57,8 @@ int aby3g_stream_create(aby3g_stream* stream);
 int aby3g_stream_destroy(aby3g_stream stream);
 int aby3g_stream_sync(aby3g_stream stream);
 int aby3g_device_sync(void);
-int aby3g_event_create(aby3g_event* ev);
+int aby3g_event_create(aby3g_event* ev);       /* ordering only (no timestamp: cheaper to record) */
+int aby3g_event_create_timed(aby3g_event* ev); /* for aby3g_event_elapsed_ms */
 int aby3g_event_destroy(aby3g_event ev);
 int aby3g_event_record(aby3g_event ev, aby3g_stream stream);
 int aby3g_event_sync(aby3g_event ev);
@@ -131,7 +132,15 @@ typedef struct {
     uint64_t prev_off;
 } aby3g_trunc_streams;
 
-/* Scratch needed by aby3g_mul_local / aby3g_mul_trunc_local (0 for Hadamard). */
+/* 1 when the whole round-1 local part runs best as one fused launch
+ * (aby3g_mul_trunc_local / aby3g_mul_local with zs): Hadamard, and GEMMs of
+ * up to 2^23 product terms, which run on the VALU instead of the int8-MFMA
+ * digit GEMM. 0 when the truncation pair should be overlapped on a second
+ * stream (aby3g_trunc_tuple + aby3g_mul_sub_local). */
+int aby3g_mul_prefers_fused(int mode, uint64_t M, uint64_t K, uint64_t N);
+
+/* Scratch needed by aby3g_mul_local / aby3g_mul_trunc_local (0 for Hadamard
+ * and small GEMMs). */
 size_t aby3g_mul_workspace_bytes(int mode, uint64_t M, uint64_t K, uint64_t N);
 
 /* asyncMul without truncation, local part (Sh3Evaluator.cpp:92-116):
@@ -229,6 +238,17 @@ typedef struct {
 int aby3g_bin_gates(const aby3g_gate* gates, uint32_t ngates, uint64_t* mem, uint64_t wires, uint64_t words,
                     const uint64_t* z, uint64_t* sendbuf, aby3g_stream stream);
 /* Level entry (:555-573): share-1 row of out_wires[j] <- recvbuf row j. */
+/* One whole communication level in one launch (roundCallback,
+ * Sh3BinaryEvaluator.cpp:539-1196): first the previous level's received AND
+ * shares are unpacked (share 1 of wire unpack_wires[j] = recvbuf row j),
+ * then the level's gates run in batch order -- batch b is gates
+ * [batch_ends[b-1], batch_ends[b]) (device array), the gates of one batch
+ * independent -- with AND-type outputs also written to sendbuf row
+ * send_row. Either part may be empty. Equivalent to aby3g_bin_unpack then
+ * one aby3g_bin_gates per batch. */
+int aby3g_bin_level(const aby3g_gate* gates, const uint32_t* batch_ends, uint32_t nbatches, const uint64_t* recvbuf,
+                    const uint32_t* unpack_wires, uint32_t nunpack, uint64_t* mem, uint64_t wires, uint64_t words,
+                    const uint64_t* z, uint64_t* sendbuf, aby3g_stream stream);
 int aby3g_bin_unpack(const uint64_t* recvbuf, const uint32_t* out_wires, uint32_t n, uint64_t* mem, uint64_t wires,
                      uint64_t words, aby3g_stream stream);
 /* setInput (:200-276): bit-transpose a [rows][cols64] i64 share matrix into
@@ -240,6 +260,13 @@ int aby3g_bits_to_wires(const int64_t* in, uint64_t rows, uint64_t cols64, uint3
  * wires, row base = mem_share) back to [rows][ceil(nbits/64)] i64. */
 int aby3g_wires_to_bits(const uint64_t* mem_share, const uint32_t* wires, uint32_t nbits, uint64_t words,
                         int64_t* out, uint64_t rows, aby3g_stream stream);
+/* Both shares in one launch: `in` / `out` are [2][rows][cols] share pairs
+ * (SharedMat layout); share s's wire rows start share_stride u64 after
+ * share 0's (= wires * words for the engine memory). */
+int aby3g_bits_to_wires2(const int64_t* in, uint64_t rows, uint64_t cols64, uint32_t nbits, uint64_t* wire_rows,
+                         uint64_t share_stride, uint64_t words, aby3g_stream stream);
+int aby3g_wires_to_bits2(const uint64_t* mem, uint64_t share_stride, const uint32_t* wires, uint32_t nbits,
+                         uint64_t words, int64_t* out, uint64_t rows, aby3g_stream stream);
 
 /* ------------------------------------------------ element-wise helpers -- */
 /* out[i] = ca*a[i] + cb*b[i] + c (mod 2^64); b may be NULL. Covers share

@@ -231,6 +231,29 @@ def test_transposes(gpu, rows, nbits):
     assert np.array_equal(host(out).reshape(rows, cols), x)
 
 
+@pytest.mark.parametrize("rows,nbits", [(1, 1), (3000, 70)])
+def test_transposes_both_shares(gpu, rows, nbits):
+    """bits_to_wires2 / wires_to_bits2 (both shares, engine memory layout)."""
+    import torch
+
+    cols = (nbits + 63) // 64
+    x = rnd(rows + 7, 2 * rows * cols).reshape(2, rows, cols)
+    if nbits % 64:
+        x[:, :, -1] &= np.int64((1 << (nbits % 64)) - 1)
+    words = 32 * ((rows + 2047) // 2048)
+    wires = nbits + 5  # the input lands at wire 3 of a 2 x wires x words memory
+    mem = empty(2 * wires * words)
+    gpu.bits_to_wires2(P(dev(x)), rows, cols, nbits, ctypes.c_void_p(mem.data_ptr() + 3 * words * 8), wires * words,
+                       words, None)
+    m = host(mem).view(np.uint64).reshape(2, wires, words)
+    for s in range(2):
+        assert np.array_equal(m[s, 3:3 + nbits], _bits_ref(x[s], nbits, words))
+    ids = torch.arange(3, 3 + nbits, dtype=torch.int32, device="cuda")
+    out = empty(2 * rows * cols)
+    gpu.wires_to_bits2(P(mem), wires * words, P(ids), nbits, words, P(out), rows, None)
+    assert np.array_equal(host(out).reshape(2, rows, cols), x)
+
+
 def _gate_ref(t, x0, x1, y0, y1, z):
     if t == 0:
         return x0 ^ y0, x1 ^ y1
@@ -289,6 +312,48 @@ def test_bin_gates_and_unpack(gpu):
     gpu.bin_unpack(P(dev(recv.view(np.int64))), P(outw), 4, P(memd), wires, words, None)
     out = host(memd).view(np.uint64).reshape(2, wires, words)
     assert np.array_equal(out[1, 22:26], recv.reshape(4, words))
+
+
+@pytest.mark.parametrize("words", [32, 4096])
+def test_bin_level_matches_unpack_then_batches(gpu, words):
+    """aby3g_bin_level == aby3g_bin_unpack + one aby3g_bin_gates per batch,
+    with a dependent chain across batches (XOR of an earlier AND output)."""
+    import torch
+
+    wires = 48
+    rng = np.random.default_rng(words)
+    mem = rng.integers(0, 2**64, size=2 * wires * words, dtype=np.uint64)
+    z = rng.integers(0, 2**64, size=4 * words, dtype=np.uint64)
+    recv = rng.integers(0, 2**64, size=3 * words, dtype=np.uint64)
+    unpack = [30, 31, 32]
+    # batch 0: independent gates reading unpacked wires; batch 1 consumes batch 0
+    batches = [[(30, 1, 20, 2), (31, 3, 21, 0), (32, 5, 22, 5), (6, 7, 23, 7), (8, 9, 24, 3)],
+               [(20, 21, 25, 0), (22, 23, 26, 4), (24, 0, 27, 6)],
+               [(25, 26, 28, 1)]]
+    flat = [g for b in batches for g in b]
+    arr = (nt.Gate * len(flat))()
+    zrow = 0
+    for i, (a, b, o, t) in enumerate(flat):
+        arr[i].in0, arr[i].in1, arr[i].out, arr[i].type = a, b, o, t
+        if t in (2, 3, 4, 5):
+            arr[i].z_row = arr[i].send_row = zrow
+            zrow += 1
+    gdev = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to("cuda")
+    ends = torch.tensor(np.cumsum([len(b) for b in batches]).tolist(), dtype=torch.int32, device="cuda")
+    uw = torch.tensor(unpack, dtype=torch.int32, device="cuda")
+    zd, rd = dev(z.view(np.int64)), dev(recv.view(np.int64))
+    # reference: the separate kernels
+    m1, s1 = dev(mem.view(np.int64)), empty(4 * words)
+    gpu.bin_unpack(P(rd), P(uw), 3, P(m1), wires, words, None)
+    gsz = ctypes.sizeof(nt.Gate)
+    first = 0
+    for b in batches:
+        gpu.bin_gates(ctypes.c_void_p(gdev.data_ptr() + gsz * first), len(b), P(m1), wires, words, P(zd), P(s1), None)
+        first += len(b)
+    m2, s2 = dev(mem.view(np.int64)), empty(4 * words)
+    gpu.bin_level(P(gdev), P(ends), len(batches), P(rd), P(uw), 3, P(m2), wires, words, P(zd), P(s2), None)
+    assert np.array_equal(host(m1), host(m2))
+    assert np.array_equal(host(s1)[:zrow * words], host(s2)[:zrow * words])
 
 
 def test_lincomb_bitops(gpu):

@@ -205,6 +205,88 @@ __global__ void __launch_bounds__(256) k_wires_to_bits(const u64* __restrict__ m
     if (row < rows) out[row * cols + c] = (i64)mine;
 }
 
+// LDS-tiled transposes (the both-share entry points): a workgroup owns 64
+// consecutive words (4096 rows) of one 64-bit column. bits -> wires: each
+// wave bit-transposes 16 words by ballots into an LDS tile [bit][word], then
+// the tile leaves as 64 contiguous 512-byte wire segments. wires -> bits:
+// the reverse, reading 512-byte wire segments into the tile.
+constexpr u32 kTileWords = 64;
+constexpr u32 kTilePitch = kTileWords + 1;  // u64 per tile row (+1: bank spread)
+
+__global__ void __launch_bounds__(256) k_bits_to_wires_tiled(const i64* __restrict__ in, u64 rows, u64 cols64,
+                                                             u32 nbits, u64* __restrict__ wrows, u64 shareStride,
+                                                             u64 words) {
+    __shared__ u64 tile[64 * kTilePitch];
+    in += (u64)blockIdx.y * rows * cols64;
+    wrows += (u64)blockIdx.y * shareStride;
+    const u64 tilesPerCol = (words + kTileWords - 1) / kTileWords;
+    const u64 c = blockIdx.x / tilesPerCol, w0 = (blockIdx.x % tilesPerCol) * kTileWords;
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // all 16 loads of this wave in flight before the first ballot
+    u64 vv[16];
+#pragma unroll
+    for (u32 k = 0; k < 16; ++k) {
+        const u32 wl = wave * 16 + k;
+        const u64 r = (w0 + wl) * 64 + lane;
+        vv[k] = (w0 + wl < words && r < rows) ? (u64)in[r * cols64 + c] : 0;
+    }
+    for (u32 k = 0; k < 16; ++k) {
+        const u32 wl = wave * 16 + k;
+        const u64 v = vv[k];
+        u64 mine = 0;
+#pragma unroll 8
+        for (u32 b = 0; b < 64; ++b) {
+            const u64 m = __ballot((v >> b) & 1);
+            if (lane == b) mine = m;
+        }
+        tile[lane * kTilePitch + wl] = mine;
+    }
+    __syncthreads();
+    for (u32 idx = threadIdx.x; idx < 64 * kTileWords; idx += 256) {
+        const u32 b = idx / kTileWords, wl = idx % kTileWords;
+        const u64 bit = c * 64 + b;
+        if (bit < nbits && w0 + wl < words) wrows[bit * words + w0 + wl] = tile[b * kTilePitch + wl];
+    }
+}
+
+__global__ void __launch_bounds__(256) k_wires_to_bits_tiled(const u64* __restrict__ mem, u64 shareStride,
+                                                             const u32* __restrict__ wires, u32 nbits, u64 words,
+                                                             i64* __restrict__ out, u64 rows) {
+    __shared__ u64 tile[64 * kTilePitch];
+    const u64 cols = (nbits + 63) / 64;
+    mem += (u64)blockIdx.y * shareStride;
+    out += (u64)blockIdx.y * rows * cols;
+    const u64 rw = (rows + 63) / 64;  // words holding real rows
+    const u64 tilesPerCol = (rw + kTileWords - 1) / kTileWords;
+    const u64 c = blockIdx.x / tilesPerCol, w0 = (blockIdx.x % tilesPerCol) * kTileWords;
+    u64 vv[16];
+#pragma unroll
+    for (u32 j = 0; j < 16; ++j) {
+        const u32 idx = threadIdx.x + 256 * j, b = idx / kTileWords, wl = idx % kTileWords;
+        const u64 bit = c * 64 + b;
+        vv[j] = (bit < nbits && w0 + wl < rw) ? mem[(u64)wires[bit] * words + w0 + wl] : 0;
+    }
+#pragma unroll
+    for (u32 j = 0; j < 16; ++j) {
+        const u32 idx = threadIdx.x + 256 * j;
+        tile[(idx / kTileWords) * kTilePitch + idx % kTileWords] = vv[j];
+    }
+    __syncthreads();
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (u32 k = 0; k < 16; ++k) {
+        const u32 wl = wave * 16 + k;
+        const u64 v = tile[lane * kTilePitch + wl];
+        u64 mine = 0;
+#pragma unroll 8
+        for (u32 r = 0; r < 64; ++r) {
+            const u64 m = __ballot((v >> r) & 1);
+            if (lane == r) mine = m;
+        }
+        const u64 row = (w0 + wl) * 64 + lane;
+        if (w0 + wl < rw && row < rows) out[row * cols + c] = (i64)mine;
+    }
+}
+
 }  // namespace
 
 }  // namespace aby3g
@@ -271,7 +353,14 @@ int aby3g_bits_to_wires(const int64_t* in, uint64_t rows, uint64_t cols64, uint3
 
 int aby3g_bits_to_wires2(const int64_t* in, uint64_t rows, uint64_t cols64, uint32_t nbits, uint64_t* wire_rows,
                          uint64_t share_stride, uint64_t words, aby3g_stream stream) {
-    return guarded([&] { bits_to_wires(in, rows, cols64, nbits, wire_rows, share_stride, 2, words, S(stream)); });
+    return guarded([&] {
+        ABY3G_REQUIRE(nbits <= cols64 * 64, "nbits exceeds input columns");
+        ABY3G_REQUIRE(words * 64 >= rows, "words too small for rows");
+        if (!nbits || !words) return;
+        const u64 tiles = ((words + kTileWords - 1) / kTileWords) * ((nbits + 63) / 64);
+        launch(PROBE_OTHER, k_bits_to_wires_tiled, dim3((u32)tiles, 2), dim3(256), 0, S(stream), in, rows, cols64,
+               nbits, wire_rows, share_stride, words);
+    });
 }
 
 int aby3g_wires_to_bits(const uint64_t* mem_share, const uint32_t* wires, uint32_t nbits, uint64_t words, int64_t* out,
@@ -281,7 +370,13 @@ int aby3g_wires_to_bits(const uint64_t* mem_share, const uint32_t* wires, uint32
 
 int aby3g_wires_to_bits2(const uint64_t* mem, uint64_t share_stride, const uint32_t* wires, uint32_t nbits,
                          uint64_t words, int64_t* out, uint64_t rows, aby3g_stream stream) {
-    return guarded([&] { wires_to_bits(mem, share_stride, 2, wires, nbits, words, out, rows, S(stream)); });
+    return guarded([&] {
+        ABY3G_REQUIRE(words * 64 >= rows, "words too small for rows");
+        if (!nbits || !rows) return;
+        const u64 tiles = (((rows + 63) / 64 + kTileWords - 1) / kTileWords) * ((nbits + 63) / 64);
+        launch(PROBE_OTHER, k_wires_to_bits_tiled, dim3((u32)tiles, 2), dim3(256), 0, S(stream), mem, share_stride,
+               wires, nbits, words, out, rows);
+    });
 }
 
 }  // extern "C"

@@ -47,14 +47,14 @@ int guarded(F&& f) {
 
 // ----------------------------------------------------------------- probe --
 enum ProbeFamily { PROBE_GEMM = 0, PROBE_EPILOGUE = 1, PROBE_BINARY = 2, PROBE_AES = 3, PROBE_OTHER = 4, PROBE_DIGITS = 5 };
-void probe_begin(hipStream_t s);
+void probe_begin(int family, hipStream_t s);
 void probe_end(int family, hipStream_t s);
 
 // Launch helper: checks the launch and feeds the probe.
 template <class K, class... Args>
 void launch(int family, K kernel, dim3 grid, dim3 block, size_t lds, hipStream_t s, Args... args) {
     if (grid.x == 0 || grid.y == 0 || grid.z == 0) return;
-    probe_begin(s);
+    probe_begin(family, s);
     hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
     ABY3G_CHECK_HIP(hipGetLastError());
     probe_end(family, s);

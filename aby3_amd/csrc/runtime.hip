@@ -16,6 +16,7 @@ struct ProbeRec {
 };
 struct Probe {
     bool on = false;
+    u32 mask = 0;  // families bracketed
     hipEvent_t pending = nullptr;
     std::vector<ProbeRec> recs;
     double ms[8] = {0};
@@ -92,8 +93,8 @@ std::map<int, u32*> g_tab_dev;
 
 void set_error(const std::string& msg) { t_err = msg; }
 
-void probe_begin(hipStream_t s) {
-    if (!t_probe.on) return;
+void probe_begin(int family, hipStream_t s) {
+    if (!t_probe.on || !((t_probe.mask >> family) & 1)) return;
     t_probe.pending = t_probe.get();
     ABY3G_CHECK_HIP(hipEventRecord(t_probe.pending, s));
 }
@@ -251,6 +252,14 @@ int aby3g_probe_enable(int on) {
     return guarded([&] {
         if (!on) t_probe.drain();
         t_probe.on = on != 0;
+        t_probe.mask = on ? 0xffu : 0u;
+    });
+}
+int aby3g_probe_enable_mask(uint32_t mask) {
+    return guarded([&] {
+        if (!mask) t_probe.drain();
+        t_probe.on = mask != 0;
+        t_probe.mask = mask;
     });
 }
 int aby3g_probe_read(int family, double* ms, uint64_t* launches) {

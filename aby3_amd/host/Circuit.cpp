@@ -1,7 +1,13 @@
 #include "Circuit.h"
+#include <atomic>
 #include <algorithm>
 
 namespace aby3 {
+
+namespace {
+std::atomic<u64> g_circuitSerial{1};
+}
+BetaCircuit::BetaCircuit() : mSerial(g_circuitSerial++) {}
 
 BetaBundle BetaCircuit::addInputBundle(u32 bits) {
     BetaBundle b(bits);
@@ -79,6 +85,7 @@ void BetaCircuit::levelByAndDepth() {
         }
     }
     mAndCount = andOrdinal;
+    mSerial = g_circuitSerial++;  // a new levelized form: device caches must not reuse the old one
 }
 
 std::vector<std::vector<u64>> BetaCircuit::evalPlain(const std::vector<std::vector<u64>>& inputs) const {

@@ -32,6 +32,10 @@ using BetaBundle = std::vector<u32>;  // wire ids, LSB first
 
 class BetaCircuit {
 public:
+    BetaCircuit();
+    // process-unique id of this circuit's levelized form (device caches key on it,
+    // never on the address, which a later circuit may reuse)
+    u64 serial() const { return mSerial; }
     u32 mWireCount = 0;
     std::vector<BetaGate> mGates;           // construction order (topological)
     std::vector<BetaBundle> mInputs, mOutputs;
@@ -60,6 +64,9 @@ public:
 
     // plaintext evaluation on 64-bit words (tests; row r of a word = bit r)
     std::vector<std::vector<u64>> evalPlain(const std::vector<std::vector<u64>>& inputs) const;
+
+private:
+    u64 mSerial;
 };
 
 // The circuit library of the hot path. Circuits are cached per shape.

@@ -38,6 +38,7 @@ Gpu::~Gpu() {
     aby3g_set_device(mDevice);
     aby3g_stream_sync(mStream);
     if (mAux) aby3g_stream_sync(mAux);
+    mAttach.clear();
     trim();
     {
         // buffers still alive elsewhere now free straight to the driver
@@ -135,6 +136,15 @@ void Gpu::trim() {
     for (auto& kv : mPool->free) aby3g_free(kv.second.ptr);
     mPool->free.clear();
     mPool->cached = 0;
+}
+
+std::shared_ptr<void> Gpu::attachment(u64 key, const std::function<std::shared_ptr<void>()>& make) {
+    std::lock_guard<std::mutex> lk(mAttachMu);
+    auto it = mAttach.find(key);
+    if (it != mAttach.end()) return it->second;
+    auto v = make();
+    mAttach.emplace(key, v);
+    return v;
 }
 
 Gpu& Gpu::current() {

@@ -4,6 +4,7 @@
 #pragma once
 #include "Defines.h"
 #include <aby3gpu.h>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -74,6 +75,10 @@ public:
     size_t cachedBytes() const { return mPool->cached; }
     void trim();  // return cached blocks to the driver
 
+    // Per-Gpu cache of derived device data (uploaded circuits, tables): the
+    // object made by `make` on the first call with `key`, released with the Gpu.
+    std::shared_ptr<void> attachment(u64 key, const std::function<std::shared_ptr<void>()>& make);
+
     // thread-local current Gpu (set by bind(), e.g. by Sh3Runtime::init)
     static Gpu& current();
     static bool hasCurrent();
@@ -84,6 +89,8 @@ private:
     aby3g_stream mAux = nullptr;
     std::unique_ptr<Event> mForkEv, mAuxEv;
     std::shared_ptr<Pool> mPool;
+    std::mutex mAttachMu;
+    std::map<u64, std::shared_ptr<void>> mAttach;
 };
 
 // Owning device allocation from a party's pool (move-only). A buffer handed

@@ -341,7 +341,7 @@ struct Session {
     bool checkOk = true;
     std::vector<CommPkg> comms;
 
-    void worker(int i, int device, bool probe) {
+    void worker(int i, int device, int probe) {
         PartyCtx p;
         u64 seen = 0;
         try {
@@ -349,7 +349,7 @@ struct Session {
             p.rt.init(i, comms[i], device);
             p.enc.init(i, toBlock(0, i), toBlock(0, (i + 1) % 3));
             p.eval.init(i, toBlock(1, i), toBlock(1, (i + 1) % 3));
-            if (probe) GPU_CALL(aby3g_probe_enable(1));
+            if (probe) GPU_CALL(aby3g_probe_enable_mask((u32)probe));
             job->setup(p);
             p.rt.gpu().sync();
         } catch (const std::exception& e) {
@@ -452,7 +452,7 @@ aby3h_session* aby3h_session_create(int job, const uint64_t* params, int nparams
             s.finished = 0;
         }
         for (int i = 0; i < 3; ++i) s.th[i] = std::thread([&s, i, devices, probe] {
-            s.worker(i, devices ? devices[i] : 0, probe != 0);
+            s.worker(i, devices ? devices[i] : 0, probe);
         });
         {
             std::unique_lock<std::mutex> lk(s.mu);

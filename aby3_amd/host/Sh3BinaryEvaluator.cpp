@@ -1,4 +1,5 @@
 #include "Sh3BinaryEvaluator.h"
+#include <cstring>
 
 namespace aby3 {
 
@@ -9,58 +10,56 @@ void Sh3BinaryEvaluator::setCir(BetaCircuit* cir, u64 width, Sh3ShareGen& gen) {
 }
 
 void Sh3BinaryEvaluator::upload(Gpu& g) {
-    auto it = mDev.find(mCir);
-    if (it != mDev.end() && it->second->gates.gpu() == &g) {
-        mCur = it->second.get();
-        return;
-    }
-    auto d = std::make_unique<DevCircuit>();
     const BetaCircuit& c = *mCir;
-    std::vector<aby3g_gate> gs(c.mBatchGates.size());
-    for (size_t i = 0; i < gs.size(); ++i) {
-        const BetaGate& b = c.mBatchGates[i];
-        gs[i] = aby3g_gate{b.in0, b.in1, b.out, (u32)b.type, c.mBatchZRow[i], c.mBatchSendRow[i]};
-    }
-    if (!gs.empty()) {
-        d->gates.reset(g, gs.size() * sizeof(aby3g_gate));
-        toDevice(d->gates.data(), gs.data(), gs.size() * sizeof(aby3g_gate), g);
-    }
-    // per level: first gate and batch end offsets (relative) for aby3g_bin_level
-    std::vector<u32> ends;
-    for (const auto& batches : c.mLevelBatches) {
-        d->levelFirstGate.push_back(batches.empty() ? 0 : batches.front().begin);
-        d->levelBatchOffset.push_back((u32)ends.size());
-        d->levelBatches.push_back((u32)batches.size());
-        for (const auto& b : batches) ends.push_back(b.begin + b.count - d->levelFirstGate.back());
-    }
-    if (!ends.empty()) {
-        d->batchEnds.reset(g, ends.size() * 4);
-        toDevice(d->batchEnds.data(), ends.data(), ends.size() * 4, g);
-    }
-    // per level, the AND outputs in level-list order = send/recv row order
-    size_t gi = 0;
-    d->hostOutWires.resize(c.mLevelCounts.size());
-    d->outWires.resize(c.mLevelCounts.size());
-    for (size_t L = 0; L < c.mLevelCounts.size(); ++L) {
-        for (u32 k = 0; k < c.mLevelCounts[L]; ++k, ++gi)
-            if (isAndType(c.mLevelGates[gi].type)) d->hostOutWires[L].push_back(c.mLevelGates[gi].out);
-        auto& v = d->hostOutWires[L];
-        if (!v.empty()) {
-            d->outWires[L].reset(g, v.size() * 4);
-            toDevice(d->outWires[L].data(), v.data(), v.size() * 4, g);
+    // key: circuit serial (unique per levelized form), tagged to stay clear of other attachment kinds
+    const u64 key = (c.serial() << 8) | 0x01;
+    mCur = std::static_pointer_cast<DevCircuit>(g.attachment(key, [&]() -> std::shared_ptr<void> {
+        auto d = std::make_shared<DevCircuit>();
+        std::vector<u8> host;
+        auto put = [&](const void* p, size_t bytes) {
+            const size_t off = (host.size() + 15) / 16 * 16;
+            host.resize(off + bytes);
+            if (bytes) std::memcpy(host.data() + off, p, bytes);
+            return off;
+        };
+        std::vector<aby3g_gate> gs(c.mBatchGates.size());
+        for (size_t i = 0; i < gs.size(); ++i) {
+            const BetaGate& b = c.mBatchGates[i];
+            gs[i] = aby3g_gate{b.in0, b.in1, b.out, (u32)b.type, c.mBatchZRow[i], c.mBatchSendRow[i]};
         }
-    }
-    std::vector<u32> all;
-    for (auto& o : c.mOutputs) {
-        d->outputOffsets.push_back((u32)all.size());
-        all.insert(all.end(), o.begin(), o.end());
-    }
-    if (!all.empty()) {
-        d->allOutputWires.reset(g, all.size() * 4);
-        toDevice(d->allOutputWires.data(), all.data(), all.size() * 4, g);
-    }
-    mCur = d.get();
-    mDev[mCir] = std::move(d);
+        const size_t oGates = put(gs.data(), gs.size() * sizeof(aby3g_gate));
+        std::vector<u32> ends;
+        for (const auto& batches : c.mLevelBatches) {
+            d->levelFirstGate.push_back(batches.empty() ? 0 : batches.front().begin);
+            d->levelBatchOffset.push_back((u32)ends.size());
+            d->levelBatches.push_back((u32)batches.size());
+            for (const auto& b : batches) ends.push_back(b.begin + b.count - d->levelFirstGate.back());
+        }
+        const size_t oEnds = put(ends.data(), ends.size() * 4);
+        // per level, the AND outputs in level-list order = send/recv row order
+        std::vector<size_t> oLevel;
+        size_t gi = 0;
+        for (size_t L = 0; L < c.mLevelCounts.size(); ++L) {
+            std::vector<u32> v;
+            for (u32 k = 0; k < c.mLevelCounts[L]; ++k, ++gi)
+                if (isAndType(c.mLevelGates[gi].type)) v.push_back(c.mLevelGates[gi].out);
+            oLevel.push_back(put(v.data(), v.size() * 4));
+        }
+        std::vector<u32> all;
+        for (auto& o : c.mOutputs) {
+            d->outputOffsets.push_back((u32)all.size());
+            all.insert(all.end(), o.begin(), o.end());
+        }
+        const size_t oOut = put(all.data(), all.size() * 4);
+        d->blob.reset(g, host.size() ? host.size() : 16);
+        if (!host.empty()) toDevice(d->blob.data(), host.data(), host.size(), g);
+        u8* base = d->blob.as<u8>();
+        d->gates = reinterpret_cast<const aby3g_gate*>(base + oGates);
+        d->batchEnds = reinterpret_cast<const u32*>(base + oEnds);
+        for (size_t o : oLevel) d->outWires.push_back(reinterpret_cast<const u32*>(base + o));
+        d->allOutputWires = reinterpret_cast<const u32*>(base + oOut);
+        return d;
+    }));
 }
 
 void Sh3BinaryEvaluator::setCir(BetaCircuit* cir, u64 width, block prevSeed, block nextSeed) {
@@ -76,19 +75,16 @@ void Sh3BinaryEvaluator::setCir(BetaCircuit* cir, u64 width, block prevSeed, blo
     upload(g);
     const u64 memBytes = 2 * (u64)cir->mWireCount * mWords * 8;
     if (mMem.bytes() < memBytes || mMem.gpu() != &g) mMem.reset(g, memBytes ? memBytes : 8);
-    // all AND masks of the circuit: z[k][w] = binary draw k*words + w
+    // all AND masks of the circuit: z[k][w] = binary draw k*words + w, drawn on
+    // the auxiliary stream while the inputs are transposed on the main one
     const u64 zWords = (u64)cir->mAndCount * mWords;
     if (zWords) {
         if (mZ.bytes() < zWords * 8 || mZ.gpu() != &g) mZ.reset(g, zWords * 8);
+        g.forkAux();
         GPU_CALL(aby3g_share_draws(ABY3G_DRAW_BIN, mKeyPrev.data(), mKeyNext.data(), 0, zWords, nullptr,
-                                   mZ.as<i64>(), nullptr, g.stream()));
+                                   mZ.as<i64>(), nullptr, g.aux()));
+        mZPending = true;
     }
-    u32 maxAnds = 0;
-    for (u32 a : cir->mLevelAndCounts) maxAnds = std::max(maxAnds, a);
-    const u64 sb = (u64)maxAnds * mWords * 8;
-    for (auto& s : mSend)
-        if (s.bytes() < sb || s.gpu() != &g) s.reset(g, sb ? sb : 8);
-    if (mRecv.bytes() < sb || mRecv.gpu() != &g) mRecv.reset(g, sb ? sb : 8);
 }
 
 void Sh3BinaryEvaluator::setInput(u64 i, const sbMatrix& in) {
@@ -132,31 +128,34 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
     const u64 W = mCir->mWireCount;
     const u64 rowBytes = mWords * 8;
     // share 1 of last level's AND outputs arrived from prev (:555-573); they
-    // are unpacked by the same launch that runs this level's gates
+    // are unpacked, straight from the sender's buffer, by the same launch that
+    // runs this level's gates
     u32 nUnpack = 0;
-    const u32* unpackWires = nullptr;
+    std::shared_ptr<DeviceBuffer> recv;
     if (mLevel) {
         nUnpack = mCir->mLevelAndCounts[mLevel - 1];
-        if (nUnpack) {
-            mRecvFutr.get();
-            unpackWires = mCur->outWires[mLevel - 1].as<u32>();
-        }
+        if (nUnpack) recv = mRecvFutr.getShared();
     }
     const bool gatesHere = mLevel < mCir->mLevelCounts.size();
     const u32 nb = gatesHere ? mCur->levelBatches[mLevel] : 0;
-    DeviceBuffer& send = mSend[mLevel & 1];
-    if (nb || nUnpack) {
-        const aby3g_gate* gl = nb ? mCur->gates.as<aby3g_gate>() + mCur->levelFirstGate[mLevel] : nullptr;
-        const u32* be = nb ? mCur->batchEnds.as<u32>() + mCur->levelBatchOffset[mLevel] : nullptr;
-        GPU_CALL(aby3g_bin_level(gl, be, nb, mRecv.as<u64>(), unpackWires, nUnpack, mMem.as<u64>(), W, mWords,
-                                 mZ.as<u64>(), send.as<u64>(), g.stream()));
+    const u32 nAnd = gatesHere ? mCir->mLevelAndCounts[mLevel] : 0;
+    std::shared_ptr<DeviceBuffer> send;
+    if (nAnd) send = std::make_shared<DeviceBuffer>(g, nAnd * rowBytes);
+    if (nb && mZPending) {
+        g.joinAux();
+        mZPending = false;
     }
-    if (gatesHere) {
-        const u32 nAnd = mCir->mLevelAndCounts[mLevel];
-        if (nAnd) {
-            comm.mNext.asyncSendDevice(send.data(), nAnd * rowBytes, g);
-            mRecvFutr = comm.mPrev.asyncRecvDevice(mRecv.data(), nAnd * rowBytes, g);
-        }
+    if (nb || nUnpack) {
+        const aby3g_gate* gl = nb ? mCur->gates + mCur->levelFirstGate[mLevel] : nullptr;
+        const u32* be = nb ? mCur->batchEnds + mCur->levelBatchOffset[mLevel] : nullptr;
+        GPU_CALL(aby3g_bin_level(gl, be, nb, recv ? recv->as<u64>() : nullptr, nUnpack ? mCur->outWires[mLevel - 1] : nullptr,
+                                 nUnpack, mMem.as<u64>(), W, mWords, mZ.as<u64>(), send ? send->as<u64>() : nullptr,
+                                 g.stream()));
+    }
+    if (recv) recv->fence(g.stream());
+    if (nAnd) {
+        comm.mNext.asyncSendShared(send, nAnd * rowBytes, g);
+        mRecvFutr = comm.mPrev.asyncRecvShared(nAnd * rowBytes, g);
     }
     ++mLevel;
     if (hasMoreRounds()) task.then([this](CommPkg& c, Sh3Task& t) { roundCallback(c, t); }, "callback");
@@ -192,7 +191,7 @@ void Sh3BinaryEvaluator::getOutput(u64 i, sbMatrix& out) {
     out.resize(mRows, wires.size());
     Gpu& g = *mGpu;
     const u64 W = mCir->mWireCount;
-    const u32* dw = mCur->allOutputWires.as<u32>() + mCur->outputOffsets[i];
+    const u32* dw = mCur->allOutputWires + mCur->outputOffsets[i];
     GPU_CALL(aby3g_wires_to_bits2(mMem.as<u64>(), W * mWords, dw, (u32)wires.size(), mWords, out.data(), mRows,
                                   g.stream()));
 }

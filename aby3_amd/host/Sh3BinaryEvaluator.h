@@ -19,6 +19,16 @@ namespace aby3 {
 
 class Sh3BinaryEvaluator {
 public:
+    Sh3BinaryEvaluator() = default;
+    Sh3BinaryEvaluator(const Sh3BinaryEvaluator&) = delete;
+    Sh3BinaryEvaluator& operator=(const Sh3BinaryEvaluator&) = delete;
+    ~Sh3BinaryEvaluator() {
+        // mZ returns to the main stream's pool behind its draw
+        if (mZPending && mGpu) try {
+                mGpu->joinAux();
+            } catch (...) {
+            }
+    }
     // consumes 16 bytes of the prev and next streams for the AND keys
     // (Sh3BinaryEvaluator.h:96-102)
     void setCir(BetaCircuit* cir, u64 width, Sh3ShareGen& gen);
@@ -37,21 +47,25 @@ public:
     BetaCircuit* mCir = nullptr;
     u64 mRows = 0, mWords = 0, mLevel = 0;
     block mKeyPrev, mKeyNext;
-    DeviceBuffer mMem, mZ, mSend[2], mRecv;
-    RecvFuture mRecvFutr;
+    DeviceBuffer mMem, mZ;
+    RecvFuture mRecvFutr;   // previous level's AND shares (zero-copy: the sender's buffer)
+    bool mZPending = false;  // z masks still being drawn on the auxiliary stream
 
 private:
+    // The levelized circuit in device memory, one packed buffer uploaded once
+    // per (circuit, Gpu): gates | batch ends | per-level AND output wires |
+    // output-bundle wires. Cached on the Gpu (Gpu::attachment), so every
+    // evaluator instance -- aby3-Basic makes one per call -- reuses it.
     struct DevCircuit {
-        DeviceBuffer gates;                 // aby3g_gate per batched gate
-        DeviceBuffer batchEnds;             // per level: batch end offsets, relative to the level's first gate
+        DeviceBuffer blob;
+        const aby3g_gate* gates = nullptr;
+        const u32* batchEnds = nullptr;        // relative to the level's first gate
         std::vector<u32> levelFirstGate, levelBatchOffset, levelBatches;
-        std::vector<DeviceBuffer> outWires; // per level: AND output wires (unpack order)
-        std::vector<std::vector<u32>> hostOutWires;
-        DeviceBuffer allOutputWires;        // output bundles, concatenated
+        std::vector<const u32*> outWires;      // per level
+        const u32* allOutputWires = nullptr;
         std::vector<u32> outputOffsets;
     };
-    std::map<const BetaCircuit*, std::unique_ptr<DevCircuit>> mDev;
-    DevCircuit* mCur = nullptr;
+    std::shared_ptr<DevCircuit> mCur;
     Gpu* mGpu = nullptr;
     void upload(Gpu& g);
 };

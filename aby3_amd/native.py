@@ -82,6 +82,7 @@ _SIGS = {
     "aby3g_stream_wait_event": (c_int, [c_void_p, c_void_p]),
     "aby3g_event_elapsed_ms": (c_int, [c_void_p, c_void_p, POINTER(c_float)]),
     "aby3g_probe_enable": (c_int, [c_int]),
+    "aby3g_probe_enable_mask": (c_int, [ctypes.c_uint32]),
     "aby3g_probe_read": (c_int, [c_int, POINTER(c_double), POINTER(c_uint64)]),
     "aby3g_probe_reset": (c_int, []),
     "aby3g_aes_block_host": (c_int, [c_u8p, c_uint64, c_u8p]),
@@ -206,11 +207,14 @@ def host():
 class Session:
     """Three in-process parties running one job of the hot path (include/aby3.h)."""
 
-    def __init__(self, job: int, params, devices=(0, 0, 0), probe: bool = True):
+    def __init__(self, job: int, params, devices=(0, 0, 0), probe=True):
+        """probe: False / True (all kernel families) or a family bitmask
+        (1 << PROBE_GEMM, ...): only those launches are bracketed by events."""
         h = host()
         p = (c_uint64 * len(params))(*params)
         dv = (c_int * 3)(*devices)
-        self._h = h.aby3h_session_create(job, p, len(params), dv, int(probe))
+        mask = 0xFF if probe is True else int(probe)
+        self._h = h.aby3h_session_create(job, p, len(params), dv, mask)
         if not self._h:
             raise NativeError("aby3h_session_create: " + h.aby3h_last_error().decode())
         self.host = h

@@ -55,6 +55,8 @@ enum {
 
 const char* aby3h_last_error(void);
 
+/* probe: 0 off, else a bitmask of aby3gpu.h probe families (1 << family) whose
+ * launches are bracketed by timing events */
 aby3h_session* aby3h_session_create(int job, const uint64_t* params, int nparams, const int* devices, int probe);
 int aby3h_session_run(aby3h_session* s, uint64_t steps);
 /* kernel time (ms) and launches of a probe family (aby3gpu.h), summed over parties */

@@ -71,7 +71,8 @@ int aby3g_event_elapsed_ms(aby3g_event start, aby3g_event end, float* ms);
  * 0 share GEMM (MFMA), 1 mul epilogue / hadamard,
  * 2 binary gate layers, 3 AES streams, 4 other, 5 GEMM digit planes.
  * Used by bench.py. */
-int aby3g_probe_enable(int on);
+int aby3g_probe_enable(int on);             /* all families (on != 0) or none */
+int aby3g_probe_enable_mask(uint32_t mask); /* only the families in mask (bit = 1 << family) */
 int aby3g_probe_read(int family, double* ms, uint64_t* launches);
 int aby3g_probe_reset(void);
 

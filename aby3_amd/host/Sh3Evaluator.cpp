@@ -171,60 +171,54 @@ Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, const si64Matrix& A, const sbMatrix&
             C.resize(n, 1);
             switch (self.getRuntime().mPartyIdx) {
                 case 0: {  // OT sender for P1 (with P2 helping), helper for P2's send (:132-163)
-                    DeviceBuffer send(g, 2 * b8), help(g, b8);
+                    // the OT messages go zero-copy: P1 reads these buffers in place
+                    auto send = std::make_shared<DeviceBuffer>(g, 2 * b8);
+                    auto help = std::make_shared<DeviceBuffer>(g, b8);
                     aby3g_stream_pos pv, nx;
                     std::memcpy(pv.seed, mShareGen.mPrevSeed.data(), 16);
                     pv.off = mShareGen.takePrev(16 * n);
                     std::memcpy(nx.seed, mShareGen.mNextSeed.data(), 16);
                     nx.off = mShareGen.takeNext(8 * n);
                     GPU_CALL(aby3g_bitmul_p0(a->data(), B.data(), n, &pv, &nx, mOtNextKey.data(), mOtNextIdx,
-                                             C.data(), send.as<i64>(), help.as<i64>(), g.stream()));
+                                             C.data(), send->as<i64>(), help->as<i64>(), g.stream()));
                     mOtNextIdx += 2 * n;
-                    comm.mNext.asyncSendDevice(send.data(), 2 * b8, g);
-                    comm.mNext.asyncSendDevice(help.data(), b8, g);
+                    comm.mNext.asyncSendShared(send, 2 * b8, g);
+                    comm.mNext.asyncSendShared(help, b8, g);
                     break;
                 }
                 case 1: {  // receiver (:165-200)
                     GPU_CALL(aby3g_prng_fill(mShareGen.mPrevSeed.data(), mShareGen.takePrev(8 * n), 8 * n,
                                              C.share(1), g.stream()));
-                    struct R {
-                        DeviceBuffer m0, h0, m1, h1;
-                    };
-                    auto r = std::make_shared<R>();
-                    r->m0.reset(g, 2 * b8);
-                    r->h0.reset(g, b8);
-                    r->m1.reset(g, 2 * b8);
-                    r->h1.reset(g, b8);
-                    // f0 = (sender prev, helper next), f1 = (sender next, helper prev)
-                    auto f0s = comm.mPrev.asyncRecvDevice(r->m0.data(), 2 * b8, g);
-                    auto f0h = comm.mNext.asyncRecvDevice(r->h0.data(), b8, g);
-                    auto f1s = comm.mNext.asyncRecvDevice(r->m1.data(), 2 * b8, g);
-                    auto f1h = comm.mPrev.asyncRecvDevice(r->h1.data(), b8, g);
-                    self.then([r, f0s, f0h, f1s, f1h, &B, &C, n, b8](CommPkg& comm2, Sh3Task& s2) {
-                        f0s.get();
-                        f0h.get();
-                        f1s.get();
-                        f1h.get();
+                    // f0 = (sender prev, helper next), f1 = (sender next, helper prev);
+                    // all four are read in place from the senders' buffers
+                    auto f0s = comm.mPrev.asyncRecvShared(2 * b8, g);
+                    auto f0h = comm.mNext.asyncRecvShared(b8, g);
+                    auto f1s = comm.mNext.asyncRecvShared(2 * b8, g);
+                    auto f1h = comm.mPrev.asyncRecvShared(b8, g);
+                    self.then([f0s, f0h, f1s, f1h, &B, &C, n, b8](CommPkg& comm2, Sh3Task& s2) {
                         Gpu& g2 = s2.getRuntime().gpu();
+                        auto m0 = f0s.getShared(), h0 = f0h.getShared(), m1 = f1s.getShared(), h1 = f1h.getShared();
                         // c0 = recv1 (choice b1 = B[1]) + recv0 (choice b0 = B[0])
-                        GPU_CALL(aby3g_ot_recv(r->m1.as<i64>(), r->h1.as<i64>(), B.share(1), n, 0, C.share(0),
+                        GPU_CALL(aby3g_ot_recv(m1->as<i64>(), h1->as<i64>(), B.share(1), n, 0, C.share(0),
                                                g2.stream()));
-                        GPU_CALL(aby3g_ot_recv(r->m0.as<i64>(), r->h0.as<i64>(), B.share(0), n, 1, C.share(0),
+                        GPU_CALL(aby3g_ot_recv(m0->as<i64>(), h0->as<i64>(), B.share(0), n, 1, C.share(0),
                                                g2.stream()));
+                        for (auto* b : {&m0, &h0, &m1, &h1}) (*b)->fence(g2.stream());
                         comm2.mNext.asyncSendDevice(C.share(0), b8, g2);
                     });
                     break;
                 }
                 case 2: {  // OT sender for P1 (with P0 helping), helper for P0's send (:202-240)
-                    DeviceBuffer send(g, 2 * b8), help(g, b8);
+                    auto send = std::make_shared<DeviceBuffer>(g, 2 * b8);
+                    auto help = std::make_shared<DeviceBuffer>(g, b8);
                     aby3g_stream_pos nx;
                     std::memcpy(nx.seed, mShareGen.mNextSeed.data(), 16);
                     nx.off = mShareGen.takeNext(16 * n);
                     GPU_CALL(aby3g_bitmul_p2(a->data(), B.data(), n, &nx, mOtPrevKey.data(), mOtPrevIdx, C.data(),
-                                             help.as<i64>(), send.as<i64>(), g.stream()));
+                                             help->as<i64>(), send->as<i64>(), g.stream()));
                     mOtPrevIdx += 2 * n;
-                    comm.mPrev.asyncSendDevice(help.data(), b8, g);
-                    comm.mPrev.asyncSendDevice(send.data(), 2 * b8, g);
+                    comm.mPrev.asyncSendShared(help, b8, g);
+                    comm.mPrev.asyncSendShared(send, 2 * b8, g);
                     self.then([&C, b8](CommPkg& comm2, Sh3Task& s2) {
                         auto f = comm2.mPrev.asyncRecvDevice(C.share(1), b8, s2.getRuntime().gpu());
                         s2.then([f](CommPkg&, Sh3Task&) { f.get(); });
@@ -248,14 +242,15 @@ Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, i64 a, const sbMatrix& B, si64Matrix
             C.resize(n, 1);
             switch (self.getRuntime().mPartyIdx) {
                 case 0: {  // (:430-447)
-                    DeviceBuffer mn(g, 2 * b8), mp(g, 2 * b8);
+                    auto mn = std::make_shared<DeviceBuffer>(g, 2 * b8);
+                    auto mp = std::make_shared<DeviceBuffer>(g, 2 * b8);
                     aby3g_zero_share zs = mShareGen.zeroShare(mShareGen.takeDraws(n));
                     GPU_CALL(aby3g_pubmul_p0(a, B.data(), n, &zs, mOtNextKey.data(), mOtNextIdx, mOtPrevKey.data(),
-                                             mOtPrevIdx, mn.as<i64>(), mp.as<i64>(), g.stream()));
+                                             mOtPrevIdx, mn->as<i64>(), mp->as<i64>(), g.stream()));
                     mOtNextIdx += n;
                     mOtPrevIdx += n;
-                    comm.mNext.asyncSendDevice(mn.data(), 2 * b8, g);
-                    comm.mPrev.asyncSendDevice(mp.data(), 2 * b8, g);
+                    comm.mNext.asyncSendShared(mn, 2 * b8, g);
+                    comm.mPrev.asyncSendShared(mp, 2 * b8, g);
                     auto fu1 = comm.mNext.asyncRecvDevice(C.share(0), b8, g);
                     auto fu2 = comm.mPrev.asyncRecvDevice(C.share(1), b8, g);
                     self.then([fu1, fu2](CommPkg&, Sh3Task&) {
@@ -267,33 +262,29 @@ Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, i64 a, const sbMatrix& B, si64Matrix
                 case 1:
                 case 2: {  // (:452-487)
                     const bool p1 = self.getRuntime().mPartyIdx == 1;
-                    DeviceBuffer help(g, b8);
+                    auto help = std::make_shared<DeviceBuffer>(g, b8);
                     aby3g_zero_share zs = mShareGen.zeroShare(mShareGen.takeDraws(n));
                     i64* mine = p1 ? C.share(1) : C.share(0);
                     const u8* key = p1 ? mOtNextKey.data() : mOtPrevKey.data();
                     u64& ctr = p1 ? mOtNextIdx : mOtPrevIdx;
-                    GPU_CALL(aby3g_pubmul_helper(p1 ? B.share(0) : B.share(1), n, &zs, key, ctr, mine, help.as<i64>(),
-                                                 g.stream()));
+                    GPU_CALL(aby3g_pubmul_helper(p1 ? B.share(0) : B.share(1), n, &zs, key, ctr, mine,
+                                                 help->as<i64>(), g.stream()));
                     ctr += n;
                     Channel& toHelped = p1 ? comm.mNext : comm.mPrev;   // the other receiver
                     Channel& toSender = p1 ? comm.mPrev : comm.mNext;   // party 0
-                    toHelped.asyncSendDevice(help.data(), b8, g);
+                    toHelped.asyncSendShared(help, b8, g);
                     toSender.asyncSendDevice(mine, b8, g);
-                    struct R {
-                        DeviceBuffer msgs, hm;
-                    };
-                    auto r = std::make_shared<R>();
-                    r->msgs.reset(g, 2 * b8);
-                    r->hm.reset(g, b8);
-                    auto fs = toSender.asyncRecvDevice(r->msgs.data(), 2 * b8, g);
-                    auto fh = toHelped.asyncRecvDevice(r->hm.data(), b8, g);
+                    // the OT messages and the helper's pads are read in place
+                    auto fs = toSender.asyncRecvShared(2 * b8, g);
+                    auto fh = toHelped.asyncRecvShared(b8, g);
                     i64* theirs = p1 ? C.share(0) : C.share(1);
                     const i64* choice = p1 ? B.share(0) : B.share(1);
-                    self.then([r, fs, fh, theirs, choice, n](CommPkg&, Sh3Task& s2) {
-                        fs.get();
-                        fh.get();
-                        GPU_CALL(aby3g_ot_recv(r->msgs.as<i64>(), r->hm.as<i64>(), choice, n, 0, theirs,
-                                               s2.getRuntime().gpu().stream()));
+                    self.then([fs, fh, theirs, choice, n](CommPkg&, Sh3Task& s2) {
+                        auto msgs = fs.getShared(), hm = fh.getShared();
+                        aby3g_stream st = s2.getRuntime().gpu().stream();
+                        GPU_CALL(aby3g_ot_recv(msgs->as<i64>(), hm->as<i64>(), choice, n, 0, theirs, st));
+                        msgs->fence(st);
+                        hm->fence(st);
                     });
                     break;
                 }

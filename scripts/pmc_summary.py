@@ -58,7 +58,7 @@ def main():
                                  hbm_bytes_per_launch=g.get("hbm_bytes_per_launch"), launches=g.get("launches"))
     else:
         tot = sum(kernels[k]["read_bytes"] + kernels[k]["write_bytes"] for k in kernels
-                  if k in ("k_bin_gates", "k_bin_unpack"))
+                  if k in ("k_bin_gates", "k_bin_unpack", "k_bin_level"))
         out["bin_gates"] = dict(config={"rows": 1 << 20}, hbm_bytes_per_step_per_party=tot / party_steps,
                                 hbm_bytes_per_launch=None)
     out.setdefault("kernels", {})[a.job] = kernels

@@ -32,15 +32,20 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 constexpr u32 BN = 64, BK = 32;  // output tile width, K' per stage
 constexpr u32 kRec = 256;        // bytes per (row, stage) record
 
-// Tile height of the share GEMM: 128 (8 waves, two per SIMD) by default,
-// 64 (4 waves, one per SIMD) with ABY3G_GEMM_TBM=64 -- kept for A/B runs.
-inline u32 gemm_tbm() {
-    static const u32 v = [] {
-        const char* e = getenv("ABY3G_GEMM_TBM");
-        return (e && atoi(e) == 64) ? 64u : 128u;
+// Share-GEMM kernel variant (ABY3G_GEMM_VARIANT, for A/B runs):
+//   'b' (default) 128 x 64 tiles, 8 waves, 2-deep ring, one workgroup per CU
+//   'c' as 'b' with the B fragments read first and MFMAs ordered by A plane
+//   'a' 64 x 64 tiles, 4 waves, 2-deep ring, two workgroups per CU
+//   'd' 64 x 64 tiles, 4 waves, 3-deep ring, one workgroup per CU
+inline char gemm_variant() {
+    static const char v = [] {
+        const char* e = getenv("ABY3G_GEMM_VARIANT");
+        return (e && (e[0] == 'a' || e[0] == 'c' || e[0] == 'd')) ? e[0] : 'b';
     }();
     return v;
 }
+inline u32 gemm_tbm() { return (gemm_variant() == 'a' || gemm_variant() == 'd') ? 64u : 128u; }
+inline u32 gemm_target_wgs() { return gemm_variant() == 'a' ? 512u : 256u; }
 
 inline u64 roundup(u64 x, u64 m) { return (x + m - 1) / m * m; }
 
@@ -72,7 +77,7 @@ GemmPlan plan_gemm(u64 M, u64 K, u64 N) {
     // Enough workgroups for one per CU, at least 8 stages per split, and
     // K' per split <= 8192 so every i32 plane stays exact.
     u32 s = 1;
-    while (tiles * s < 256 && stages / (2 * s) >= 8) s *= 2;
+    while (tiles * s < gemm_target_wgs() && stages / (2 * s) >= 8) s *= 2;
     while ((stages + s - 1) / s * BK > 8192) s *= 2;
     p.splits = s;
     p.kPerSplit = (stages + s - 1) / s * BK;
@@ -211,8 +216,8 @@ typedef __attribute__((address_space(1))) void glb_void;
 //
 // Epilogue: recombine the 8 planes in i64; one split -> out = product (-
 // sub), several -> the split's slab of P.
-template <u32 TBM, u32 NBUF>
-__global__ void __launch_bounds__(TBM / 32 * 2 * 64, 1)
+template <u32 TBM, u32 NBUF, u32 OCC, bool PORD>
+__global__ void __launch_bounds__(TBM / 32 * 2 * 64, OCC)
     k_share_gemm(const u8* __restrict__ Ad, const u8* __restrict__ Bd, u64 M, u64 N, u64 stagesTotal,
                  u64 stagesPerSplit, u32 TM, u32 TN, u32 splits, i64* __restrict__ P, const i64* __restrict__ sub) {
     constexpr u32 kWaves = TBM / 32 * 2, kT = kWaves * 64;
@@ -285,15 +290,31 @@ __global__ void __launch_bounds__(TBM / 32 * 2 * 64, 1)
         if (i + NBUF - 1 < nst) issue(s0 + i + NBUF - 1, (buf + NBUF - 1) % NBUF);
         const u8* ls = lds + buf * kStage;
         v4i a[8], b[8];
+        if (PORD) {
+            // B planes first, then each A plane right before the MFMAs that use it,
+            // so the first MFMAs wait only for the reads they consume
 #pragma unroll
-        for (int p = 0; p < 8; ++p) {
-            a[p] = *reinterpret_cast<const v4i*>(ls + offRA[p]);
-            b[p] = *reinterpret_cast<const v4i*>(ls + offRB[p]);
-        }
+            for (int q = 0; q < 8; ++q) b[q] = *reinterpret_cast<const v4i*>(ls + offRB[q]);
 #pragma unroll
-        for (int s = 0; s < 8; ++s) {
+            for (int p = 0; p < 8; ++p) a[p] = *reinterpret_cast<const v4i*>(ls + offRA[p]);
 #pragma unroll
-            for (int p = 0; p <= s; ++p) acc[s] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[p], b[s - p], acc[s], 0, 0, 0);
+            for (int p = 0; p < 8; ++p) {
+#pragma unroll
+                for (int q = 0; q + p < 8; ++q)
+                    acc[p + q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[p], b[q], acc[p + q], 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+                a[p] = *reinterpret_cast<const v4i*>(ls + offRA[p]);
+                b[p] = *reinterpret_cast<const v4i*>(ls + offRB[p]);
+            }
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+#pragma unroll
+                for (int p = 0; p <= s; ++p)
+                    acc[s] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[p], b[s - p], acc[s], 0, 0, 0);
+            }
         }
         buf = buf + 1 == NBUF ? 0 : buf + 1;
     }
@@ -390,12 +411,25 @@ void run_gemm(const GemmPlan& p, const i64* A, const i64* B, const Workspace& w,
     MfmaTurn turn(s);
     i64* dst = direct ? out : w.P;
     const i64* sb = direct ? sub : nullptr;
-    if (p.tbm == 64)
-        launch(PROBE_GEMM, k_share_gemm<64, 3>, dim3(TM * TN * p.splits), dim3(256), 0, s, (const u8*)w.Ad,
-               (const u8*)w.Bd, p.M, p.N, stages, p.kPerSplit / BK, TM, TN, p.splits, dst, sb);
-    else
-        launch(PROBE_GEMM, k_share_gemm<128, 2>, dim3(TM * TN * p.splits), dim3(512), 0, s, (const u8*)w.Ad,
-               (const u8*)w.Bd, p.M, p.N, stages, p.kPerSplit / BK, TM, TN, p.splits, dst, sb);
+    const dim3 grid(TM * TN * p.splits);
+    const u64 sps = p.kPerSplit / BK;
+    switch (gemm_variant()) {
+        case 'a':
+            launch(PROBE_GEMM, k_share_gemm<64, 2, 2, false>, grid, dim3(256), 0, s, (const u8*)w.Ad, (const u8*)w.Bd,
+                   p.M, p.N, stages, sps, TM, TN, p.splits, dst, sb);
+            break;
+        case 'd':
+            launch(PROBE_GEMM, k_share_gemm<64, 3, 1, false>, grid, dim3(256), 0, s, (const u8*)w.Ad, (const u8*)w.Bd,
+                   p.M, p.N, stages, sps, TM, TN, p.splits, dst, sb);
+            break;
+        case 'c':
+            launch(PROBE_GEMM, k_share_gemm<128, 2, 1, true>, grid, dim3(512), 0, s, (const u8*)w.Ad, (const u8*)w.Bd,
+                   p.M, p.N, stages, sps, TM, TN, p.splits, dst, sb);
+            break;
+        default:
+            launch(PROBE_GEMM, k_share_gemm<128, 2, 1, false>, grid, dim3(512), 0, s, (const u8*)w.Ad,
+                   (const u8*)w.Bd, p.M, p.N, stages, sps, TM, TN, p.splits, dst, sb);
+    }
 }
 
 void check_ws(const GemmPlan& p, void* ws, size_t bytes) {

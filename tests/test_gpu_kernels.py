@@ -55,7 +55,8 @@ def k16(seed):
     return bytes(np.random.default_rng(seed).integers(0, 256, size=16, dtype=np.uint8))
 
 
-@pytest.mark.parametrize("base,n", [(0, 1), (5, 1000), (2**40 + 3, 4097)])
+# sizes >= 2^16 blocks take the bitsliced kernels, smaller ones the T-table ones
+@pytest.mark.parametrize("base,n", [(0, 1), (5, 1000), (2**40 + 3, 4097), (2047, 70001), (2**64 - 100000, 99999)])
 def test_aes_ctr(gpu, base, n):
     key = k16(1)
     out = empty(2 * n)
@@ -72,7 +73,7 @@ def test_prng_fill(gpu, off, n):
 
 
 @pytest.mark.parametrize("kind", [nt.DRAW_ARITH, nt.DRAW_BIN, nt.DRAW_RANDPAIR])
-@pytest.mark.parametrize("base,n", [(0, 1), (1, 2), (513, 5000)])
+@pytest.mark.parametrize("base,n", [(0, 1), (1, 2), (513, 5000), (3, 200003)])
 def test_share_draws(gpu, kind, base, n):
     kp, kn = k16(3), k16(4)
     o0, o1 = empty(n), empty(n)
@@ -155,9 +156,9 @@ def _ts(ns, noff, ps, poff):
 
 @pytest.mark.parametrize("noff,poff", [(32, 32), (40, 32), (32, 48)])
 @pytest.mark.parametrize("d", [8, 16, 27])
-def test_trunc_tuple(gpu, noff, poff, d):
+@pytest.mark.parametrize("n", [3001, 140001])
+def test_trunc_tuple(gpu, noff, poff, d, n):
     ns, ps = k16(11), k16(12)
-    n = 3001
     R, RT = empty(n), empty(2 * n)
     gpu.trunc_tuple(ctypes.byref(_ts(ns, noff, ps, poff)), n, d, P(R), P(RT), None)
     eR, e0, e1 = orc.trunc_tuple(ns, noff, ps, poff, n, d)

@@ -91,43 +91,78 @@ struct AesState {
 // AES-128 of the counter block LE64(ctr) || 0^8 under `k`, T-table form.
 // Column c of the state is the LE word of bytes 4c..4c+3; after ShiftRows,
 // row r of column c comes from column c+r, and MixColumns row weights of
-// input row r are T0 rotated left by 8r bits.
-__host__ __device__ __forceinline__ void aes_ctr_block(const u32* __restrict__ T, u32 lane32, const AesKey& k, u64 ctr,
-                                              u64& lo, u64& hi) {
-    u32 s0 = (u32)ctr ^ k.rk[0];
-    u32 s1 = (u32)(ctr >> 32) ^ k.rk[1];
-    u32 s2 = k.rk[2];
-    u32 s3 = k.rk[3];
-#define T0L(x) T[((x) << 5) | lane32]
+// input row r are T0 rotated left by 8r bits. NB blocks (keys / counters of
+// their own) are interleaved so each round issues 16 * NB independent table
+// reads: the LDS latency of one block hides behind the others.
+#define ABY3G_T0L(x) T[((x) << 5) | lane32]
+#define ABY3G_SB(x) ((ABY3G_T0L(x) >> 8) & 0xff)
+template <int NB>
+__host__ __device__ __forceinline__ void aes_ctr_blocks(const u32* __restrict__ T, u32 lane32, const AesKey* const* k,
+                                                        const u64* ctr, u64* lo, u64* hi) {
+    u32 s0[NB], s1[NB], s2[NB], s3[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        s0[b] = (u32)ctr[b] ^ k[b]->rk[0];
+        s1[b] = (u32)(ctr[b] >> 32) ^ k[b]->rk[1];
+        s2[b] = k[b]->rk[2];
+        s3[b] = k[b]->rk[3];
+    }
 #pragma unroll
     for (int r = 1; r < 10; ++r) {
-        u32 t0 = T0L(s0 & 0xff) ^ rotl(T0L((s1 >> 8) & 0xff), 8) ^ rotl(T0L((s2 >> 16) & 0xff), 16) ^
-                 rotl(T0L(s3 >> 24), 24) ^ k.rk[4 * r + 0];
-        u32 t1 = T0L(s1 & 0xff) ^ rotl(T0L((s2 >> 8) & 0xff), 8) ^ rotl(T0L((s3 >> 16) & 0xff), 16) ^
-                 rotl(T0L(s0 >> 24), 24) ^ k.rk[4 * r + 1];
-        u32 t2 = T0L(s2 & 0xff) ^ rotl(T0L((s3 >> 8) & 0xff), 8) ^ rotl(T0L((s0 >> 16) & 0xff), 16) ^
-                 rotl(T0L(s1 >> 24), 24) ^ k.rk[4 * r + 2];
-        u32 t3 = T0L(s3 & 0xff) ^ rotl(T0L((s0 >> 8) & 0xff), 8) ^ rotl(T0L((s1 >> 16) & 0xff), 16) ^
-                 rotl(T0L(s2 >> 24), 24) ^ k.rk[4 * r + 3];
-        s0 = t0;
-        s1 = t1;
-        s2 = t2;
-        s3 = t3;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const u32* rk = k[b]->rk;
+            u32 t0 = ABY3G_T0L(s0[b] & 0xff) ^ rotl(ABY3G_T0L((s1[b] >> 8) & 0xff), 8) ^
+                     rotl(ABY3G_T0L((s2[b] >> 16) & 0xff), 16) ^ rotl(ABY3G_T0L(s3[b] >> 24), 24) ^ rk[4 * r + 0];
+            u32 t1 = ABY3G_T0L(s1[b] & 0xff) ^ rotl(ABY3G_T0L((s2[b] >> 8) & 0xff), 8) ^
+                     rotl(ABY3G_T0L((s3[b] >> 16) & 0xff), 16) ^ rotl(ABY3G_T0L(s0[b] >> 24), 24) ^ rk[4 * r + 1];
+            u32 t2 = ABY3G_T0L(s2[b] & 0xff) ^ rotl(ABY3G_T0L((s3[b] >> 8) & 0xff), 8) ^
+                     rotl(ABY3G_T0L((s0[b] >> 16) & 0xff), 16) ^ rotl(ABY3G_T0L(s1[b] >> 24), 24) ^ rk[4 * r + 2];
+            u32 t3 = ABY3G_T0L(s3[b] & 0xff) ^ rotl(ABY3G_T0L((s0[b] >> 8) & 0xff), 8) ^
+                     rotl(ABY3G_T0L((s1[b] >> 16) & 0xff), 16) ^ rotl(ABY3G_T0L(s2[b] >> 24), 24) ^ rk[4 * r + 3];
+            s0[b] = t0;
+            s1[b] = t1;
+            s2[b] = t2;
+            s3[b] = t3;
+        }
     }
     // last round: SubBytes + ShiftRows; S[x] = byte 1 of T0[x]
-#define SB(x) ((T0L(x) >> 8) & 0xff)
-    u32 o0 = (SB(s0 & 0xff) | (SB((s1 >> 8) & 0xff) << 8) | (SB((s2 >> 16) & 0xff) << 16) | (SB(s3 >> 24) << 24)) ^
-             k.rk[40];
-    u32 o1 = (SB(s1 & 0xff) | (SB((s2 >> 8) & 0xff) << 8) | (SB((s3 >> 16) & 0xff) << 16) | (SB(s0 >> 24) << 24)) ^
-             k.rk[41];
-    u32 o2 = (SB(s2 & 0xff) | (SB((s3 >> 8) & 0xff) << 8) | (SB((s0 >> 16) & 0xff) << 16) | (SB(s1 >> 24) << 24)) ^
-             k.rk[42];
-    u32 o3 = (SB(s3 & 0xff) | (SB((s0 >> 8) & 0xff) << 8) | (SB((s1 >> 16) & 0xff) << 16) | (SB(s2 >> 24) << 24)) ^
-             k.rk[43];
-#undef SB
-#undef T0L
-    lo = (u64)o0 | ((u64)o1 << 32);
-    hi = (u64)o2 | ((u64)o3 << 32);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const u32* rk = k[b]->rk;
+        u32 o0 = (ABY3G_SB(s0[b] & 0xff) | (ABY3G_SB((s1[b] >> 8) & 0xff) << 8) |
+                  (ABY3G_SB((s2[b] >> 16) & 0xff) << 16) | (ABY3G_SB(s3[b] >> 24) << 24)) ^ rk[40];
+        u32 o1 = (ABY3G_SB(s1[b] & 0xff) | (ABY3G_SB((s2[b] >> 8) & 0xff) << 8) |
+                  (ABY3G_SB((s3[b] >> 16) & 0xff) << 16) | (ABY3G_SB(s0[b] >> 24) << 24)) ^ rk[41];
+        u32 o2 = (ABY3G_SB(s2[b] & 0xff) | (ABY3G_SB((s3[b] >> 8) & 0xff) << 8) |
+                  (ABY3G_SB((s0[b] >> 16) & 0xff) << 16) | (ABY3G_SB(s1[b] >> 24) << 24)) ^ rk[42];
+        u32 o3 = (ABY3G_SB(s3[b] & 0xff) | (ABY3G_SB((s0[b] >> 8) & 0xff) << 8) |
+                  (ABY3G_SB((s1[b] >> 16) & 0xff) << 16) | (ABY3G_SB(s2[b] >> 24) << 24)) ^ rk[43];
+        lo[b] = (u64)o0 | ((u64)o1 << 32);
+        hi[b] = (u64)o2 | ((u64)o3 << 32);
+    }
+}
+#undef ABY3G_SB
+#undef ABY3G_T0L
+
+__host__ __device__ __forceinline__ void aes_ctr_block(const u32* __restrict__ T, u32 lane32, const AesKey& k, u64 ctr,
+                                              u64& lo, u64& hi) {
+    const AesKey* kp = &k;
+    aes_ctr_blocks<1>(T, lane32, &kp, &ctr, &lo, &hi);
+}
+
+// two independent blocks, interleaved (e.g. the prev / next keys of a draw)
+__host__ __device__ __forceinline__ void aes_ctr_block2(const u32* __restrict__ T, u32 lane32, const AesKey& k1,
+                                                        u64 c1, const AesKey& k2, u64 c2, u64& lo1, u64& hi1,
+                                                        u64& lo2, u64& hi2) {
+    const AesKey* ks[2] = {&k1, &k2};
+    const u64 cs[2] = {c1, c2};
+    u64 lo[2], hi[2];
+    aes_ctr_blocks<2>(T, lane32, ks, cs, lo, hi);
+    lo1 = lo[0];
+    hi1 = hi[0];
+    lo2 = lo[1];
+    hi2 = hi[1];
 }
 
 // Grid sizing for grid-stride AES kernels: every workgroup pays a 32 KiB LDS

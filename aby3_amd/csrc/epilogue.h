@@ -26,6 +26,28 @@ __device__ __forceinline__ void stream_window(const u32* T, const AesKey& k, u64
     }
 }
 
+// Two stream windows at once: wn <- words [nw, nw + En) of kn's stream,
+// wp <- words [pw, pw + Ep) of kp's, two AES blocks interleaved per step.
+__device__ __forceinline__ void stream_window2(const u32* T, const AesKey& kn, u64 nw, u32 En, u64* wn,
+                                               const AesKey& kp, u64 pw, u32 Ep, u64* wp) {
+    const u64 cn0 = nw >> 1, cp0 = pw >> 1;
+    const u32 ncn = (u32)(((nw + En - 1) >> 1) - cn0 + 1), ncp = (u32)(((pw + Ep - 1) >> 1) - cp0 + 1);
+    const u32 nc = ncn > ncp ? ncn : ncp;
+    const u32 lane32 = threadIdx.x & 31;
+    for (u32 j = threadIdx.x; j < nc; j += blockDim.x) {
+        u64 a0, a1, b0, b1;
+        aes_ctr_block2(T, lane32, kn, cn0 + j, kp, cp0 + j, a0, a1, b0, b1);
+        if (j < ncn) {
+            wn[2 * j] = a0;
+            wn[2 * j + 1] = a1;
+        }
+        if (j < ncp) {
+            wp[2 * j] = b0;
+            wp[2 * j + 1] = b1;
+        }
+    }
+}
+
 // No product: plain getTruncationTuple.
 struct SrcNone {
     __device__ u64 operator()(u64) const { return 0; }
@@ -116,8 +138,7 @@ __global__ void __launch_bounds__(kEpiBlock) k_finish_zero_share(const u32* __re
     for (u64 c = c_first + (u64)blockIdx.x * blockDim.x + threadIdx.x; c <= c_last;
          c += (u64)gridDim.x * blockDim.x) {
         u64 p[2], q[2];
-        aes_ctr_block(lds, lane32, kp, c, p[0], p[1]);
-        aes_ctr_block(lds, lane32, kn, c, q[0], q[1]);
+        aes_ctr_block2(lds, lane32, kp, c, kn, c, p[0], p[1], q[0], q[1]);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             u64 j = 2 * c + h;
@@ -140,8 +161,7 @@ __global__ void __launch_bounds__(kEpiBlock) k_finish_trunc(const u32* __restric
     for (u64 e0 = (u64)blockIdx.x * kEpiWin; e0 < n; e0 += (u64)gridDim.x * kEpiWin) {
         const u32 E = (u32)min((u64)kEpiWin, n - e0);
         __syncthreads();
-        stream_window(lds, kn, nw0 + e0, E, wn);
-        stream_window(lds, kp, pw0 + e0, E, wp);
+        stream_window2(lds, kn, nw0 + e0, E, wn, kp, pw0 + e0, E, wp);
         __syncthreads();
         const u32 on = (u32)((nw0 + e0) & 1), op = (u32)((pw0 + e0) & 1);
         for (u32 e = threadIdx.x; e < E; e += blockDim.x) {

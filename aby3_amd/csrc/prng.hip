@@ -19,11 +19,18 @@ __global__ void __launch_bounds__(kBlock) k_aes_ctr(const u32* __restrict__ T0g,
     extern __shared__ u32 lds[];
     aes_fill_lds(lds, T0g);
     const u32 lane32 = threadIdx.x & 31;
-    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
-        u64 lo, hi;
-        aes_ctr_block(lds, lane32, k, base + i, lo, hi);
+    const u64 stride = (u64)gridDim.x * blockDim.x;
+    // two counters per step, interleaved: i and i + stride
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += 2 * stride) {
+        const u64 i2 = i + stride;
+        u64 lo, hi, lo2, hi2;
+        aes_ctr_block2(lds, lane32, k, base + i, k, base + i2, lo, hi, lo2, hi2);
         out[2 * i] = lo;
         out[2 * i + 1] = hi;
+        if (i2 < n) {
+            out[2 * i2] = lo2;
+            out[2 * i2 + 1] = hi2;
+        }
     }
 }
 
@@ -55,8 +62,7 @@ __global__ void __launch_bounds__(kBlock) k_share_draws(const u32* __restrict__ 
     for (u64 c = c_first + (u64)blockIdx.x * blockDim.x + threadIdx.x; c <= c_last;
          c += (u64)gridDim.x * blockDim.x) {
         u64 p[2], q[2];
-        aes_ctr_block(lds, lane32, kp, c, p[0], p[1]);
-        aes_ctr_block(lds, lane32, kn, c, q[0], q[1]);
+        aes_ctr_block2(lds, lane32, kp, c, kn, c, p[0], p[1], q[0], q[1]);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             u64 j = 2 * c + h;
@@ -93,8 +99,7 @@ __global__ void __launch_bounds__(kBlock) k_bitmul_p0(const u32* __restrict__ T0
     for (u64 e0 = (u64)blockIdx.x * E; e0 < n; e0 += (u64)gridDim.x * E) {
         const u32 En = (u32)min((u64)E, n - e0);
         __syncthreads();
-        stream_window(lds, kprev, pw0 + 2 * e0, 2 * En, wp);
-        stream_window(lds, knext, nw0 + e0, En, wn);
+        stream_window2(lds, kprev, pw0 + 2 * e0, 2 * En, wp, knext, nw0 + e0, En, wn);
         __syncthreads();
         const u32 op = (u32)((pw0 + 2 * e0) & 1), on = (u32)((nw0 + e0) & 1);
         for (u32 e = threadIdx.x; e < En; e += blockDim.x) {
@@ -108,12 +113,11 @@ __global__ void __launch_bounds__(kBlock) k_bitmul_p0(const u32* __restrict__ T0
             u64 s[2];
             s[bb0] = zz;
             s[bb0 ^ 1] = a + zz;
-            u64 lo, hi;
-            aes_ctr_block(lds, lane32, kot, ctr + i, lo, hi);  // send pads
+            u64 lo, hi, hlo, hhi;  // send pads, help pads
+            aes_ctr_block2(lds, lane32, kot, ctr + i, kot, ctr + n + i, lo, hi, hlo, hhi);
             send[2 * i] = (i64)(lo ^ s[0]);
             send[2 * i + 1] = (i64)(hi ^ s[1]);
-            aes_ctr_block(lds, lane32, kot, ctr + n + i, lo, hi);  // help pads
-            help[i] = (i64)(bb1 ? hi : lo);
+            help[i] = (i64)(bb1 ? hhi : hlo);
         }
     }
 }
@@ -143,10 +147,9 @@ __global__ void __launch_bounds__(kBlock) k_bitmul_p2(const u32* __restrict__ T0
             u64 s[2];
             s[bb1] = zr;
             s[bb1 ^ 1] = (u64)A1[i] + zr;
-            u64 lo, hi;
-            aes_ctr_block(lds, lane32, kot, ctr + i, lo, hi);
-            help[i] = (i64)(bb0 ? hi : lo);
-            aes_ctr_block(lds, lane32, kot, ctr + n + i, lo, hi);
+            u64 lo, hi, hlo, hhi;  // help pads, send pads
+            aes_ctr_block2(lds, lane32, kot, ctr + i, kot, ctr + n + i, hlo, hhi, lo, hi);
+            help[i] = (i64)(bb0 ? hhi : hlo);
             send[2 * i] = (i64)(lo ^ s[0]);
             send[2 * i + 1] = (i64)(hi ^ s[1]);
         }
@@ -174,20 +177,18 @@ __global__ void __launch_bounds__(kBlock) k_pubmul_p0(const u32* __restrict__ T0
     for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
         const u64 j = dbase + i;
         u64 p[2], q[2];
-        aes_ctr_block(lds, lane32, kp, j >> 1, p[0], p[1]);
-        aes_ctr_block(lds, lane32, kn, j >> 1, q[0], q[1]);
+        aes_ctr_block2(lds, lane32, kp, j >> 1, kn, j >> 1, p[0], p[1], q[0], q[1]);
         const u64 zs = p[j & 1] - q[j & 1];
         const u32 bb = (u32)((B0[i] ^ B1[i]) & 1);
         u64 s[2];
         s[bb] = zs;
         s[bb ^ 1] = (u64)a + zs;
-        u64 lo, hi;
-        aes_ctr_block(lds, lane32, kon, ctrn + i, lo, hi);
+        u64 lo, hi, lo2, hi2;
+        aes_ctr_block2(lds, lane32, kon, ctrn + i, kop, ctrp + i, lo, hi, lo2, hi2);
         mnext[2 * i] = (i64)(lo ^ s[0]);
         mnext[2 * i + 1] = (i64)(hi ^ s[1]);
-        aes_ctr_block(lds, lane32, kop, ctrp + i, lo, hi);
-        mprev[2 * i] = (i64)(lo ^ s[0]);
-        mprev[2 * i + 1] = (i64)(hi ^ s[1]);
+        mprev[2 * i] = (i64)(lo2 ^ s[0]);
+        mprev[2 * i + 1] = (i64)(hi2 ^ s[1]);
     }
 }
 
@@ -201,8 +202,7 @@ __global__ void __launch_bounds__(kBlock) k_pubmul_helper(const u32* __restrict_
     for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
         const u64 j = dbase + i;
         u64 p[2], q[2];
-        aes_ctr_block(lds, lane32, kp, j >> 1, p[0], p[1]);
-        aes_ctr_block(lds, lane32, kn, j >> 1, q[0], q[1]);
+        aes_ctr_block2(lds, lane32, kp, j >> 1, kn, j >> 1, p[0], p[1], q[0], q[1]);
         share[i] = (i64)(p[j & 1] - q[j & 1]);
         u64 lo, hi;
         aes_ctr_block(lds, lane32, kot, ctr + i, lo, hi);

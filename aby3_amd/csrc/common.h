@@ -71,34 +71,58 @@ AesKey expand_key(const u8 key[16]);
 // (computed on the host from the S-box definition, uploaded once).
 const u32* aes_table();
 
-// The LDS copy of T0 is replicated 32 times with entry x of copy c at word
-// 32*x + c, and lane l reads copy (l & 31): ds_read_b32 serves a wave in two
+// LDS image of the round tables: T0 and T1 = rotl(T0, 8), each replicated
+// 32 times, at byte address x << 8 | t << 7 | c << 2 (table t, entry x,
+// copy c). Lane l reads copy (l & 31): ds_read_b32 serves a wave in two
 // 32-lane halves over 32 banks, so every lane hits its own bank and the
-// random S-box lookups are conflict-free. 32 KiB per workgroup.
-constexpr int kAesLdsWords = 256 * 32;
-
-__device__ __forceinline__ void aes_fill_lds(u32* lds, const u32* __restrict__ T0g) {
-    for (int i = threadIdx.x; i < kAesLdsWords; i += blockDim.x) lds[i] = T0g[i >> 5];
-    __syncthreads();
-}
+// random lookups are conflict-free. Because the entry sits in address byte 1
+// and (table, copy) in byte 0, one v_perm_b32 of (state word, per-lane
+// constant) forms a lookup address -- one VALU op instead of extract + scale
+// + add. 64 KiB per workgroup.
+constexpr int kAesLdsWords = 256 * 64;
 
 __host__ __device__ __forceinline__ u32 rotl(u32 x, int r) { return __builtin_rotateleft32(x, r); }
 
-struct AesState {
-    u32 s0, s1, s2, s3;
-};
+__device__ __forceinline__ void aes_fill_lds(u32* lds, const u32* __restrict__ T0g) {
+    for (int i = threadIdx.x; i < kAesLdsWords; i += blockDim.x) {
+        const u32 v = T0g[i >> 6];
+        lds[i] = (i & 32) ? rotl(v, 8) : v;
+    }
+    __syncthreads();
+}
+
+// byte offset of the entry (byte j of s) in the table / copy selected by L's byte 0
+__host__ __device__ __forceinline__ u32 aes_addr(u32 s, u32 L, int j) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_perm(s, L, 0x0c0c0000u | ((4u + j) << 8));
+#else
+    return (((s >> (8 * j)) & 0xffu) << 8) | (L & 0xffu);
+#endif
+}
+
+// S-box bytes of four T0 entries, packed little-endian: S[x] = byte 1 of T0[x]
+__host__ __device__ __forceinline__ u32 aes_sb4(u32 A, u32 B, u32 C, u32 D) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const u32 u = __builtin_amdgcn_perm(B, A, 0x0c0c0501u), v = __builtin_amdgcn_perm(D, C, 0x0c0c0501u);
+    return __builtin_amdgcn_perm(v, u, 0x05040100u);
+#else
+    return ((A >> 8) & 0xffu) | (B & 0xff00u) | (((C >> 8) & 0xffu) << 16) | ((D & 0xff00u) << 16);
+#endif
+}
 
 // AES-128 of the counter block LE64(ctr) || 0^8 under `k`, T-table form.
 // Column c of the state is the LE word of bytes 4c..4c+3; after ShiftRows,
 // row r of column c comes from column c+r, and MixColumns row weights of
-// input row r are T0 rotated left by 8r bits. NB blocks (keys / counters of
-// their own) are interleaved so each round issues 16 * NB independent table
-// reads: the LDS latency of one block hides behind the others.
-#define ABY3G_T0L(x) T[((x) << 5) | lane32]
-#define ABY3G_SB(x) ((ABY3G_T0L(x) >> 8) & 0xff)
+// input row r are T0 rotated left by 8r bits, so a column is
+//   T0[a] ^ T1[b] ^ rotl(T0[c] ^ T1[d], 16) ^ rk.
+// NB blocks (keys / counters of their own) are interleaved so each round
+// issues 16 * NB independent table reads.
 template <int NB>
 __host__ __device__ __forceinline__ void aes_ctr_blocks(const u32* __restrict__ T, u32 lane32, const AesKey* const* k,
                                                         const u64* ctr, u64* lo, u64* hi) {
+    const u8* Tb = reinterpret_cast<const u8*>(T);
+    const u32 L0 = lane32 << 2, L1 = L0 | 0x80u;
+#define ABY3G_TL(s, L, j) (*reinterpret_cast<const u32*>(Tb + aes_addr((s), (L), (j))))
     u32 s0[NB], s1[NB], s2[NB], s3[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
@@ -112,38 +136,37 @@ __host__ __device__ __forceinline__ void aes_ctr_blocks(const u32* __restrict__ 
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
             const u32* rk = k[b]->rk;
-            u32 t0 = ABY3G_T0L(s0[b] & 0xff) ^ rotl(ABY3G_T0L((s1[b] >> 8) & 0xff), 8) ^
-                     rotl(ABY3G_T0L((s2[b] >> 16) & 0xff), 16) ^ rotl(ABY3G_T0L(s3[b] >> 24), 24) ^ rk[4 * r + 0];
-            u32 t1 = ABY3G_T0L(s1[b] & 0xff) ^ rotl(ABY3G_T0L((s2[b] >> 8) & 0xff), 8) ^
-                     rotl(ABY3G_T0L((s3[b] >> 16) & 0xff), 16) ^ rotl(ABY3G_T0L(s0[b] >> 24), 24) ^ rk[4 * r + 1];
-            u32 t2 = ABY3G_T0L(s2[b] & 0xff) ^ rotl(ABY3G_T0L((s3[b] >> 8) & 0xff), 8) ^
-                     rotl(ABY3G_T0L((s0[b] >> 16) & 0xff), 16) ^ rotl(ABY3G_T0L(s1[b] >> 24), 24) ^ rk[4 * r + 2];
-            u32 t3 = ABY3G_T0L(s3[b] & 0xff) ^ rotl(ABY3G_T0L((s0[b] >> 8) & 0xff), 8) ^
-                     rotl(ABY3G_T0L((s1[b] >> 16) & 0xff), 16) ^ rotl(ABY3G_T0L(s2[b] >> 24), 24) ^ rk[4 * r + 3];
+            const u32 t0 = ABY3G_TL(s0[b], L0, 0) ^ ABY3G_TL(s1[b], L1, 1) ^
+                           rotl(ABY3G_TL(s2[b], L0, 2) ^ ABY3G_TL(s3[b], L1, 3), 16) ^ rk[4 * r + 0];
+            const u32 t1 = ABY3G_TL(s1[b], L0, 0) ^ ABY3G_TL(s2[b], L1, 1) ^
+                           rotl(ABY3G_TL(s3[b], L0, 2) ^ ABY3G_TL(s0[b], L1, 3), 16) ^ rk[4 * r + 1];
+            const u32 t2 = ABY3G_TL(s2[b], L0, 0) ^ ABY3G_TL(s3[b], L1, 1) ^
+                           rotl(ABY3G_TL(s0[b], L0, 2) ^ ABY3G_TL(s1[b], L1, 3), 16) ^ rk[4 * r + 2];
+            const u32 t3 = ABY3G_TL(s3[b], L0, 0) ^ ABY3G_TL(s0[b], L1, 1) ^
+                           rotl(ABY3G_TL(s1[b], L0, 2) ^ ABY3G_TL(s2[b], L1, 3), 16) ^ rk[4 * r + 3];
             s0[b] = t0;
             s1[b] = t1;
             s2[b] = t2;
             s3[b] = t3;
         }
     }
-    // last round: SubBytes + ShiftRows; S[x] = byte 1 of T0[x]
+    // last round: SubBytes + ShiftRows
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
         const u32* rk = k[b]->rk;
-        u32 o0 = (ABY3G_SB(s0[b] & 0xff) | (ABY3G_SB((s1[b] >> 8) & 0xff) << 8) |
-                  (ABY3G_SB((s2[b] >> 16) & 0xff) << 16) | (ABY3G_SB(s3[b] >> 24) << 24)) ^ rk[40];
-        u32 o1 = (ABY3G_SB(s1[b] & 0xff) | (ABY3G_SB((s2[b] >> 8) & 0xff) << 8) |
-                  (ABY3G_SB((s3[b] >> 16) & 0xff) << 16) | (ABY3G_SB(s0[b] >> 24) << 24)) ^ rk[41];
-        u32 o2 = (ABY3G_SB(s2[b] & 0xff) | (ABY3G_SB((s3[b] >> 8) & 0xff) << 8) |
-                  (ABY3G_SB((s0[b] >> 16) & 0xff) << 16) | (ABY3G_SB(s1[b] >> 24) << 24)) ^ rk[42];
-        u32 o3 = (ABY3G_SB(s3[b] & 0xff) | (ABY3G_SB((s0[b] >> 8) & 0xff) << 8) |
-                  (ABY3G_SB((s1[b] >> 16) & 0xff) << 16) | (ABY3G_SB(s2[b] >> 24) << 24)) ^ rk[43];
+        const u32 o0 = aes_sb4(ABY3G_TL(s0[b], L0, 0), ABY3G_TL(s1[b], L0, 1), ABY3G_TL(s2[b], L0, 2),
+                               ABY3G_TL(s3[b], L0, 3)) ^ rk[40];
+        const u32 o1 = aes_sb4(ABY3G_TL(s1[b], L0, 0), ABY3G_TL(s2[b], L0, 1), ABY3G_TL(s3[b], L0, 2),
+                               ABY3G_TL(s0[b], L0, 3)) ^ rk[41];
+        const u32 o2 = aes_sb4(ABY3G_TL(s2[b], L0, 0), ABY3G_TL(s3[b], L0, 1), ABY3G_TL(s0[b], L0, 2),
+                               ABY3G_TL(s1[b], L0, 3)) ^ rk[42];
+        const u32 o3 = aes_sb4(ABY3G_TL(s3[b], L0, 0), ABY3G_TL(s0[b], L0, 1), ABY3G_TL(s1[b], L0, 2),
+                               ABY3G_TL(s2[b], L0, 3)) ^ rk[43];
         lo[b] = (u64)o0 | ((u64)o1 << 32);
         hi[b] = (u64)o2 | ((u64)o3 << 32);
     }
+#undef ABY3G_TL
 }
-#undef ABY3G_SB
-#undef ABY3G_T0L
 
 __host__ __device__ __forceinline__ void aes_ctr_block(const u32* __restrict__ T, u32 lane32, const AesKey& k, u64 ctr,
                                               u64& lo, u64& hi) {
@@ -165,12 +188,12 @@ __host__ __device__ __forceinline__ void aes_ctr_block2(const u32* __restrict__ 
     hi2 = hi[1];
 }
 
-// Grid sizing for grid-stride AES kernels: every workgroup pays a 32 KiB LDS
-// table fill, so stop at 4 workgroups per CU and let each one loop over
-// several windows; never more workgroups than the work.
+// Grid sizing for grid-stride AES kernels: every workgroup pays a 64 KiB LDS
+// table fill and two fit a CU, so stop at 2 workgroups per CU (512) and let
+// each one loop over several windows; never more workgroups than the work.
 inline u32 aes_grid(u64 items, u32 block) {
     u64 g = (items + block - 1) / block;
-    if (g > 1024) g = 1024;
+    if (g > 512) g = 512;
     return (u32)(g ? g : 1);
 }
 

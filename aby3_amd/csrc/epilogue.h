@@ -10,7 +10,6 @@ namespace aby3g {
 
 constexpr u32 kEpiBlock = 256;
 constexpr u32 kEpiWin = 512;  // elements per window (2 per thread)
-constexpr size_t kAesLds = kAesLdsWords * sizeof(u32);
 
 // win[0 .. 2*nc) <- words of PRNG stream k covering stream words
 // [wbase, wbase + E); the word of element e is win[(wbase & 1) + e].
@@ -131,7 +130,7 @@ template <class Src>
 __global__ void __launch_bounds__(kEpiBlock) k_finish_zero_share(const u32* __restrict__ T0g, Src src, u64 n,
                                                                  AesKey kp, AesKey kn, u64 base,
                                                                  i64* __restrict__ C0) {
-    extern __shared__ u32 lds[];
+    __shared__ u32 lds[kAesLdsWords];  // static: lookups fold the table base into ds_read's offset
     aes_fill_lds(lds, T0g);
     const u32 lane32 = threadIdx.x & 31;
     const u64 c_first = base >> 1, c_last = (base + n - 1) >> 1;
@@ -155,7 +154,7 @@ __global__ void __launch_bounds__(kEpiBlock) k_finish_trunc(const u32* __restric
                                                             AesKey kp, u64 pw0, u64 n, u32 d, i64* __restrict__ R,
                                                             i64* __restrict__ RT0, i64* __restrict__ RT1,
                                                             i64* __restrict__ z) {
-    extern __shared__ u32 lds[];
+    __shared__ u32 lds[kAesLdsWords];  // static: lookups fold the table base into ds_read's offset
     aes_fill_lds(lds, T0g);
     __shared__ u64 wn[kEpiWin + 2], wp[kEpiWin + 2];
     for (u64 e0 = (u64)blockIdx.x * kEpiWin; e0 < n; e0 += (u64)gridDim.x * kEpiWin) {
@@ -181,7 +180,7 @@ void launch_finish_zero_share(Src src, u64 n, const aby3g_zero_share& zs, i64* C
     if (!n) return;
     AesKey kp = expand_key(zs.k_prev), kn = expand_key(zs.k_next);
     u64 counters = ((zs.draw_base + n - 1) >> 1) - (zs.draw_base >> 1) + 1;
-    launch(PROBE_EPILOGUE, k_finish_zero_share<Src>, dim3(aes_grid(counters, kEpiBlock)), dim3(kEpiBlock), kAesLds, s,
+    launch(PROBE_EPILOGUE, k_finish_zero_share<Src>, dim3(aes_grid(counters, kEpiBlock)), dim3(kEpiBlock), 0, s,
            aes_table(), src, n, kp, kn, zs.draw_base, C0);
 }
 
@@ -199,7 +198,7 @@ void launch_finish_trunc(Src src, const aby3g_trunc_streams& ts, u64 n, unsigned
     if (!n) return;
     AesKey kn = expand_key(ts.next_seed), kp = expand_key(ts.prev_seed);
     u32 grid = aes_grid((n + kEpiWin - 1) / kEpiWin, 1);
-    launch(PROBE_EPILOGUE, k_finish_trunc<Src>, dim3(grid), dim3(kEpiBlock), kAesLds, s, aes_table(), src, kn,
+    launch(PROBE_EPILOGUE, k_finish_trunc<Src>, dim3(grid), dim3(kEpiBlock), 0, s, aes_table(), src, kn,
            ts.next_off / 8, kp, ts.prev_off / 8, n, (u32)d, R, RT0, RT1, z);
 }
 

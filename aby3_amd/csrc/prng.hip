@@ -16,7 +16,7 @@ constexpr u32 kWin = kEpiWin;
 
 __global__ void __launch_bounds__(kBlock) k_aes_ctr(const u32* __restrict__ T0g, AesKey k, u64 base, u64 n,
                                                     u64* __restrict__ out) {
-    extern __shared__ u32 lds[];
+    __shared__ u32 lds[kAesLdsWords];  // static: lookups fold the table base into ds_read's offset
     aes_fill_lds(lds, T0g);
     const u32 lane32 = threadIdx.x & 31;
     const u64 stride = (u64)gridDim.x * blockDim.x;
@@ -37,7 +37,7 @@ __global__ void __launch_bounds__(kBlock) k_aes_ctr(const u32* __restrict__ T0g,
 // out[i] = stream word (w0 + i), i < n
 __global__ void __launch_bounds__(kBlock) k_prng_words(const u32* __restrict__ T0g, AesKey k, u64 w0, u64 n,
                                                        u64* __restrict__ out) {
-    extern __shared__ u32 lds[];
+    __shared__ u32 lds[kAesLdsWords];  // static: lookups fold the table base into ds_read's offset
     aes_fill_lds(lds, T0g);
     const u32 lane32 = threadIdx.x & 31;
     const u64 c_first = w0 >> 1, c_last = (w0 + n - 1) >> 1;
@@ -55,7 +55,7 @@ __global__ void __launch_bounds__(kBlock) k_prng_words(const u32* __restrict__ T
 __global__ void __launch_bounds__(kBlock) k_share_draws(const u32* __restrict__ T0g, AesKey kp, AesKey kn, int kind,
                                                         u64 base, u64 n, const i64* __restrict__ addend,
                                                         i64* __restrict__ out0, i64* __restrict__ out1) {
-    extern __shared__ u32 lds[];
+    __shared__ u32 lds[kAesLdsWords];  // static: lookups fold the table base into ds_read's offset
     aes_fill_lds(lds, T0g);
     const u32 lane32 = threadIdx.x & 31;
     const u64 c_first = base >> 1, c_last = (base + n - 1) >> 1;
@@ -91,7 +91,7 @@ __global__ void __launch_bounds__(kBlock) k_bitmul_p0(const u32* __restrict__ T0
                                                       AesKey knext, u64 nw0, AesKey kot, u64 ctr,
                                                       i64* __restrict__ C0, i64* __restrict__ C1,
                                                       i64* __restrict__ send, i64* __restrict__ help) {
-    extern __shared__ u32 lds[];
+    __shared__ u32 lds[kAesLdsWords];  // static: lookups fold the table base into ds_read's offset
     aes_fill_lds(lds, T0g);
     constexpr u32 E = kWin / 2;  // 256 elements: 512 prev words, 256 next words
     __shared__ u64 wp[2 * E + 2], wn[E + 2];
@@ -128,7 +128,7 @@ __global__ void __launch_bounds__(kBlock) k_bitmul_p2(const u32* __restrict__ T0
                                                       AesKey knext, u64 nw0, AesKey kot, u64 ctr,
                                                       i64* __restrict__ C0, i64* __restrict__ help,
                                                       i64* __restrict__ send) {
-    extern __shared__ u32 lds[];
+    __shared__ u32 lds[kAesLdsWords];  // static: lookups fold the table base into ds_read's offset
     aes_fill_lds(lds, T0g);
     constexpr u32 E = kWin / 2;
     __shared__ u64 wn[2 * E + 2];
@@ -171,7 +171,7 @@ __global__ void __launch_bounds__(kBlock) k_pubmul_p0(const u32* __restrict__ T0
                                                       const i64* __restrict__ B1, u64 n, AesKey kp, AesKey kn,
                                                       u64 dbase, AesKey kon, u64 ctrn, AesKey kop, u64 ctrp,
                                                       i64* __restrict__ mnext, i64* __restrict__ mprev) {
-    extern __shared__ u32 lds[];
+    __shared__ u32 lds[kAesLdsWords];  // static: lookups fold the table base into ds_read's offset
     aes_fill_lds(lds, T0g);
     const u32 lane32 = threadIdx.x & 31;
     for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
@@ -196,7 +196,7 @@ __global__ void __launch_bounds__(kBlock) k_pubmul_p0(const u32* __restrict__ T0
 __global__ void __launch_bounds__(kBlock) k_pubmul_helper(const u32* __restrict__ T0g, const i64* __restrict__ choice,
                                                           u64 n, AesKey kp, AesKey kn, u64 dbase, AesKey kot, u64 ctr,
                                                           i64* __restrict__ share, i64* __restrict__ help) {
-    extern __shared__ u32 lds[];
+    __shared__ u32 lds[kAesLdsWords];  // static: lookups fold the table base into ds_read's offset
     aes_fill_lds(lds, T0g);
     const u32 lane32 = threadIdx.x & 31;
     for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
@@ -219,7 +219,7 @@ void share_draws_launch(int kind, const u8* kprev, const u8* knext, u64 base, u6
     if (!n) return;
     AesKey kp = expand_key(kprev), kn = expand_key(knext);
     u64 counters = ((base + n - 1) >> 1) - (base >> 1) + 1;
-    launch(family, k_share_draws, dim3(aes_grid(counters, kBlock)), dim3(kBlock), kAesLds, s, aes_table(), kp, kn,
+    launch(family, k_share_draws, dim3(aes_grid(counters, kBlock)), dim3(kBlock), 0, s, aes_table(), kp, kn,
            kind, base, n, addend, out0, out1);
 }
 
@@ -233,7 +233,7 @@ int aby3g_aes_ctr(const uint8_t key[16], uint64_t ctr_base, uint64_t nblocks, vo
     return guarded([&] {
         if (!nblocks) return;
         AesKey k = expand_key(key);
-        launch(PROBE_AES, k_aes_ctr, dim3(aes_grid(nblocks, kBlock)), dim3(kBlock), kAesLds, S(stream), aes_table(),
+        launch(PROBE_AES, k_aes_ctr, dim3(aes_grid(nblocks, kBlock)), dim3(kBlock), 0, S(stream), aes_table(),
                k, ctr_base, nblocks, (u64*)out);
     });
 }
@@ -245,7 +245,7 @@ int aby3g_prng_fill(const uint8_t seed[16], uint64_t byte_off, uint64_t nbytes, 
         AesKey k = expand_key(seed);
         u64 w0 = byte_off / 8, n = nbytes / 8;
         u64 counters = ((w0 + n - 1) >> 1) - (w0 >> 1) + 1;
-        launch(PROBE_AES, k_prng_words, dim3(aes_grid(counters, kBlock)), dim3(kBlock), kAesLds, S(stream),
+        launch(PROBE_AES, k_prng_words, dim3(aes_grid(counters, kBlock)), dim3(kBlock), 0, S(stream),
                aes_table(), k, w0, n, (u64*)out);
     });
 }
@@ -273,7 +273,7 @@ int aby3g_bitmul_p0(const int64_t* A, const int64_t* B, uint64_t n, const aby3g_
         if (!n) return;
         AesKey kp = expand_key(prev->seed), kn = expand_key(next->seed), ko = expand_key(ot_key);
         u32 grid = aes_grid((n + 255) / 256, 1);
-        launch(PROBE_AES, k_bitmul_p0, dim3(grid), dim3(kBlock), kAesLds, S(stream), aes_table(), A, A + n, B, B + n,
+        launch(PROBE_AES, k_bitmul_p0, dim3(grid), dim3(kBlock), 0, S(stream), aes_table(), A, A + n, B, B + n,
                n, kp, prev->off / 8, kn, next->off / 8, ko, ot_ctr, C, C + n, send_msgs, help_msgs);
     });
 }
@@ -287,7 +287,7 @@ int aby3g_bitmul_p2(const int64_t* A, const int64_t* B, uint64_t n, const aby3g_
         if (!n) return;
         AesKey kn = expand_key(next->seed), ko = expand_key(ot_key);
         u32 grid = aes_grid((n + 255) / 256, 1);
-        launch(PROBE_AES, k_bitmul_p2, dim3(grid), dim3(kBlock), kAesLds, S(stream), aes_table(), A + n, B, B + n, n,
+        launch(PROBE_AES, k_bitmul_p2, dim3(grid), dim3(kBlock), 0, S(stream), aes_table(), A + n, B, B + n, n,
                kn, next->off / 8, ko, ot_ctr, C, help_msgs, send_msgs);
     });
 }
@@ -309,7 +309,7 @@ int aby3g_pubmul_p0(int64_t a, const int64_t* B, uint64_t n, const aby3g_zero_sh
         if (!n) return;
         AesKey kp = expand_key(zs->k_prev), kn = expand_key(zs->k_next);
         AesKey kon = expand_key(ot_next_key), kop = expand_key(ot_prev_key);
-        launch(PROBE_AES, k_pubmul_p0, dim3(aes_grid(n, kBlock)), dim3(kBlock), kAesLds, S(stream), aes_table(), a, B,
+        launch(PROBE_AES, k_pubmul_p0, dim3(aes_grid(n, kBlock)), dim3(kBlock), 0, S(stream), aes_table(), a, B,
                B + n, n, kp, kn, zs->draw_base, kon, ctr_next, kop, ctr_prev, msgs_next, msgs_prev);
     });
 }
@@ -320,7 +320,7 @@ int aby3g_pubmul_helper(const int64_t* choice_src, uint64_t n, const aby3g_zero_
         ABY3G_REQUIRE(zs != nullptr, "null zero-share keys");
         if (!n) return;
         AesKey kp = expand_key(zs->k_prev), kn = expand_key(zs->k_next), ko = expand_key(ot_key);
-        launch(PROBE_AES, k_pubmul_helper, dim3(aes_grid(n, kBlock)), dim3(kBlock), kAesLds, S(stream), aes_table(),
+        launch(PROBE_AES, k_pubmul_helper, dim3(aes_grid(n, kBlock)), dim3(kBlock), 0, S(stream), aes_table(),
                choice_src, n, kp, kn, zs->draw_base, ko, ctr, share_out, help_msgs);
     });
 }

@@ -237,7 +237,10 @@ int aby3g_aes_block_host(const uint8_t key[16], uint64_t ctr, uint8_t out[16]) {
     return guarded([&] {
         static std::vector<u32> rep = [] {
             std::vector<u32> r(kAesLdsWords);
-            for (int i = 0; i < kAesLdsWords; ++i) r[i] = tables().T0[i >> 5];
+            for (int i = 0; i < kAesLdsWords; ++i) {
+                const u32 v = tables().T0[i >> 6];
+                r[i] = (i & 32) ? rotl(v, 8) : v;
+            }
             return r;
         }();
         AesKey k = expand_key(key);

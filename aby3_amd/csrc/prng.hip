@@ -14,7 +14,7 @@ namespace {
 constexpr u32 kBlock = kEpiBlock;
 constexpr u32 kWin = kEpiWin;
 
-__global__ void __launch_bounds__(kBlock) k_aes_ctr(const u32* __restrict__ T0g, AesKey k, u64 base, u64 n,
+__global__ void __launch_bounds__(kBlock, 4) k_aes_ctr(const u32* __restrict__ T0g, AesKey k, u64 base, u64 n,
                                                     u64* __restrict__ out) {
     __shared__ u32 lds[kAesLdsWords];  // static: lookups fold the table base into ds_read's offset
     aes_fill_lds(lds, T0g);
@@ -35,7 +35,7 @@ __global__ void __launch_bounds__(kBlock) k_aes_ctr(const u32* __restrict__ T0g,
 }
 
 // out[i] = stream word (w0 + i), i < n
-__global__ void __launch_bounds__(kBlock) k_prng_words(const u32* __restrict__ T0g, AesKey k, u64 w0, u64 n,
+__global__ void __launch_bounds__(kBlock, 4) k_prng_words(const u32* __restrict__ T0g, AesKey k, u64 w0, u64 n,
                                                        u64* __restrict__ out) {
     __shared__ u32 lds[kAesLdsWords];  // static: lookups fold the table base into ds_read's offset
     aes_fill_lds(lds, T0g);
@@ -51,41 +51,41 @@ __global__ void __launch_bounds__(kBlock) k_prng_words(const u32* __restrict__ T
     }
 }
 
-// ShareGen draws (Sh3ShareGen.h:60-109): thread per counter c; draws 2c, 2c+1.
-__global__ void __launch_bounds__(kBlock) k_share_draws(const u32* __restrict__ T0g, AesKey kp, AesKey kn, int kind,
-                                                        u64 base, u64 n, const i64* __restrict__ addend,
-                                                        i64* __restrict__ out0, i64* __restrict__ out1) {
+// ShareGen draws (Sh3ShareGen.h:60-109): windows of kPairWin counters, both
+// keys' blocks staged in LDS (pair_windows; kk = (prev, next)), then one draw
+// per thread.
+__global__ void __launch_bounds__(kBlock, 4) k_share_draws(const u32* __restrict__ T0g, AesKeyPair kk, int kind,
+                                                           u64 base, u64 n, const i64* __restrict__ addend,
+                                                           i64* __restrict__ out0, i64* __restrict__ out1) {
     __shared__ u32 lds[kAesLdsWords];  // static: lookups fold the table base into ds_read's offset
     aes_fill_lds(lds, T0g);
-    const u32 lane32 = threadIdx.x & 31;
-    const u64 c_first = base >> 1, c_last = (base + n - 1) >> 1;
-    for (u64 c = c_first + (u64)blockIdx.x * blockDim.x + threadIdx.x; c <= c_last;
-         c += (u64)gridDim.x * blockDim.x) {
-        u64 p[2], q[2];
-        aes_ctr_block2(lds, lane32, kp, c, kn, c, p[0], p[1], q[0], q[1]);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            u64 j = 2 * c + h;
-            if (j < base || j - base >= n) continue;
-            u64 i = j - base;
-            if (kind == ABY3G_DRAW_ARITH) {
-                u64 v = p[h] - q[h];
-                if (addend) v += (u64)addend[i];
-                out0[i] = (i64)v;
-            } else if (kind == ABY3G_DRAW_BIN) {
-                u64 v = p[h] ^ q[h];
-                if (addend) v ^= (u64)addend[i];
-                out0[i] = (i64)v;
-            } else {
-                out0[i] = (i64)q[h];
-                out1[i] = (i64)p[h];
-            }
+    __shared__ u64 wp[2 * kPairWin], wn[2 * kPairWin];
+    const u64 c_first = base >> 1, nc = ((base + n - 1) >> 1) - c_first + 1;
+    for (u64 w0 = (u64)blockIdx.x * kPairWin; w0 < nc; w0 += (u64)gridDim.x * kPairWin) {
+        __syncthreads();
+        const u32 m = (u32)min((u64)kPairWin, nc - w0);
+        pair_windows(lds, kk, c_first + w0, m, c_first + w0, m, wp, wn);
+        __syncthreads();
+        const u64 j = 2 * (c_first + w0) + threadIdx.x;
+        if (j < base || j - base >= n) continue;
+        const u64 i = j - base, p = wp[threadIdx.x], q = wn[threadIdx.x];
+        if (kind == ABY3G_DRAW_ARITH) {
+            u64 v = p - q;
+            if (addend) v += (u64)addend[i];
+            out0[i] = (i64)v;
+        } else if (kind == ABY3G_DRAW_BIN) {
+            u64 v = p ^ q;
+            if (addend) v ^= (u64)addend[i];
+            out0[i] = (i64)v;
+        } else {
+            out0[i] = (i64)q;
+            out1[i] = (i64)p;
         }
     }
 }
 
 // --- 3-party OT multiplication, party 0 (Sh3Evaluator.cpp:132-163, SharedOT.cpp:6-94)
-__global__ void __launch_bounds__(kBlock) k_bitmul_p0(const u32* __restrict__ T0g, const i64* __restrict__ A0,
+__global__ void __launch_bounds__(kBlock, 4) k_bitmul_p0(const u32* __restrict__ T0g, const i64* __restrict__ A0,
                                                       const i64* __restrict__ A1, const i64* __restrict__ B0,
                                                       const i64* __restrict__ B1, u64 n, AesKey kprev, u64 pw0,
                                                       AesKey knext, u64 nw0, AesKey kot, u64 ctr,
@@ -123,7 +123,7 @@ __global__ void __launch_bounds__(kBlock) k_bitmul_p0(const u32* __restrict__ T0
 }
 
 // party 2 (Sh3Evaluator.cpp:202-240): help first, then send.
-__global__ void __launch_bounds__(kBlock) k_bitmul_p2(const u32* __restrict__ T0g, const i64* __restrict__ A1,
+__global__ void __launch_bounds__(kBlock, 4) k_bitmul_p2(const u32* __restrict__ T0g, const i64* __restrict__ A1,
                                                       const i64* __restrict__ B0, const i64* __restrict__ B1, u64 n,
                                                       AesKey knext, u64 nw0, AesKey kot, u64 ctr,
                                                       i64* __restrict__ C0, i64* __restrict__ help,
@@ -167,7 +167,7 @@ __global__ void k_ot_recv(const i64* __restrict__ msgs, const i64* __restrict__ 
 }
 
 // public a x shared bit, party 0 (Sh3Evaluator.cpp:430-447)
-__global__ void __launch_bounds__(kBlock) k_pubmul_p0(const u32* __restrict__ T0g, i64 a, const i64* __restrict__ B0,
+__global__ void __launch_bounds__(kBlock, 4) k_pubmul_p0(const u32* __restrict__ T0g, i64 a, const i64* __restrict__ B0,
                                                       const i64* __restrict__ B1, u64 n, AesKey kp, AesKey kn,
                                                       u64 dbase, AesKey kon, u64 ctrn, AesKey kop, u64 ctrp,
                                                       i64* __restrict__ mnext, i64* __restrict__ mprev) {
@@ -193,7 +193,7 @@ __global__ void __launch_bounds__(kBlock) k_pubmul_p0(const u32* __restrict__ T0
 }
 
 // parties 1/2 (Sh3Evaluator.cpp:452-487): share <- getShare(), help pads.
-__global__ void __launch_bounds__(kBlock) k_pubmul_helper(const u32* __restrict__ T0g, const i64* __restrict__ choice,
+__global__ void __launch_bounds__(kBlock, 4) k_pubmul_helper(const u32* __restrict__ T0g, const i64* __restrict__ choice,
                                                           u64 n, AesKey kp, AesKey kn, u64 dbase, AesKey kot, u64 ctr,
                                                           i64* __restrict__ share, i64* __restrict__ help) {
     __shared__ u32 lds[kAesLdsWords];  // static: lookups fold the table base into ds_read's offset
@@ -217,10 +217,10 @@ void share_draws_launch(int kind, const u8* kprev, const u8* knext, u64 base, u6
     ABY3G_REQUIRE(kind >= 0 && kind <= 2, "bad draw kind");
     ABY3G_REQUIRE(kind != ABY3G_DRAW_RANDPAIR || out1, "RANDPAIR needs out1");
     if (!n) return;
-    AesKey kp = expand_key(kprev), kn = expand_key(knext);
+    const AesKeyPair kk{{expand_key(kprev), expand_key(knext)}};
     u64 counters = ((base + n - 1) >> 1) - (base >> 1) + 1;
-    launch(family, k_share_draws, dim3(aes_grid(counters, kBlock)), dim3(kBlock), 0, s, aes_table(), kp, kn,
-           kind, base, n, addend, out0, out1);
+    launch(family, k_share_draws, dim3(aes_grid(counters, kPairWin)), dim3(kBlock), 0, s, aes_table(), kk, kind,
+           base, n, addend, out0, out1);
 }
 
 }  // namespace aby3g

@@ -19,6 +19,24 @@ typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
 constexpr u32 kGateBlock = 256;
 
+// 64 x 64 bit transpose across a wave: lane i holds row i (bit k = column k);
+// afterwards lane i holds column i (bit k = bit i of row k). Six butterfly
+// stages: at stage j the lanes i and i ^ j swap the off-diagonal j x j
+// blocks of their 2j x 2j block (one 64-bit lane exchange + masks each),
+// instead of 64 ballots.
+__device__ __forceinline__ u64 transpose64(u64 x, u32 lane) {
+    constexpr u64 kMask[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
+                              0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
+#pragma unroll
+    for (int st = 0; st < 6; ++st) {
+        const u32 j = 32u >> st;
+        const u64 m = kMask[st];
+        const u64 y = __shfl_xor(x, (int)j, 64);
+        x = (lane & j) ? ((x & ~m) | ((y & ~m) >> j)) : ((x & m) | ((y & m) << j));
+    }
+    return x;
+}
+
 __global__ void __launch_bounds__(kGateBlock) k_bin_gates(const aby3g_gate* __restrict__ gates, u64* __restrict__ mem,
                                                           u64 wires, u64 words, const u64* __restrict__ z,
                                                           u64* __restrict__ sendbuf) {
@@ -73,39 +91,47 @@ __global__ void __launch_bounds__(kGateBlock) k_bin_gates(const aby3g_gate* __re
 }
 
 // One whole communication level per launch. A workgroup owns 32 consecutive
-// words (2048 rows) of every wire; its 256 threads are 8 gate slots x 32
-// word lanes. It first unpacks the previous level's received AND shares
-// into share 1, then runs the level's gate batches in order, the 8 slots
-// striding over a batch's (independent) gates, with a workgroup barrier
+// words (2048 rows) of every wire; its threads are 8 (or, for launches of
+// few workgroups, 32) gate slots x 32 word lanes. It first unpacks the
+// previous level's received AND shares into share 1, then runs the level's
+// gate batches in order, the slots striding over a batch's (independent)
+// gates, with a workgroup barrier
 // between batches: a gate only ever reads words of its own rows, so the
 // per-workgroup barrier orders every dependency of the level.
 constexpr u32 kLevelWords = 32;
 
-__device__ __forceinline__ void gate_word(const aby3g_gate& g, u64* s0, u64* s1, u64 words, u64 w,
-                                          const u64* __restrict__ z, u64* __restrict__ sendbuf) {
-    const u64 x0 = s0[g.in0 * words + w], x1 = s1[g.in0 * words + w];
+// Operands of one gate on one word, loaded ahead of its evaluation so that a
+// slot can have several independent gates' loads in flight.
+struct GateOps {
+    u64 x0, x1, y0, y1, z;
+};
+
+__device__ __forceinline__ bool gate_is_and(u32 t) {
+    return t == ABY3G_GATE_AND || t == ABY3G_GATE_OR || t == ABY3G_GATE_NOR || t == ABY3G_GATE_NA_AND;
+}
+
+__device__ __forceinline__ void gate_load(const aby3g_gate& g, const u64* s0, const u64* s1, u64 words, u64 w,
+                                          const u64* __restrict__ z, GateOps& o) {
+    // unary gates read in0 twice (in1 of an external gate list may be anything)
+    const bool unary = g.type == ABY3G_GATE_COPY || g.type == ABY3G_GATE_INV;
+    const u64 in1 = unary ? g.in0 : g.in1;
+    o.x0 = s0[g.in0 * words + w];
+    o.x1 = s1[g.in0 * words + w];
+    o.y0 = s0[in1 * words + w];
+    o.y1 = s1[in1 * words + w];
+    o.z = gate_is_and(g.type) ? z[(u64)g.z_row * words + w] : 0;
+}
+
+__device__ __forceinline__ void gate_eval(const aby3g_gate& g, const GateOps& o, u64* s0, u64* s1, u64 words, u64 w,
+                                          u64* __restrict__ sendbuf) {
+    const u64 x0 = o.x0, x1 = o.x1, y0 = o.y0, y1 = o.y1;
     u64 o0, o1;
     switch (g.type) {
-        case ABY3G_GATE_COPY:
-            o0 = x0;
-            o1 = x1;
-            break;
-        case ABY3G_GATE_INV:
-            o0 = ~x0;
-            o1 = ~x1;
-            break;
+        case ABY3G_GATE_COPY: o0 = x0; o1 = x1; break;
+        case ABY3G_GATE_INV: o0 = ~x0; o1 = ~x1; break;
+        case ABY3G_GATE_XOR: o0 = x0 ^ y0; o1 = x1 ^ y1; break;
+        case ABY3G_GATE_NXOR: o0 = ~(x0 ^ y0); o1 = ~(x1 ^ y1); break;
         default: {
-            const u64 y0 = s0[g.in1 * words + w], y1 = s1[g.in1 * words + w];
-            if (g.type == ABY3G_GATE_XOR) {
-                o0 = x0 ^ y0;
-                o1 = x1 ^ y1;
-                break;
-            }
-            if (g.type == ABY3G_GATE_NXOR) {
-                o0 = ~(x0 ^ y0);
-                o1 = ~(x1 ^ y1);
-                break;
-            }
             u64 r;
             if (g.type == ABY3G_GATE_AND)
                 r = (x0 & y0) ^ (x0 & y1) ^ (x1 & y0);
@@ -115,7 +141,7 @@ __device__ __forceinline__ void gate_word(const aby3g_gate& g, u64* s0, u64* s1,
                 r = (~x0 & ~y0) ^ (~x0 & ~y1) ^ (~x1 & ~y0);
             else /* NA_AND */
                 r = (~x0 & y0) ^ (~x0 & y1) ^ (~x1 & y0);
-            r ^= z[(u64)g.z_row * words + w];
+            r ^= o.z;
             s0[g.out * words + w] = r;
             sendbuf[(u64)g.send_row * words + w] = r;
             return;
@@ -125,21 +151,42 @@ __device__ __forceinline__ void gate_word(const aby3g_gate& g, u64* s0, u64* s1,
     s1[g.out * words + w] = o1;
 }
 
-__global__ void __launch_bounds__(256) k_bin_level(const aby3g_gate* __restrict__ gates,
-                                                   const u32* __restrict__ batch_ends, u32 nbatches,
-                                                   const u64* __restrict__ recv, const u32* __restrict__ unpack_wires,
-                                                   u32 nunpack, u64* __restrict__ mem, u64 wires, u64 words,
-                                                   const u64* __restrict__ z, u64* __restrict__ sendbuf) {
+// SLOTS gate slots x 32 word lanes. Each slot takes kLevelUnroll gates of a
+// batch per iteration, all their loads issued before any evaluation (the
+// gates of a batch are independent), so a batch of G gates costs about
+// G / (SLOTS * kLevelUnroll) dependent memory round trips -- the bound for the
+// few-workgroup launches of small row counts (LR: 256 rows, one workgroup).
+constexpr u32 kLevelUnroll = 4;
+template <u32 SLOTS>
+__global__ void __launch_bounds__(SLOTS * 32) k_bin_level(const aby3g_gate* __restrict__ gates,
+                                                         const u32* __restrict__ batch_ends, u32 nbatches,
+                                                         const u64* __restrict__ recv,
+                                                         const u32* __restrict__ unpack_wires, u32 nunpack,
+                                                         u64* __restrict__ mem, u64 wires, u64 words,
+                                                         const u64* __restrict__ z, u64* __restrict__ sendbuf) {
     const u32 lane = threadIdx.x & 31, slot = threadIdx.x >> 5;
     const u64 w = (u64)blockIdx.x * kLevelWords + lane;
     u64* s0 = mem;
     u64* s1 = mem + wires * words;
-    for (u32 j = slot; j < nunpack; j += 8) s1[(u64)unpack_wires[j] * words + w] = recv[(u64)j * words + w];
+#pragma unroll 4
+    for (u32 j = slot; j < nunpack; j += SLOTS) s1[(u64)unpack_wires[j] * words + w] = recv[(u64)j * words + w];
     u32 begin = 0;
     for (u32 b = 0; b < nbatches; ++b) {
         __syncthreads();
         const u32 end = batch_ends[b];
-        for (u32 gi = begin + slot; gi < end; gi += 8) gate_word(gates[gi], s0, s1, words, w, z, sendbuf);
+        for (u32 g0 = begin + slot; g0 < end; g0 += kLevelUnroll * SLOTS) {
+            aby3g_gate g[kLevelUnroll];
+            GateOps o[kLevelUnroll];
+#pragma unroll
+            for (u32 k = 0; k < kLevelUnroll; ++k)
+                if (g0 + k * SLOTS < end) g[k] = gates[g0 + k * SLOTS];
+#pragma unroll
+            for (u32 k = 0; k < kLevelUnroll; ++k)
+                if (g0 + k * SLOTS < end) gate_load(g[k], s0, s1, words, w, z, o[k]);
+#pragma unroll
+            for (u32 k = 0; k < kLevelUnroll; ++k)
+                if (g0 + k * SLOTS < end) gate_eval(g[k], o[k], s0, s1, words, w, sendbuf);
+        }
         begin = end;
     }
 }
@@ -155,7 +202,7 @@ __global__ void __launch_bounds__(kGateBlock) k_bin_unpack(const u64* __restrict
 }
 
 // One wave per (64-row word w, 64-bit column c): lane r holds row 64w + r;
-// the ballot of bit b over the wave is word w of wire b (LSB = row 64w).
+// after the wave transpose lane b holds word w of wire b (LSB = row 64w).
 // blockIdx.y = share: input share s at in + s * rows * cols64, its wire rows
 // at wrows + s * shareStride
 __global__ void __launch_bounds__(256) k_bits_to_wires(const i64* __restrict__ in, u64 rows, u64 cols64, u32 nbits,
@@ -169,12 +216,7 @@ __global__ void __launch_bounds__(256) k_bits_to_wires(const i64* __restrict__ i
     const u64 w = waveId % words, c = waveId / words;
     const u64 r = w * 64 + lane;
     const u64 v = r < rows ? (u64)in[r * cols64 + c] : 0;
-    u64 mine = 0;
-#pragma unroll 8
-    for (u32 b = 0; b < 64; ++b) {
-        const u64 m = __ballot((v >> b) & 1);
-        if (lane == b) mine = m;
-    }
+    const u64 mine = transpose64(v, lane);
     const u64 bit = c * 64 + lane;
     if (bit < nbits) wrows[bit * words + w] = mine;
 }
@@ -195,19 +237,14 @@ __global__ void __launch_bounds__(256) k_wires_to_bits(const u64* __restrict__ m
     const u64 w = waveId % rw, c = waveId / rw;
     const u64 bit = c * 64 + lane;
     const u64 v = bit < nbits ? mem[(u64)wires[bit] * words + w] : 0;
-    u64 mine = 0;
-#pragma unroll 8
-    for (u32 r = 0; r < 64; ++r) {
-        const u64 m = __ballot((v >> r) & 1);
-        if (lane == r) mine = m;
-    }
+    const u64 mine = transpose64(v, lane);
     const u64 row = w * 64 + lane;
     if (row < rows) out[row * cols + c] = (i64)mine;
 }
 
 // LDS-tiled transposes (the both-share entry points): a workgroup owns 64
 // consecutive words (4096 rows) of one 64-bit column. bits -> wires: each
-// wave bit-transposes 16 words by ballots into an LDS tile [bit][word], then
+// wave bit-transposes 16 words (transpose64) into an LDS tile [bit][word], then
 // the tile leaves as 64 contiguous 512-byte wire segments. wires -> bits:
 // the reverse, reading 512-byte wire segments into the tile.
 constexpr u32 kTileWords = 64;
@@ -222,7 +259,7 @@ __global__ void __launch_bounds__(256) k_bits_to_wires_tiled(const i64* __restri
     const u64 tilesPerCol = (words + kTileWords - 1) / kTileWords;
     const u64 c = blockIdx.x / tilesPerCol, w0 = (blockIdx.x % tilesPerCol) * kTileWords;
     const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // all 16 loads of this wave in flight before the first ballot
+    // all 16 loads of this wave in flight before the first transpose
     u64 vv[16];
 #pragma unroll
     for (u32 k = 0; k < 16; ++k) {
@@ -232,13 +269,7 @@ __global__ void __launch_bounds__(256) k_bits_to_wires_tiled(const i64* __restri
     }
     for (u32 k = 0; k < 16; ++k) {
         const u32 wl = wave * 16 + k;
-        const u64 v = vv[k];
-        u64 mine = 0;
-#pragma unroll 8
-        for (u32 b = 0; b < 64; ++b) {
-            const u64 m = __ballot((v >> b) & 1);
-            if (lane == b) mine = m;
-        }
+        const u64 mine = transpose64(vv[k], lane);
         tile[lane * kTilePitch + wl] = mine;
     }
     __syncthreads();
@@ -275,13 +306,7 @@ __global__ void __launch_bounds__(256) k_wires_to_bits_tiled(const u64* __restri
     const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (u32 k = 0; k < 16; ++k) {
         const u32 wl = wave * 16 + k;
-        const u64 v = tile[lane * kTilePitch + wl];
-        u64 mine = 0;
-#pragma unroll 8
-        for (u32 r = 0; r < 64; ++r) {
-            const u64 m = __ballot((v >> r) & 1);
-            if (lane == r) mine = m;
-        }
+        const u64 mine = transpose64(tile[lane * kTilePitch + wl], lane);
         const u64 row = (w0 + wl) * 64 + lane;
         if (w0 + wl < rw && row < rows) out[row * cols + c] = (i64)mine;
     }
@@ -311,8 +336,14 @@ int aby3g_bin_level(const aby3g_gate* gates, const uint32_t* batch_ends, uint32_
     return guarded([&] {
         ABY3G_REQUIRE(words % kLevelWords == 0, "words must be padded to a multiple of 32 (2048 rows)");
         if ((!nbatches && !nunpack) || !words) return;
-        launch(PROBE_BINARY, k_bin_level, dim3((u32)(words / kLevelWords)), dim3(256), 0, S(stream), gates, batch_ends,
-               nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf);
+        const u32 wgs = (u32)(words / kLevelWords);
+        // few workgroups (small row counts): 32 slots per workgroup for gate parallelism
+        if (wgs < 128)
+            launch(PROBE_BINARY, k_bin_level<32>, dim3(wgs), dim3(32 * 32), 0, S(stream), gates, batch_ends,
+                   nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf);
+        else
+            launch(PROBE_BINARY, k_bin_level<8>, dim3(wgs), dim3(8 * 32), 0, S(stream), gates, batch_ends, nbatches,
+                   recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf);
     });
 }
 

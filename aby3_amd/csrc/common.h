@@ -89,10 +89,20 @@ constexpr int kAesLdsWords = 256 * 64;
 
 __host__ __device__ __forceinline__ u32 rotl(u32 x, int r) { return __builtin_rotateleft32(x, r); }
 
+// One global load per thread, then 128 B of replicated copies from registers:
+// thread t covers entry x = t % 256 of table t / 256 (T1 = rotl(T0, 8)); a
+// loop of dependent global loads here would cost ~1 us per iteration.
 __device__ __forceinline__ void aes_fill_lds(u32* lds, const u32* __restrict__ T0g) {
-    for (int i = threadIdx.x; i < kAesLdsWords; i += blockDim.x) {
-        const u32 v = T0g[i >> 6];
-        lds[i] = (i & 32) ? rotl(v, 8) : v;
+    static_assert(kAesLdsWords == 256 * 64, "layout");
+    for (u32 t = threadIdx.x; t < 512; t += blockDim.x) {
+        const u32 x = t & 255, tab = t >> 8;
+        u32 v = T0g[x];
+        if (tab) v = rotl(v, 8);
+        typedef u32 v4u __attribute__((ext_vector_type(4)));
+        v4u* dst = reinterpret_cast<v4u*>(lds + (x << 6) + (tab << 5));
+        const v4u q = {v, v, v, v};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dst[i] = q;
     }
     __syncthreads();
 }

@@ -91,31 +91,6 @@ struct SrcSlabs {
         return v;
     }
 };
-// Small GEMM on the VALU (no digit split, no MFMA), for products too small
-// to fill the chip: element i = (m, n) is the K-long dot product of
-// [A0 | A1] row m and [[B0 + B1]; [B0]] column n, mod 2^64. Lets the whole
-// asyncMul round-1 (product + zero-share / truncation pair) be one launch.
-struct SrcSmallGemm {
-    const i64 *A0, *A1, *B0, *B1;
-    u64 K, N;
-    __device__ u64 operator()(u64 i) const {
-        const u64 m = i / N, n = i % N;
-        const i64* a0 = A0 + m * K;
-        const i64* a1 = A1 + m * K;
-        u64 acc = 0;
-        for (u64 k = 0; k < K; ++k) {
-            const u64 b0 = (u64)B0[k * N + n], b1 = (u64)B1[k * N + n];
-            acc += (u64)a0[k] * (b0 + b1) + (u64)a1[k] * b0;
-        }
-        return acc;
-    }
-};
-struct SrcSmallGemmMinus {
-    SrcSmallGemm g;
-    const i64* sub;
-    __device__ u64 operator()(u64 i) const { return g(i) - (u64)sub[i]; }
-};
-
 // GEMM product minus a subtrahend (z = product - R of the truncation pair).
 struct SrcSlabsMinus {
     const i64* P;

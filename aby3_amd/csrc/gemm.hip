@@ -49,9 +49,40 @@ inline u32 gemm_target_wgs() { return gemm_variant() == 'a' ? 512u : 256u; }
 
 inline u64 roundup(u64 x, u64 m) { return (x + m - 1) / m * m; }
 
-// GEMMs up to this many product terms run on the VALU in one fused kernel.
+// GEMMs up to this many product terms run on the VALU (k_small_gemm), with
+// no digit split and no MFMA; the epilogue then works in place on the product.
 constexpr u64 kSmallGemmTerms = 1ull << 23;
 inline bool small_gemm(u64 M, u64 K, u64 N) { return M * N * K <= kSmallGemmTerms; }
+
+// C0-part of the share product, out = [A0 | A1] . [[B0 + B1]; [B0]] mod 2^64,
+// one wave per output element: the lanes split the K terms and a butterfly
+// sums them, so an element costs K / 64 dependent load rounds, not K (the
+// small GEMMs of an LR iteration have 128-256 outputs of 128-256 terms).
+__global__ void __launch_bounds__(256) k_small_gemm(const i64* __restrict__ A0, const i64* __restrict__ A1,
+                                                    const i64* __restrict__ B0, const i64* __restrict__ B1, u64 M,
+                                                    u64 K, u64 N, i64* __restrict__ out) {
+    const u32 lane = threadIdx.x & 63;
+    const u64 n = M * N, waves = (u64)gridDim.x * (blockDim.x >> 6);
+    for (u64 i = (u64)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < n; i += waves) {
+        const u64 m = i / N, c = i % N;
+        const i64* a0 = A0 + m * K;
+        const i64* a1 = A1 + m * K;
+        u64 acc = 0;
+        for (u64 k = lane; k < K; k += 64) {
+            const u64 b0 = (u64)B0[k * N + c], b1 = (u64)B1[k * N + c];
+            acc += (u64)a0[k] * (b0 + b1) + (u64)a1[k] * b0;
+        }
+#pragma unroll
+        for (int o = 32; o; o >>= 1) acc += __shfl_xor(acc, o, 64);
+        if (lane == 0) out[i] = (i64)acc;
+    }
+}
+
+void run_small_gemm(const i64* A, const i64* B, u64 M, u64 K, u64 N, i64* out, hipStream_t s) {
+    const u64 n = M * N;
+    const u32 grid = (u32)std::min<u64>((n + 3) / 4, 2048);
+    launch(PROBE_EPILOGUE, k_small_gemm, dim3(grid), dim3(256), 0, s, A, A + M * K, B, B + K * N, M, K, N, out);
+}
 
 struct GemmPlan {
     u64 M, K, N;
@@ -468,11 +499,8 @@ int aby3g_mul_local(int mode, const int64_t* A, const int64_t* B, int64_t* C0, u
             return;
         }
         if (small_gemm(M, K, N)) {
-            SrcSmallGemm src{A, A + M * K, B, B + K * N, K, N};
-            if (zs)
-                launch_finish_zero_share(src, n, *zs, C0, S(stream));
-            else
-                launch_finish_plain(src, n, C0, S(stream));
+            run_small_gemm(A, B, M, K, N, C0, S(stream));
+            if (zs) launch_finish_zero_share(SrcSlabs{C0, 1, n}, n, *zs, C0, S(stream));
             return;
         }
         GemmPlan p = plan_gemm(M, K, N);
@@ -507,8 +535,8 @@ int aby3g_mul_trunc_local(int mode, const int64_t* A, const int64_t* B, uint64_t
             return;
         }
         if (small_gemm(M, K, N)) {
-            launch_finish_trunc(SrcSmallGemm{A, A + M * K, B, B + K * N, K, N}, *ts, n, d, nullptr, C, C + n, z,
-                                S(stream));
+            run_small_gemm(A, B, M, K, N, z, S(stream));  // product into z, then z -= r in place
+            launch_finish_trunc(SrcSlabs{z, 1, n}, *ts, n, d, nullptr, C, C + n, z, S(stream));
             return;
         }
         GemmPlan p = plan_gemm(M, K, N);
@@ -539,8 +567,9 @@ int aby3g_mul_sub_local(int mode, const int64_t* A, const int64_t* B, const int6
             return;
         }
         if (small_gemm(M, K, N)) {
+            run_small_gemm(A, B, M, K, N, out, S(stream));
             if (sub_ready) ABY3G_CHECK_HIP(hipStreamWaitEvent(S(stream), (hipEvent_t)sub_ready, 0));
-            launch_finish_plain(SrcSmallGemmMinus{{A, A + M * K, B, B + K * N, K, N}, sub}, n, out, S(stream));
+            launch_finish_plain(SrcSlabsMinus{out, 1, n, sub}, n, out, S(stream));
             return;
         }
         GemmPlan p = plan_gemm(M, K, N);

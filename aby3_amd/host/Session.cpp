@@ -341,12 +341,37 @@ struct Session {
     bool checkOk = true;
     std::vector<CommPkg> comms;
 
+    // Stream creation order. HIP maps streams onto GPU_MAX_HW_QUEUES hardware
+    // queues in creation order, so with the three parties on one device the
+    // order decides which streams share a queue. Parties create their
+    // streams in turn (party 0 first), main and auxiliary together.
+    std::mutex turnMu;
+    std::condition_variable turnCv;
+    int turnNext = 0;
+    template <class F>
+    void inTurn(int i, F&& f) {
+        std::unique_lock<std::mutex> lk(turnMu);
+        turnCv.wait(lk, [&] { return turnNext == i; });
+        try {
+            f();
+        } catch (...) {
+            ++turnNext;
+            turnCv.notify_all();
+            throw;
+        }
+        ++turnNext;
+        turnCv.notify_all();
+    }
+
     void worker(int i, int device, int probe) {
         PartyCtx p;
         u64 seen = 0;
         try {
             p.idx = i;
-            p.rt.init(i, comms[i], device);
+            inTurn(i, [&] {
+                p.rt.init(i, comms[i], device);
+                p.rt.gpu().aux();
+            });
             p.enc.init(i, toBlock(0, i), toBlock(0, (i + 1) % 3));
             p.eval.init(i, toBlock(1, i), toBlock(1, (i + 1) % 3));
             if (probe) GPU_CALL(aby3g_probe_enable_mask((u32)probe));

@@ -47,7 +47,7 @@ Gpu::~Gpu() {
     }
     mForkEv.reset();
     mAuxEv.reset();
-    if (mAux) aby3g_stream_destroy(mAux);
+    if (mAux && !mAuxAliased) aby3g_stream_destroy(mAux);
     aby3g_stream_destroy(mStream);
     if (t_current == this) t_current = nullptr;
 }
@@ -65,7 +65,10 @@ void Gpu::sync() {
 aby3g_stream Gpu::aux() {
     if (!mAux) {
         GPU_CALL(aby3g_set_device(mDevice));
-        GPU_CALL(aby3g_stream_create(&mAux));
+        if (mAuxAliased)
+            mAux = mStream;
+        else
+            GPU_CALL(aby3g_stream_create(&mAux));
         mForkEv = std::make_unique<Event>();
         mAuxEv = std::make_unique<Event>();
     }
@@ -74,8 +77,14 @@ aby3g_stream Gpu::aux() {
 
 void Gpu::forkAux() {
     aby3g_stream a = aux();
+    if (mAuxAliased) return;  // one stream: already in order
     mForkEv->record(mStream);
     GPU_CALL(aby3g_stream_wait_event(a, mForkEv->get()));
+}
+
+void Gpu::aliasAux() {
+    if (mAux && !mAuxAliased) throw std::runtime_error("Gpu::aliasAux after the auxiliary stream was created");
+    mAuxAliased = true;
 }
 
 aby3g_event Gpu::recordAux() {
@@ -84,7 +93,10 @@ aby3g_event Gpu::recordAux() {
     return mAuxEv->get();
 }
 
-void Gpu::joinAux() { GPU_CALL(aby3g_stream_wait_event(mStream, recordAux())); }
+void Gpu::joinAux() {
+    if (aux() == mStream) return;
+    GPU_CALL(aby3g_stream_wait_event(mStream, recordAux()));
+}
 
 void* Gpu::alloc(size_t bytes) {
     size_t cls = sizeClass(bytes);
@@ -164,6 +176,11 @@ void DeviceBuffer::reset(Gpu& gpu, size_t bytes) {
 
 void DeviceBuffer::fence(aby3g_stream s) {
     if (!mPtr) return;
+    if (mPool) {
+        // the owner's stream: the pool reuses blocks in that stream's order anyway
+        std::lock_guard<std::mutex> lk(mPool->mu);
+        if (mPool->stream == s) return;
+    }
     auto ev = std::make_unique<Event>();
     ev->record(s);
     std::lock_guard<std::mutex> lk(mFences->mu);

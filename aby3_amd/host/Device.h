@@ -55,6 +55,9 @@ public:
     void forkAux();             // aux waits for all work enqueued so far on the main stream
     aby3g_event recordAux();    // event: all work enqueued so far on aux
     void joinAux();             // main waits for all work enqueued so far on aux
+    // Make aux() the main stream itself (fork/join become no-ops in effect);
+    // for co-located parties, whose extra streams would share hardware queues.
+    void aliasAux();
 
     struct FreeBlock {
         void* ptr;
@@ -87,6 +90,7 @@ private:
     int mDevice;
     aby3g_stream mStream = nullptr;
     aby3g_stream mAux = nullptr;
+    bool mAuxAliased = false;  // aliasAux(): the auxiliary stream is the main stream
     std::unique_ptr<Event> mForkEv, mAuxEv;
     std::shared_ptr<Pool> mPool;
     std::mutex mAttachMu;

@@ -130,7 +130,7 @@ Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, const si64Matrix& A, const si64Matri
                     DeviceBuffer r(g, bytes);
                     g.forkAux();
                     GPU_CALL(aby3g_trunc_tuple(&ts, n, (unsigned)shift, r.as<i64>(), C.data(), g.aux()));
-                    aby3g_event rReady = g.recordAux();
+                    aby3g_event rReady = g.aux() == g.stream() ? nullptr : g.recordAux();
                     GPU_CALL(aby3g_mul_sub_local((int)mode, A.data(), B.data(), r.as<i64>(), rReady, z->as<i64>(), M,
                                                  K, N, ws, wsBytes, g.stream()));
                 }

@@ -162,7 +162,8 @@ class _Lib:
 
 
 JOB_MUL_TRUNC, JOB_MUL, JOB_MSB, JOB_LR, JOB_MERGE_LAYER = range(5)
-INFO = dict(mults_per_step=0, gemm_int8_ops=1, and_words=2, gate_words=3, gate_bytes=4, bytes_sent=5)
+INFO = dict(mults_per_step=0, gemm_int8_ops=1, and_words=2, gate_words=3, gate_bytes=4, bytes_sent=5,
+            host_enqueue_us=6, host_drain_us=7)
 
 _HOST_SIGS = {
     "aby3h_last_error": (c_char_p, []),
@@ -233,8 +234,8 @@ class Session:
         self.host.aby3h_session_probe_reset(self._h)
 
     def info(self) -> dict:
-        out = (c_double * 6)()
-        self.host.aby3h_session_info(self._h, out, 6)
+        out = (c_double * len(INFO))()
+        self.host.aby3h_session_info(self._h, out, len(INFO))
         return {k: out[v] for k, v in INFO.items()}
 
     def check(self) -> bool:

@@ -50,7 +50,9 @@ enum {
     ABY3H_INFO_GATE_WORDS = 3,        /* all gates x words per step */
     ABY3H_INFO_GATE_BYTES = 4,        /* algorithmic HBM bytes of the gate kernels per step */
     ABY3H_INFO_BYTES_SENT = 5,        /* bytes sent by party 0 per step */
-    ABY3H_INFO_COUNT = 6
+    ABY3H_INFO_HOST_ENQUEUE_US = 6,   /* last run: host time per step issuing work, max over parties */
+    ABY3H_INFO_HOST_DRAIN_US = 7,     /* last run: host wait for the streams to drain after the last step */
+    ABY3H_INFO_COUNT = 8
 };
 
 const char* aby3h_last_error(void);

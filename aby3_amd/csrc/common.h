@@ -2,6 +2,7 @@
 // and the device AES-128 used by every randomness kernel.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <chrono>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -31,8 +32,20 @@ struct Error {
         if (!(cond)) throw ::aby3g::Error{ABY3G_EINVAL, std::string(__func__) + ": " + (msg)};       \
     } while (0)
 
+// calling thread's time inside C-ABI calls (host overhead accounting)
+extern thread_local double t_api_us;
+extern thread_local u64 t_api_calls;
+struct ApiClock {
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    ~ApiClock() {
+        t_api_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        ++t_api_calls;
+    }
+};
+
 template <class F>
 int guarded(F&& f) {
+    ApiClock clock;
     try {
         f();
         return ABY3G_OK;

@@ -7,6 +7,9 @@
 
 namespace aby3g {
 
+thread_local double t_api_us = 0;
+thread_local u64 t_api_calls = 0;
+
 namespace {
 thread_local std::string t_err;
 
@@ -155,6 +158,14 @@ int aby3g_device_count(int* n) {
 }
 int aby3g_set_device(int device) {
     return guarded([&] { ABY3G_CHECK_HIP(hipSetDevice(device)); });
+}
+int aby3g_api_time(double* us, uint64_t* calls) {
+    *us = t_api_us;
+    *calls = t_api_calls;
+    return 0;
+}
+int aby3g_get_device(int* device) {
+    return guarded([&] { ABY3G_CHECK_HIP(hipGetDevice(device)); });
 }
 
 int aby3g_malloc(void** ptr, size_t bytes) {

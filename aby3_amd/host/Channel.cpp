@@ -1,4 +1,6 @@
 #include "Channel.h"
+#include <chrono>
+#include <atomic>
 #include <map>
 
 namespace aby3 {
@@ -23,6 +25,10 @@ struct Msg {
 };
 }  // namespace
 
+// how long a receive polls before it sleeps on the condition variable
+constexpr int kSpinUs = 500;
+thread_local double t_recvWaitUs = 0;
+
 struct Pipe {
     std::mutex mu;
     std::condition_variable cv;
@@ -40,13 +46,28 @@ struct Pipe {
             }
     }
 
+    std::atomic<u64> published{0};  // messages pushed so far (sendSeq, readable without the lock)
+
     void push(Msg&& m) {
         std::lock_guard<std::mutex> lk(mu);
         sent += m.bytes;
         msgs.emplace(sendSeq++, std::move(m));
+        published.store(sendSeq, std::memory_order_release);
         cv.notify_all();
     }
     Msg pop(u64 ticket) {
+        // The parties' threads hand messages to each other every protocol
+        // round; a condition-variable sleep costs a futex wake-up (tens of us)
+        // per round, so poll for a while first.
+        const auto t0 = std::chrono::steady_clock::now();
+        struct WaitClock {
+            std::chrono::steady_clock::time_point t0;
+            ~WaitClock() { t_recvWaitUs += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count(); }
+        } clock{t0};
+        while (published.load(std::memory_order_acquire) <= ticket &&
+               std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(kSpinUs)) {
+            for (int i = 0; i < 64; ++i) __builtin_ia32_pause();
+        }
         std::unique_lock<std::mutex> lk(mu);
         cv.wait(lk, [&] { return msgs.count(ticket) != 0; });
         Msg m = std::move(msgs[ticket]);
@@ -207,6 +228,8 @@ void Channel::resetStats() {
     if (mOut) mOut->sent = 0;
     if (mIn) mIn->received = 0;
 }
+
+double recvWaitUs() { return t_recvWaitUs; }
 
 std::vector<CommPkg> makeLocalRing() {
     // pipe[i][j]: messages from party i to party j

@@ -84,6 +84,9 @@ struct CommPkg {
     Channel mPrev, mNext;
 };
 
+// Host time this thread has spent inside receives waiting for messages (us).
+double recvWaitUs();
+
 // Three in-process parties connected in a ring: result[i].mNext talks to
 // party i+1, result[i].mPrev to party i-1.
 std::vector<CommPkg> makeLocalRing();

@@ -1,4 +1,7 @@
 #include "Device.h"
+#include <mutex>
+#include <vector>
+#include <map>
 
 namespace aby3 {
 
@@ -19,9 +22,49 @@ void gpuCheck(int rc, const char* what) {
     if (rc != 0) throw std::runtime_error(std::string(what) + ": " + aby3g_last_error());
 }
 
-Event::Event() { GPU_CALL(aby3g_event_create(&mEv)); }
+// Events are recycled: a protocol round creates several (message readiness,
+// buffer fences) and creating + destroying a HIP event costs two runtime
+// calls. An Event is only destroyed after every wait on it was enqueued, and
+// a wait refers to the record preceding it, so re-recording a recycled event
+// cannot affect earlier waits.
+namespace {
+struct EventCache {
+    std::mutex mu;
+    std::map<int, std::vector<aby3g_event>> free;  // per device
+};
+EventCache& eventCache() {
+    static EventCache* c = new EventCache;  // never destroyed: events may die during static teardown
+    return *c;
+}
+constexpr size_t kEventCacheMax = 4096;
+}  // namespace
+
+Event::Event() {
+    GPU_CALL(aby3g_get_device(&mDevice));
+    {
+        EventCache& c = eventCache();
+        std::lock_guard<std::mutex> lk(c.mu);
+        auto& v = c.free[mDevice];
+        if (!v.empty()) {
+            mEv = v.back();
+            v.pop_back();
+            return;
+        }
+    }
+    GPU_CALL(aby3g_event_create(&mEv));
+}
 Event::~Event() {
-    if (mEv) aby3g_event_destroy(mEv);
+    if (!mEv) return;
+    {
+        EventCache& c = eventCache();
+        std::lock_guard<std::mutex> lk(c.mu);
+        auto& v = c.free[mDevice];
+        if (v.size() < kEventCacheMax) {
+            v.push_back(mEv);
+            return;
+        }
+    }
+    aby3g_event_destroy(mEv);
 }
 void Event::record(aby3g_stream s) { GPU_CALL(aby3g_event_record(mEv, s)); }
 void Event::sync() { GPU_CALL(aby3g_event_sync(mEv)); }

@@ -28,6 +28,7 @@ public:
 
 private:
     aby3g_event mEv = nullptr;
+    int mDevice = 0;
 };
 
 // One party's device context. Allocations are cached per size class and

@@ -341,7 +341,8 @@ struct Session {
     int probeFamily = 0;
     bool checkOk = true;
     std::vector<CommPkg> comms;
-    double hostEnqueueUs[3] = {0, 0, 0}, hostDrainUs[3] = {0, 0, 0};
+    double hostEnqueueUs[3] = {0, 0, 0}, hostDrainUs[3] = {0, 0, 0}, hostRecvWaitUs[3] = {0, 0, 0};
+    double hostApiUs[3] = {0, 0, 0}, hostApiCalls[3] = {0, 0, 0};
     bool colocated = false;  // two or more parties on one device
 
     // Stream creation order. HIP maps streams onto GPU_MAX_HW_QUEUES hardware
@@ -408,7 +409,15 @@ struct Session {
                 if (!err.empty()) throw std::runtime_error("session failed earlier");
                 if (c == 1) {
                     const auto t0 = std::chrono::steady_clock::now();
+                    const double w0 = recvWaitUs();
+                    double a0 = 0, a1 = 0;
+                    uint64_t c0 = 0, c1 = 0;
+                    aby3g_api_time(&a0, &c0);
                     for (u64 s = 0; s < n; ++s) job->step(p);
+                    aby3g_api_time(&a1, &c1);
+                    hostRecvWaitUs[i] = n ? (recvWaitUs() - w0) / n : 0;
+                    hostApiUs[i] = n ? (a1 - a0) / n : 0;
+                    hostApiCalls[i] = n ? (double)(c1 - c0) / n : 0;
                     const auto t1 = std::chrono::steady_clock::now();
                     p.rt.gpu().sync();
                     const auto t2 = std::chrono::steady_clock::now();
@@ -542,6 +551,9 @@ int aby3h_session_info(aby3h_session* h, double* out, int n) {
     h->s.job->info(tmp);
     tmp[ABY3H_INFO_HOST_ENQUEUE_US] = *std::max_element(h->s.hostEnqueueUs, h->s.hostEnqueueUs + 3);
     tmp[ABY3H_INFO_HOST_DRAIN_US] = h->s.hostDrainUs[0];
+    tmp[ABY3H_INFO_HOST_RECV_WAIT_US] = h->s.hostRecvWaitUs[0];
+    tmp[ABY3H_INFO_HOST_API_US] = h->s.hostApiUs[0];
+    tmp[ABY3H_INFO_HOST_API_CALLS] = h->s.hostApiCalls[0];
     for (int i = 0; i < n && i < ABY3H_INFO_COUNT; ++i) out[i] = tmp[i];
     return 0;
 }

@@ -64,6 +64,8 @@ _SIGS = {
     "aby3g_version": (c_int, []),
     "aby3g_device_count": (c_int, [POINTER(c_int)]),
     "aby3g_set_device": (c_int, [c_int]),
+    "aby3g_get_device": (c_int, [POINTER(c_int)]),
+    "aby3g_api_time": (c_int, [POINTER(c_double), POINTER(c_uint64)]),
     "aby3g_malloc": (c_int, [POINTER(c_void_p), c_size_t]),
     "aby3g_free": (c_int, [c_void_p]),
     "aby3g_host_malloc": (c_int, [POINTER(c_void_p), c_size_t]),
@@ -163,7 +165,7 @@ class _Lib:
 
 JOB_MUL_TRUNC, JOB_MUL, JOB_MSB, JOB_LR, JOB_MERGE_LAYER = range(5)
 INFO = dict(mults_per_step=0, gemm_int8_ops=1, and_words=2, gate_words=3, gate_bytes=4, bytes_sent=5,
-            host_enqueue_us=6, host_drain_us=7)
+            host_enqueue_us=6, host_drain_us=7, host_recv_wait_us=8, host_api_us=9, host_api_calls=10)
 
 _HOST_SIGS = {
     "aby3h_last_error": (c_char_p, []),

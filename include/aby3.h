@@ -52,7 +52,10 @@ enum {
     ABY3H_INFO_BYTES_SENT = 5,        /* bytes sent by party 0 per step */
     ABY3H_INFO_HOST_ENQUEUE_US = 6,   /* last run: host time per step issuing work, max over parties */
     ABY3H_INFO_HOST_DRAIN_US = 7,     /* last run: host wait for the streams to drain after the last step */
-    ABY3H_INFO_COUNT = 8
+    ABY3H_INFO_HOST_RECV_WAIT_US = 8, /* last run: host time per step waiting for peers' messages (party 0) */
+    ABY3H_INFO_HOST_API_US = 9,       /* last run: host time per step inside aby3g_* calls (party 0) */
+    ABY3H_INFO_HOST_API_CALLS = 10,   /* last run: aby3g_* calls per step (party 0) */
+    ABY3H_INFO_COUNT = 11
 };
 
 const char* aby3h_last_error(void);

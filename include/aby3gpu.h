@@ -43,6 +43,9 @@ const char* aby3g_last_error(void);
 int aby3g_version(void);
 int aby3g_device_count(int* n);
 int aby3g_set_device(int device);
+int aby3g_get_device(int* device);
+/* Host time the calling thread has spent inside aby3g_* calls, and their number. */
+int aby3g_api_time(double* us, uint64_t* calls);
 
 /* Memory, streams and events. The host runtime reaches the GPU only through
  * this header. kind: 0 host->device, 1 device->host, 2 device->device,

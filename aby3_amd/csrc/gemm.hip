@@ -32,20 +32,18 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 constexpr u32 BN = 64, BK = 32;  // output tile width, K' per stage
 constexpr u32 kRec = 256;        // bytes per (row, stage) record
 
-// Share-GEMM kernel variant (ABY3G_GEMM_VARIANT, for A/B runs):
-//   'b' (default) 128 x 64 tiles, 8 waves, 2-deep ring, one workgroup per CU
-//   'c' as 'b' with the B fragments read first and MFMAs ordered by A plane
-//   'a' 64 x 64 tiles, 4 waves, 2-deep ring, two workgroups per CU
-//   'd' 64 x 64 tiles, 4 waves, 3-deep ring, one workgroup per CU
+// Share-GEMM kernel (ABY3G_GEMM_VARIANT, for A/B runs): default the
+// staggered 16x16x64 kernel (k_share_gemm16s); 'b' the 32x32x32 kernel
+// (k_share_gemm) it replaced.
 inline char gemm_variant() {
     static const char v = [] {
         const char* e = getenv("ABY3G_GEMM_VARIANT");
-        return (e && (e[0] == 'a' || e[0] == 'c' || e[0] == 'd')) ? e[0] : 'b';
+        return (e && e[0] == 'b') ? 'b' : 's';
     }();
     return v;
 }
-inline u32 gemm_tbm() { return (gemm_variant() == 'a' || gemm_variant() == 'd') ? 64u : 128u; }
-inline u32 gemm_target_wgs() { return gemm_variant() == 'a' ? 512u : 256u; }
+constexpr u32 TBM = 128;  // output tile height (8 waves of 32 x 32)
+inline u32 gemm_target_wgs() { return 256u; }
 
 inline u64 roundup(u64 x, u64 m) { return (x + m - 1) / m * m; }
 
@@ -98,7 +96,7 @@ GemmPlan plan_gemm(u64 M, u64 K, u64 N) {
     p.M = M;
     p.K = K;
     p.N = N;
-    p.tbm = gemm_tbm();
+    p.tbm = TBM;
     p.Mp = roundup(M ? M : 1, p.tbm);
     p.Np = roundup(N ? N : 1, BN);
     p.Kp = roundup(K ? K : 1, 16);
@@ -233,8 +231,9 @@ __device__ __forceinline__ TileCoord tile_of(u32 pid, u32 TM, u32 TN, u32 splits
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
 
-// One TBM x 64 output tile over the K' stages [s0, s1) of its split;
-// TBM / 32 x 2 waves, each a 32 x 32 tile with 8 digit-plane accumulators.
+// k_share_gemm ('b', the previous default): one 128 x 64 output tile over
+// the K' stages [s0, s1) of its split; 8 waves (two per SIMD), each a 32 x 32
+// tile with 8 digit-plane accumulators, v_mfma_i32_32x32x32_i8.
 //
 // Staging: LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction)
 // into an NBUF-deep ring of stages. The LDS image is lane-linear, so the bank
@@ -242,16 +241,17 @@ typedef __attribute__((address_space(1))) void glb_void;
 // SOURCE address. Stage i + NBUF - 1 is issued right after the barrier of
 // stage i; the wait is a counted vmcnt (the pieces of the later stages stay
 // in flight) and the barrier a raw s_barrier, so the DMA is not drained by
-// it. Variants: TBM 64 / NBUF 3 (4 waves, one per SIMD) and TBM 128 / NBUF 2
-// (8 waves, two per SIMD: a second wave to issue MFMAs while one waits).
+// it. Measured (4096^3, random digits): 49-52 % of the spec int8 peak, and
+// 58 % with the DMA removed -- its 32x32x32 MFMAs alone, fragments in
+// registers, sustain only 56 % on random operands (scripts/mfma_peak.hip).
 //
 // Epilogue: recombine the 8 planes in i64; one split -> out = product (-
 // sub), several -> the split's slab of P.
-template <u32 TBM, u32 NBUF, u32 OCC, bool PORD>
-__global__ void __launch_bounds__(TBM / 32 * 2 * 64, OCC)
+template <u32 NBUF>
+__global__ void __launch_bounds__(512, 1)
     k_share_gemm(const u8* __restrict__ Ad, const u8* __restrict__ Bd, u64 M, u64 N, u64 stagesTotal,
                  u64 stagesPerSplit, u32 TM, u32 TN, u32 splits, i64* __restrict__ P, const i64* __restrict__ sub) {
-    constexpr u32 kWaves = TBM / 32 * 2, kT = kWaves * 64;
+    constexpr u32 kWaves = 8, kT = 512;
     constexpr u32 kStageA = TBM * kRec, kStageB = BN * kRec, kStage = kStageA + kStageB;
     constexpr u32 kPiecesA = TBM / 4, kPieces = kPiecesA + BN / 4, kPerWave = kPieces / kWaves;
     static_assert(kPieces % kWaves == 0, "pieces must split evenly over waves");
@@ -318,34 +318,19 @@ __global__ void __launch_bounds__(TBM / 32 * 2 * 64, OCC)
         else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        if (i + NBUF - 1 < nst) issue(s0 + i + NBUF - 1, (buf + NBUF - 1) % NBUF);
         const u8* ls = lds + buf * kStage;
         v4i a[8], b[8];
-        if (PORD) {
-            // B planes first, then each A plane right before the MFMAs that use it,
-            // so the first MFMAs wait only for the reads they consume
+        if (i + NBUF - 1 < nst) issue(s0 + i + NBUF - 1, (buf + NBUF - 1) % NBUF);
 #pragma unroll
-            for (int q = 0; q < 8; ++q) b[q] = *reinterpret_cast<const v4i*>(ls + offRB[q]);
+        for (int p = 0; p < 8; ++p) {
+            a[p] = *reinterpret_cast<const v4i*>(ls + offRA[p]);
+            b[p] = *reinterpret_cast<const v4i*>(ls + offRB[p]);
+        }
 #pragma unroll
-            for (int p = 0; p < 8; ++p) a[p] = *reinterpret_cast<const v4i*>(ls + offRA[p]);
+        for (int s = 0; s < 8; ++s) {
 #pragma unroll
-            for (int p = 0; p < 8; ++p) {
-#pragma unroll
-                for (int q = 0; q + p < 8; ++q)
-                    acc[p + q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[p], b[q], acc[p + q], 0, 0, 0);
-            }
-        } else {
-#pragma unroll
-            for (int p = 0; p < 8; ++p) {
-                a[p] = *reinterpret_cast<const v4i*>(ls + offRA[p]);
-                b[p] = *reinterpret_cast<const v4i*>(ls + offRB[p]);
-            }
-#pragma unroll
-            for (int s = 0; s < 8; ++s) {
-#pragma unroll
-                for (int p = 0; p <= s; ++p)
-                    acc[s] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[p], b[s - p], acc[s], 0, 0, 0);
-            }
+            for (int p = 0; p <= s; ++p)
+                acc[s] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[p], b[s - p], acc[s], 0, 0, 0);
         }
         buf = buf + 1 == NBUF ? 0 : buf + 1;
     }
@@ -364,6 +349,167 @@ __global__ void __launch_bounds__(TBM / 32 * 2 * 64, OCC)
             dst[i] = (i64)v;
         }
     }
+}
+
+// k_share_gemm16s (default): the same 128 x 64 tile and records with
+// v_mfma_i32_16x16x64_i8, which sustains ~1.5x the int8 rate of the 32x32x32
+// form on gfx950 with random operands (scripts/mfma_peak.hip: 87 % vs 56 % of
+// the spec peak). Each wave's 32 x 32 tile is 2 x 2 16x16 blocks. One MFMA
+// sums TWO digit pairs of the same plane s over a 32-wide K' slice: its
+// 64-deep K is [plane P1 | plane P2] of the stage (lanes 0-31 read plane P1,
+// lanes 32-63 plane P2, each lane its 16-byte chunk of the record), so
+// A-pair e = planes (2e, 2e+1) times B-pair f = planes (f, f-1) adds
+// A_2e B_f + A_2e+1 B_f-1 into plane 2e + f. B-pair "0Z" is plane 0 with a
+// zero upper half, for the odd pair (A_s, B_0) of an even plane s. 20 MFMAs
+// per block and stage cover the 36 digit pairs (4 of them half-used).
+//
+// The two waves of each SIMD run half a stage apart. Waves 0-3 ("X") and 4-7
+// ("Y") alternate between a read phase (this stage's 24 fragments from LDS,
+// and 6 DMA pieces of the stage two ahead) and an MFMA phase (80 MFMAs),
+// separated by raw barriers; Y starts one phase late, so in every phase one
+// wave of each SIMD feeds the MFMA pipe while the other reads: the LDS reads
+// and DMA issue hide behind the other wave's MFMAs instead of stalling both.
+// 3-deep ring (144 KiB):
+//   X: phase 2s = read s + DMA s+2, phase 2s+1 = MFMA s
+//   Y: phase 2s+1 = read s + DMA s+2, phase 2s+2 = MFMA s
+// Stage s+2's buffer (that of s-1) was last read in phase 2s-1 (Y), retired
+// by Y's lgkmcnt(0) before barrier 2s. Stage s+1 is needed from phase 2s+2:
+// both groups retire their pieces of it (vmcnt(6): stage s+2's stay in
+// flight) before barrier 2s+2. Measured at 4096^3: MFMA pipe busy 85 % of
+// the shader clock, which under this load settles near 1.65 GHz (power).
+__global__ void __launch_bounds__(512, 1)
+    k_share_gemm16s(const u8* __restrict__ Ad, const u8* __restrict__ Bd, u64 M, u64 N, u64 stagesTotal,
+                    u64 stagesPerSplit, u32 TM, u32 TN, u32 splits, i64* __restrict__ P, const i64* __restrict__ sub) {
+    constexpr u32 NBUF = 3, kT = 512;
+    constexpr u32 kStageA = TBM * kRec, kStageB = BN * kRec, kStage = kStageA + kStageB;
+    constexpr u32 kPiecesA = TBM / 4, kPieces = kPiecesA + BN / 4, kPerWave = kPieces / 8;
+    __shared__ __attribute__((aligned(16))) u8 lds[NBUF * kStage];
+    const u32 tid = threadIdx.x, lane = tid & 63;
+    const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool Y = wave >= 4;
+    const TileCoord tc = tile_of(blockIdx.x, TM, TN, splits);
+    const u64 m0 = (u64)tc.tm * TBM, n0 = (u64)tc.tn * BN;
+    const u64 s0 = (u64)tc.split * stagesPerSplit;
+    const u64 s1 = min(stagesTotal, s0 + stagesPerSplit);
+    i64* dst = P + (splits > 1 ? (u64)tc.split * M * N : 0);
+    if (s0 >= s1) {
+        for (u32 i = tid; i < TBM * BN; i += kT) {
+            u64 m = m0 + i / BN, n = n0 + i % BN;
+            if (m < M && n < N) dst[m * N + n] = 0;
+        }
+        return;
+    }
+    const u32 nst = (u32)(s1 - s0);
+
+    const u32 lrow = lane >> 4, lslot = lane & 15;
+    const u8* src[kPerWave];
+    u32 ldsOff[kPerWave];
+#pragma unroll
+    for (u32 j = 0; j < kPerWave; ++j) {
+        const u32 q = wave * kPerWave + j;
+        const bool isA = q < kPiecesA;
+        const u32 r = 4 * (isA ? q : q - kPiecesA) + lrow;
+        const u32 g = lslot ^ (r & 15);
+        src[j] = (isA ? Ad + (m0 + r) * stagesTotal * kRec : Bd + (n0 + r) * stagesTotal * kRec) + g * 16;
+        ldsOff[j] = (isA ? 0 : kStageA) + 4 * (isA ? q : q - kPiecesA) * kRec;
+    }
+    auto issue = [&](u64 st, u32 b) {
+#pragma unroll
+        for (u32 j = 0; j < kPerWave; ++j)
+            __builtin_amdgcn_global_load_lds((glb_void*)(src[j] + st * kRec), (lds_void*)(lds + b * kStage + ldsOff[j]),
+                                             16, 0, 0);
+    };
+
+    v4i acc[8][2][2];
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[s][i][j] = v4i{0};
+
+    const u32 wr = (wave >> 1 & 1) * 32 + (wave >> 2) * 64, wc = (wave & 1) * 32;
+    const u32 r16 = lane & 15, g4 = lane >> 4, hi = g4 >> 1, hf = g4 & 1;
+    u32 offA[4][2], offB[8][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const u32 row = wr + 16 * i + r16;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) offA[e][i] = row * kRec + (((2 * (2 * e + hi) + hf) ^ r16) * 16);
+        const u32 col = wc + 16 * i + r16;
+#pragma unroll
+        for (int f = 0; f < 8; ++f) {
+            const u32 g = 2 * (f == 0 ? 0 : (hi ? f - 1 : f)) + hf;
+            offB[f][i] = kStageA + col * kRec + ((g ^ r16) * 16);
+        }
+    }
+    const bool zhalf = hi != 0;
+
+    {
+        issue(s0, 0);
+        issue(min(s0 + 1, s1 - 1), 1);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPerWave) : "memory");
+    }
+    __builtin_amdgcn_s_barrier();      // barrier 0: stage 0 visible
+    if (Y) __builtin_amdgcn_s_barrier();  // Y starts one phase late
+
+    u32 buf = 0;
+    for (u32 it = 0; it < nst; ++it) {
+        // ---- read phase: DMA of stage it + 2 into the free buffer, this stage's fragments
+        issue(min(s0 + it + 2, s1 - 1), buf == 0 ? 2 : buf - 1);
+        const u8* ls = lds + buf * kStage;
+        v4i a[4][2], b[8][2];
+#pragma unroll
+        for (int f = 0; f < 8; ++f)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) b[f][j] = *reinterpret_cast<const v4i*>(ls + offB[f][j]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) a[e][i] = *reinterpret_cast<const v4i*>(ls + offA[e][i]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (Y) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPerWave) : "memory");
+        __builtin_amdgcn_s_barrier();
+        // ---- MFMA phase
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            if (zhalf) b[0][j] = v4i{0};
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int f = 0; f + 2 * e < 8; ++f)
+                        acc[2 * e + f][i][j] =
+                            __builtin_amdgcn_mfma_i32_16x16x64_i8(a[e][i], b[f][j], acc[2 * e + f][i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        if (!Y) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPerWave) : "memory");
+        __builtin_amdgcn_s_barrier();
+        buf = buf == 2 ? 0 : buf + 1;
+    }
+    if (!Y) __builtin_amdgcn_s_barrier();  // equal barrier counts
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                u64 v = 0;
+#pragma unroll
+                for (int s = 0; s < 8; ++s) v += (u64)(i64)acc[s][i][j][r] << (8 * s);
+                const u64 m = m0 + wr + 16 * i + 4 * g4 + r;
+                const u64 n = n0 + wc + 16 * j + r16;
+                if (m < M && n < N) {
+                    const u64 x = m * N + n;
+                    if (sub) v -= (u64)sub[x];
+                    dst[x] = (i64)v;
+                }
+            }
 }
 
 // Share-GEMM launches on one device run one at a time, in issue order,
@@ -444,23 +590,12 @@ void run_gemm(const GemmPlan& p, const i64* A, const i64* B, const Workspace& w,
     const i64* sb = direct ? sub : nullptr;
     const dim3 grid(TM * TN * p.splits);
     const u64 sps = p.kPerSplit / BK;
-    switch (gemm_variant()) {
-        case 'a':
-            launch(PROBE_GEMM, k_share_gemm<64, 2, 2, false>, grid, dim3(256), 0, s, (const u8*)w.Ad, (const u8*)w.Bd,
-                   p.M, p.N, stages, sps, TM, TN, p.splits, dst, sb);
-            break;
-        case 'd':
-            launch(PROBE_GEMM, k_share_gemm<64, 3, 1, false>, grid, dim3(256), 0, s, (const u8*)w.Ad, (const u8*)w.Bd,
-                   p.M, p.N, stages, sps, TM, TN, p.splits, dst, sb);
-            break;
-        case 'c':
-            launch(PROBE_GEMM, k_share_gemm<128, 2, 1, true>, grid, dim3(512), 0, s, (const u8*)w.Ad, (const u8*)w.Bd,
-                   p.M, p.N, stages, sps, TM, TN, p.splits, dst, sb);
-            break;
-        default:
-            launch(PROBE_GEMM, k_share_gemm<128, 2, 1, false>, grid, dim3(512), 0, s, (const u8*)w.Ad,
-                   (const u8*)w.Bd, p.M, p.N, stages, sps, TM, TN, p.splits, dst, sb);
-    }
+    if (gemm_variant() == 'b')
+        launch(PROBE_GEMM, k_share_gemm<2>, grid, dim3(512), 0, s, (const u8*)w.Ad, (const u8*)w.Bd, p.M, p.N, stages,
+               sps, TM, TN, p.splits, dst, sb);
+    else
+        launch(PROBE_GEMM, k_share_gemm16s, grid, dim3(512), 0, s, (const u8*)w.Ad, (const u8*)w.Bd, p.M, p.N, stages,
+               sps, TM, TN, p.splits, dst, sb);
 }
 
 void check_ws(const GemmPlan& p, void* ws, size_t bytes) {

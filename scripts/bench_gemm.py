@@ -23,6 +23,19 @@ for (M, K, N) in sizes:
     for _ in range(5):
         L.mul_local(1, P(A), P(B), P(C0), M, K, N, None, P(ws), wsb, None)
     torch.cuda.synchronize()
+    # exact check of 64 sampled outputs: C0 = A0 (B0 + B1) + A1 B0 mod 2^64
+    import numpy as np
+    a = A.cpu().numpy().view(np.uint64).reshape(2, M, K)
+    b = B.cpu().numpy().view(np.uint64).reshape(2, K, N)
+    c = C0.cpu().numpy().view(np.uint64).reshape(M, N)
+    rs = np.random.default_rng(1)
+    bad = 0
+    with np.errstate(over="ignore"):
+        for _ in range(64):
+            m, n = int(rs.integers(M)), int(rs.integers(N))
+            exp = (a[0, m] * (b[0, :, n] + b[1, :, n]) + a[1, m] * b[0, :, n]).sum(dtype=np.uint64)
+            bad += int(exp != c[m, n])
+    print(f"{M}x{K}x{N}: sampled check {'ok' if bad == 0 else f'FAILED ({bad}/64)'}", flush=True)
     L.probe_enable(1)
     L.probe_reset()
     it = 20

@@ -12,9 +12,6 @@ namespace aby3g {
 constexpr u32 kEpiBlock = 512;
 // generic windows (OT kernels): 512 stream words
 constexpr u32 kEpiWin = 512;
-// truncation windows: 510 elements, so that each stream's words span at most
-// 256 AES counters -- one block per thread, half the workgroup per stream
-constexpr u32 kTruncWin = kEpiBlock - 2;
 
 // win[0 .. 2*nc) <- words of PRNG stream k covering stream words
 // [wbase, wbase + E); the word of element e is win[(wbase & 1) + e].
@@ -151,31 +148,52 @@ __global__ void __launch_bounds__(kEpiBlock, 4) k_finish_zero_share(const u32* _
 }
 
 // R = t0 >> 2, RT = (t0 >> (d+2), t1 >> (d+2)); z = src(i) - R when z != null.
+// t0 = word (nw0 + i) of the next stream, t1 = word (pw0 + i) of the prev
+// stream. No windows: a thread encrypts one counter c of ONE stream and emits
+// the elements of its two words 2c, 2c+1 (whatever the stream's parity), so
+// threads never exchange words and the grid-stride loop balances to a block.
+// Even waves run the next stream (R, RT0, z), odd waves the prev stream
+// (RT1): the key is wave-uniform, one schedule in SGPRs.
 template <class Src>
-__global__ void __launch_bounds__(kEpiBlock, 4) k_finish_trunc(const u32* __restrict__ T0g, Src src, AesKeyPair kk,
-                                                               u64 nw0, u64 pw0, u64 n, u32 d, i64* __restrict__ R,
+__global__ void __launch_bounds__(kEpiBlock) k_finish_trunc(const u32* __restrict__ T0g, Src src, AesKeyPair kk,
+                                                            u64 nw0, u64 pw0, u64 n, u32 d, i64* __restrict__ R,
                                                             i64* __restrict__ RT0, i64* __restrict__ RT1,
                                                             i64* __restrict__ z) {
     __shared__ u32 lds[kAesLdsWords];  // static: lookups fold the table base into ds_read's offset
     aes_fill_lds(lds, T0g);
-    __shared__ u64 wn[kTruncWin + 2], wp[kTruncWin + 2];
-    for (u64 e0 = (u64)blockIdx.x * kTruncWin; e0 < n; e0 += (u64)gridDim.x * kTruncWin) {
-        const u32 E = (u32)min((u64)kTruncWin, n - e0);
-        __syncthreads();
-        // kk = (next, prev); each stream's E words span at most kPairWin counters
-        const u64 cn = (nw0 + e0) >> 1, cp = (pw0 + e0) >> 1;
-        pair_windows(lds, kk, cn, (u32)(((nw0 + e0 + E - 1) >> 1) - cn + 1), cp,
-                     (u32)(((pw0 + e0 + E - 1) >> 1) - cp + 1), wn, wp);
-        __syncthreads();
-        const u32 on = (u32)((nw0 + e0) & 1), op = (u32)((pw0 + e0) & 1);
-        for (u32 e = threadIdx.x; e < E; e += blockDim.x) {
-            const i64 t0 = (i64)wn[on + e], t1 = (i64)wp[op + e];
-            const i64 r = t0 >> 2;
-            const u64 i = e0 + e;
-            if (R) R[i] = r;
-            if (z) z[i] = (i64)(src(i) - (u64)r);
-            RT0[i] = t0 >> (d + 2);
-            RT1[i] = t1 >> (d + 2);
+    const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), h = wave & 1, lane = threadIdx.x & 63;
+    u32 off = h * (u32)sizeof(AesKey);
+    asm volatile("" : "+s"(off));  // opaque: load only the selected schedule
+    const AesKey& k = *reinterpret_cast<const AesKey*>(reinterpret_cast<const char*>(&kk) + off);
+    const u64 w0 = h ? pw0 : nw0;
+    const u64 c_first = w0 >> 1, c_last = (w0 + n - 1) >> 1;
+    const u64 per = (u64)gridDim.x * (blockDim.x >> 1);  // threads per stream
+    // two counters per step (c, c + per), as k_aes_ctr
+    for (u64 c = c_first + ((u64)blockIdx.x * (blockDim.x >> 7) + (wave >> 1)) * 64 + lane; c <= c_last;
+         c += 2 * per) {
+        u64 w[4];
+        {
+            // interleaved: the two blocks' table reads overlap (latency-bound at small n)
+            const AesKey* ks[2] = {&k, &k};
+            const u64 ctr[2] = {c, c + per};
+            u64 lo[2], hi[2];
+            aes_ctr_blocks<2>(lds, threadIdx.x & 31, ks, ctr, lo, hi);
+            w[0] = lo[0], w[1] = hi[0], w[2] = lo[1], w[3] = hi[1];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const u64 j = 2 * (c + (q >> 1) * per) + (q & 1);
+            if (j < w0 || j - w0 >= n) continue;
+            const u64 i = j - w0;
+            const i64 t = (i64)w[q];
+            if (h) {
+                RT1[i] = t >> (d + 2);
+            } else {
+                const i64 r = t >> 2;
+                if (R) R[i] = r;
+                if (z) z[i] = (i64)(src(i) - (u64)r);
+                RT0[i] = t >> (d + 2);
+            }
         }
     }
 }
@@ -202,7 +220,7 @@ void launch_finish_trunc(Src src, const aby3g_trunc_streams& ts, u64 n, unsigned
     ABY3G_REQUIRE(d < 62, "shift too large");
     if (!n) return;
     const AesKeyPair kk{{expand_key(ts.next_seed), expand_key(ts.prev_seed)}};
-    u32 grid = aes_grid((n + kTruncWin - 1) / kTruncWin, 1);
+    u32 grid = aes_grid(n / 2 + 1, kEpiBlock / 2);
     launch(PROBE_EPILOGUE, k_finish_trunc<Src>, dim3(grid), dim3(kEpiBlock), 0, s, aes_table(), src, kk,
            ts.next_off / 8, ts.prev_off / 8, n, (u32)d, R, RT0, RT1, z);
 }

@@ -59,6 +59,7 @@ public:
     // Make aux() the main stream itself (fork/join become no-ops in effect);
     // for co-located parties, whose extra streams would share hardware queues.
     void aliasAux();
+    bool auxAliased() const { return mAuxAliased; }
 
     struct FreeBlock {
         void* ptr;

@@ -117,8 +117,12 @@ Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, const si64Matrix& A, const si64Matri
                 std::memcpy(ts.prev_seed, mShareGen.mPrevSeed.data(), 16);
                 ts.next_off = mShareGen.takeNext(8 * n);
                 ts.prev_off = mShareGen.takePrev(8 * n);
-                if (aby3g_mul_prefers_fused((int)mode, M, K, N)) {
-                    // small or element-wise: product, truncation pair and z in one launch
+                // One launch pass for the product's epilogue, the truncation pair
+                // and z when the product is small / element-wise, or when this
+                // party has no second stream (co-located parties: the share GEMM
+                // holds every CU's registers while it runs, so nothing would
+                // overlap it and the fused form saves the split-K slab pass).
+                if (aby3g_mul_prefers_fused((int)mode, M, K, N) || g.auxAliased()) {
                     GPU_CALL(aby3g_mul_trunc_local((int)mode, A.data(), B.data(), M, K, N, (unsigned)shift, &ts,
                                                    z->as<i64>(), C.data(), ws, wsBytes, g.stream()));
                 } else {

@@ -67,3 +67,9 @@ L.probe_enable(0)
 dig_bytes = 8 * (2 * M * K + 3 * K * N) + 16 * (M * K + K * N)
 print(f"mul_sub_local {M}^3: {wall:.1f} us/call; digits {res['digits']:.1f} us ({dig_bytes / res['digits'] * 1e-3:.0f} "
       f"GB/s), gemm {res['gemm']:.1f} us, slab pass {res['epi']:.1f} us", flush=True)
+
+key = (ctypes.c_uint8 * 16)(*range(16))
+for nb in (4096, 65536, n // 4, n, 8 * n):
+    o = torch.empty(2 * nb, dtype=torch.int64, device="cuda")
+    us = timed(lambda: L.aes_ctr(key, 0, nb, P(o), None))
+    print(f"aes_ctr {nb} blocks: {us:.1f} us, {nb / us * 1e-3:.1f} G blocks/s", flush=True)

@@ -99,7 +99,7 @@ GemmPlan plan_gemm(u64 M, u64 K, u64 N) {
     p.tbm = TBM;
     p.Mp = roundup(M ? M : 1, p.tbm);
     p.Np = roundup(N ? N : 1, BN);
-    p.Kp = roundup(K ? K : 1, 16);
+    p.Kp = roundup(K ? K : 1, 32);  // each half of K' a whole number of stages
     p.Kc = 2 * p.Kp;
     const u64 stages = p.Kc / BK;
     const u64 tiles = (p.Mp / p.tbm) * (p.Np / BN);
@@ -123,79 +123,118 @@ GemmPlan plan_gemm(u64 M, u64 K, u64 N) {
 // int8 whose bits are (byte p of y) ^ 0x80:  x = sum_p d_p 2^(8p) mod 2^64.
 constexpr u64 kDigitBias = 0x8080808080808080ull;
 
-// One launch builds both digit operands. A workgroup stages a 64 x 32 tile
-// of i64 (A: 64 rows x 32 K'; B': 32 K' x 64 columns, B0 + B1 summed for the
-// first half of K') in LDS with coalesced loads, then writes the tile's 64
-// records: 16 lanes per 256-byte record, lane (plane p, half h) packs digit
-// p of the 16 values of K' half h into one 16-byte store, so every record is
-// written by one contiguous 256-byte burst.
-constexpr u32 kDigitTile = 64;   // rows (A) or columns (B) per workgroup
-constexpr u32 kLdsPitch = 33;    // i64 per staged row: 32 + 1 pad (bank spread)
+// One launch builds both digit operands. K' = [first half | second half]
+// with Kp (a multiple of 32) per half, so a 32-wide slice st of the original K
+// yields record stage st of the first half and st + Kp/32 of the second:
+//   A-workgroup: 32 rows x 32 k of A0 and A1 -> 64 records
+//   B-workgroup: 32 k x 64 columns of B0, B1 -> 128 records (B0 + B1, B0)
+// so every input element is read once. A thread holds 4 consecutive k of one
+// row / column, forms the 8 digit-plane words of those 4 values with 16
+// v_perm_b32 (a 4 x 8 byte transpose), and writes them into the record image
+// in LDS (272-byte pitch: a ds_write_b32 pass of 32 lanes hits 32 banks on
+// the A side, 2-way on the B side); the images then leave as 16-byte chunks,
+// 16 lanes per 256-byte record.
+constexpr u32 kDigitPitch = 272;  // LDS bytes per record image (256 + 16)
+constexpr u32 kDigitRows = 32;    // A rows per A-workgroup
+constexpr u32 kDigitCols = 64;    // B columns per B-workgroup
+
+// digit-plane words of 4 values: word p = digit p of v0..v3, one byte each
+__device__ __forceinline__ void digit_words(const u64 (&v)[4], u32 (&w)[8]) {
+    u32 lo[4], hi[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const u64 y = v[i] + kDigitBias;
+        lo[i] = (u32)y;
+        hi[i] = (u32)(y >> 32);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const u32* q = h ? hi : lo;
+        const u32 t0 = __builtin_amdgcn_perm(q[1], q[0], 0x05010400u), t1 = __builtin_amdgcn_perm(q[1], q[0], 0x07030602u);
+        const u32 u0 = __builtin_amdgcn_perm(q[3], q[2], 0x05010400u), u1 = __builtin_amdgcn_perm(q[3], q[2], 0x07030602u);
+        w[4 * h + 0] = __builtin_amdgcn_perm(u0, t0, 0x05040100u) ^ 0x80808080u;
+        w[4 * h + 1] = __builtin_amdgcn_perm(u0, t0, 0x07060302u) ^ 0x80808080u;
+        w[4 * h + 2] = __builtin_amdgcn_perm(u1, t1, 0x05040100u) ^ 0x80808080u;
+        w[4 * h + 3] = __builtin_amdgcn_perm(u1, t1, 0x07060302u) ^ 0x80808080u;
+    }
+}
 
 __global__ void __launch_bounds__(256) k_digits(const i64* __restrict__ A0, const i64* __restrict__ A1,
                                                 const i64* __restrict__ B0, const i64* __restrict__ B1, u64 M,
-                                                u64 K, u64 N, u64 Kp, u64 aTiles, u64 stages, u8* __restrict__ Ad,
+                                                u64 K, u64 N, u64 S2, u64 aGroups, u64 stages, u8* __restrict__ Ad,
                                                 u8* __restrict__ Bd) {
-    __shared__ u64 tile[kDigitTile * kLdsPitch];  // [row or column][32 K'] + pad
+    __shared__ __attribute__((aligned(16))) u8 img[2 * kDigitCols * kDigitPitch];  // record images
     const u32 t = threadIdx.x;
-    const bool isA = blockIdx.x < aTiles;
-    const u64 tix = isA ? blockIdx.x : blockIdx.x - aTiles;
-    const u64 r0 = (tix / stages) * kDigitTile;  // first row (A) / column (B)
-    const u64 st = tix % stages;                 // 32-wide stage of K'
-    const u64 kc0 = st * BK;
+    const bool isA = blockIdx.x < aGroups;
+    const u64 g = isA ? blockIdx.x : blockIdx.x - aGroups;
+    const u64 st = g % S2, k0 = st * 32;
+    u32 nrec;
+    u8* out;
+    u64 r0;
     if (isA) {
+        // record (row, half) at image index 2 * row + half
+        r0 = (g / S2) * kDigitRows;
+        const u32 row = t >> 3, kq = t & 7;
+        const u64 m = r0 + row;
+        u64 v0[4], v1[4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const u32 q = t + 256 * j;
-            const u32 r = q >> 5, kk = q & 31;
-            const u64 m = r0 + r, kc = kc0 + kk;
-            u64 v = 0;
-            if (m < M) {
-                if (kc < Kp) {
-                    if (kc < K) v = (u64)A0[m * K + kc];
-                } else if (kc - Kp < K) {
-                    v = (u64)A1[m * K + (kc - Kp)];
-                }
-            }
-            tile[r * kLdsPitch + kk] = v;
+        for (int j = 0; j < 4; ++j) {
+            const u64 k = k0 + 4 * kq + j;
+            const bool in = m < M && k < K;
+            v0[j] = in ? (u64)A0[m * K + k] : 0;
+            v1[j] = in ? (u64)A1[m * K + k] : 0;
         }
+        u32 w0[8], w1[8];
+        digit_words(v0, w0);
+        digit_words(v1, w1);
+        u32* i0 = reinterpret_cast<u32*>(img + (2 * row) * kDigitPitch) + kq;
+        u32* i1 = reinterpret_cast<u32*>(img + (2 * row + 1) * kDigitPitch) + kq;
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            i0[8 * p] = w0[p];
+            i1[8 * p] = w1[p];
+        }
+        nrec = 2 * kDigitRows;
+        out = Ad;
     } else {
+        // record (column, half) at image index half * 64 + column
+        r0 = (g / S2) * kDigitCols;
+        const u32 col = t & 63;
+        const u64 n = r0 + col;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const u32 q = t + 256 * j;
-            const u32 kk = q >> 6, c = q & 63;
-            const u64 n = r0 + c, kc = kc0 + kk;
-            u64 v = 0;
-            if (n < N) {
-                if (kc < Kp) {
-                    if (kc < K) v = (u64)B0[kc * N + n] + (u64)B1[kc * N + n];
-                } else if (kc - Kp < K) {
-                    v = (u64)B0[(kc - Kp) * N + n];
-                }
+        for (int e = 0; e < 2; ++e) {
+            const u32 kq = (t >> 6) + 4 * e;
+            u64 vs[4], vb[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const u64 k = k0 + 4 * kq + j;
+                const bool in = n < N && k < K;
+                const u64 b0 = in ? (u64)B0[k * N + n] : 0, b1 = in ? (u64)B1[k * N + n] : 0;
+                vs[j] = b0 + b1;
+                vb[j] = b0;
             }
-            tile[c * kLdsPitch + kk] = v;
+            u32 ws[8], wb[8];
+            digit_words(vs, ws);
+            digit_words(vb, wb);
+            u32* i0 = reinterpret_cast<u32*>(img + col * kDigitPitch) + kq;
+            u32* i1 = reinterpret_cast<u32*>(img + (kDigitCols + col) * kDigitPitch) + kq;
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+                i0[8 * p] = ws[p];
+                i1[8 * p] = wb[p];
+            }
         }
+        nrec = 2 * kDigitCols;
+        out = Bd;
     }
     __syncthreads();
-    u8* out = isA ? Ad : Bd;
-    const u32 lane16 = t & 15, p = lane16 >> 1, h = lane16 & 1;
-#pragma unroll
-    for (int pass = 0; pass < 4; ++pass) {
-        const u32 r = pass * 16 + (t >> 4);  // record (row / column) within the tile
-        const u64* src = tile + r * kLdsPitch + 16 * h;
-        u32 w[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            u32 acc = 0;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const u64 y = src[4 * q + e] + kDigitBias;
-                acc |= ((u32)(y >> (8 * p)) & 0xffu) << (8 * e);
-            }
-            w[q] = acc ^ 0x80808080u;
-        }
-        u8* rec = out + ((r0 + r) * stages + st) * kRec + p * 32 + h * 16;
-        *reinterpret_cast<v4i*>(rec) = v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
+    // 16 chunks of 16 B per record; record (r, half) -> stage st + half * S2 of row / column r0 + r
+    for (u32 c = t; c < nrec * 16; c += blockDim.x) {
+        const u32 rec = c >> 4, ch = c & 15;
+        const u32 rr = isA ? rec >> 1 : rec & (kDigitCols - 1), half = isA ? rec & 1 : rec / kDigitCols;
+        const u64 r = r0 + rr, stg = st + half * S2;
+        const v4i x = *reinterpret_cast<const v4i*>(img + rec * kDigitPitch + ch * 16);
+        *reinterpret_cast<v4i*>(out + (r * stages + stg) * kRec + ch * 16) = x;
     }
 }
 
@@ -579,9 +618,10 @@ void run_gemm(const GemmPlan& p, const i64* A, const i64* B, const Workspace& w,
     const i64* B0 = B;
     const i64* B1 = B + p.K * p.N;
     const u64 stages = p.Kc / BK;
-    const u64 aTiles = (p.Mp / kDigitTile) * stages, bTiles = (p.Np / kDigitTile) * stages;
-    launch(PROBE_DIGITS, k_digits, dim3((u32)(aTiles + bTiles)), dim3(256), 0, s, A0, A1, B0, B1, p.M, p.K, p.N, p.Kp,
-           aTiles, stages, w.Ad, w.Bd);
+    const u64 S2 = p.Kp / 32;
+    const u64 aGroups = (p.Mp / kDigitRows) * S2, bGroups = (p.Np / kDigitCols) * S2;
+    launch(PROBE_DIGITS, k_digits, dim3((u32)(aGroups + bGroups)), dim3(256), 0, s, A0, A1, B0, B1, p.M, p.K, p.N, S2,
+           aGroups, stages, w.Ad, w.Bd);
     const u32 TM = (u32)(p.Mp / p.tbm), TN = (u32)(p.Np / BN);
     const bool direct = p.splits == 1 && out != nullptr;
     if (direct && sub && subReady) ABY3G_CHECK_HIP(hipStreamWaitEvent(s, subReady, 0));

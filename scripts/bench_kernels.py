@@ -64,7 +64,7 @@ for f, name in [(0, "gemm"), (1, "epi"), (5, "digits")]:
     L.dll.aby3g_probe_read(f, ctypes.byref(ms), ctypes.byref(cnt))
     res[name] = ms.value / it * 1e3
 L.probe_enable(0)
-dig_bytes = 8 * (2 * M * K + 3 * K * N) + 16 * (M * K + K * N)
+dig_bytes = 8 * (2 * M * K + 2 * K * N) + 16 * (M * K + K * N)
 print(f"mul_sub_local {M}^3: {wall:.1f} us/call; digits {res['digits']:.1f} us ({dig_bytes / res['digits'] * 1e-3:.0f} "
       f"GB/s), gemm {res['gemm']:.1f} us, slab pass {res['epi']:.1f} us", flush=True)
 

@@ -233,7 +233,7 @@ def main():
         },
         "roofline": {
             "bound": "mfma",
-            "kernel": "k_share_gemm (int8 MFMA 32x32x32, 36 digit-pair planes)",
+            "kernel": "k_share_gemm16s (int8 MFMA 16x16x64, 36 digit pairs as 20 two-pair MFMAs per block and stage)",
             "achieved": achieved_tops,
             "peak": PEAK_INT8_TOPS,
             "unit": "TFLOP/s",

@@ -53,7 +53,7 @@ def main():
                            "gfx950 FETCH_SIZE read-side correction x2")
     party_steps = 3 * a.steps
     if a.job == "mul":
-        g = kernels.get("k_share_gemm", {})
+        g = next((v for k, v in kernels.items() if k.startswith("k_share_gemm")), {})
         out["share_gemm"] = dict(config={"m": 1024, "k": 1024, "n": 1024},
                                  hbm_bytes_per_launch=g.get("hbm_bytes_per_launch"), launches=g.get("launches"))
     else:

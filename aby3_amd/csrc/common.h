@@ -239,4 +239,13 @@ inline u32 aes_grid(u64 items, u32 block) {
 
 inline hipStream_t S(aby3g_stream s) { return reinterpret_cast<hipStream_t>(s); }
 
+// The calling thread's current device as last set through aby3g_set_device
+// (queried from HIP once per thread otherwise). Threads that drive the
+// library switch devices only through aby3g_set_device.
+extern thread_local int t_device;
+int current_device();
+
+// device-to-device copy on the current device (runtime.hip)
+void launch_copy(void* dst, const void* src, size_t bytes, hipStream_t s);
+
 }  // namespace aby3g

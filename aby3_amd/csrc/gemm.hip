@@ -560,9 +560,7 @@ __global__ void __launch_bounds__(512, 1)
 class MfmaTurn {
 public:
     explicit MfmaTurn(hipStream_t s) : s_(s) {
-        int dev = 0;
-        ABY3G_CHECK_HIP(hipGetDevice(&dev));
-        dev_ = dev;
+        dev_ = current_device();
         mu().lock();
         hipEvent_t& last = events()[dev_];
         if (last) {

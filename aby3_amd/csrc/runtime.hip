@@ -95,6 +95,7 @@ std::map<int, u32*> g_tab_dev;
 }  // namespace
 
 void set_error(const std::string& msg) { t_err = msg; }
+thread_local int t_device = -1;
 
 void probe_begin(int family, hipStream_t s) {
     if (!t_probe.on || !((t_probe.mask >> family) & 1)) return;
@@ -131,9 +132,13 @@ AesKey expand_key(const u8 key[16]) {
     return k;
 }
 
+int current_device() {
+    if (t_device < 0) ABY3G_CHECK_HIP(hipGetDevice(&t_device));
+    return t_device;
+}
+
 const u32* aes_table() {
-    int dev = 0;
-    ABY3G_CHECK_HIP(hipGetDevice(&dev));
+    const int dev = current_device();
     std::lock_guard<std::mutex> lk(g_tab_mu);
     auto it = g_tab_dev.find(dev);
     if (it != g_tab_dev.end()) return it->second;
@@ -142,6 +147,27 @@ const u32* aes_table() {
     ABY3G_CHECK_HIP(hipMemcpy(p, tables().T0, sizeof(tables().T0), hipMemcpyHostToDevice));
     g_tab_dev[dev] = p;
     return p;
+}
+
+namespace {
+// dst[0, n) <- src[0, n) in 16-byte pieces (both 16-byte aligned), grid-stride
+__global__ void __launch_bounds__(256) k_copy16(uint4* __restrict__ dst, const uint4* __restrict__ src, u64 n) {
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) dst[i] = src[i];
+}
+__global__ void __launch_bounds__(256) k_copy1(u8* __restrict__ dst, const u8* __restrict__ src, u64 n) {
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) dst[i] = src[i];
+}
+}  // namespace
+
+void launch_copy(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (!bytes) return;
+    const bool aligned = (((uintptr_t)dst | (uintptr_t)src | bytes) & 15) == 0;
+    const u64 n = aligned ? bytes / 16 : bytes;
+    const u32 grid = (u32)std::min<u64>((n + 255) / 256, 2048);
+    if (aligned)
+        launch(PROBE_OTHER, k_copy16, dim3(grid), dim3(256), 0, s, (uint4*)dst, (const uint4*)src, n);
+    else
+        launch(PROBE_OTHER, k_copy1, dim3(grid), dim3(256), 0, s, (u8*)dst, (const u8*)src, n);
 }
 
 }  // namespace aby3g
@@ -157,7 +183,15 @@ int aby3g_device_count(int* n) {
     return guarded([&] { ABY3G_CHECK_HIP(hipGetDeviceCount(n)); });
 }
 int aby3g_set_device(int device) {
-    return guarded([&] { ABY3G_CHECK_HIP(hipSetDevice(device)); });
+    // hipSetDevice / hipGetDevice are not free (they serialise with the other
+    // threads' launches: 15-100 us per call measured with three party
+    // threads); the library remembers the device it last set on this thread
+    // and skips the call when it is unchanged
+    return guarded([&] {
+        if (t_device == device) return;
+        ABY3G_CHECK_HIP(hipSetDevice(device));
+        t_device = device;
+    });
 }
 int aby3g_api_time(double* us, uint64_t* calls) {
     *us = t_api_us;
@@ -165,7 +199,7 @@ int aby3g_api_time(double* us, uint64_t* calls) {
     return 0;
 }
 int aby3g_get_device(int* device) {
-    return guarded([&] { ABY3G_CHECK_HIP(hipGetDevice(device)); });
+    return guarded([&] { *device = current_device(); });
 }
 
 int aby3g_malloc(void** ptr, size_t bytes) {
@@ -190,6 +224,12 @@ int aby3g_memcpy(void* dst, const void* src, size_t bytes, int kind, aby3g_strea
                           : kind == 1 ? hipMemcpyDeviceToHost
                           : kind == 2 ? hipMemcpyDeviceToDevice
                                       : hipMemcpyDefault;
+        if (k == hipMemcpyDeviceToDevice) {
+            // device-to-device on the current device: one copy kernel, cheaper to
+            // issue than the runtime's blit path
+            launch_copy(dst, src, bytes, S(stream));
+            return;
+        }
         ABY3G_CHECK_HIP(hipMemcpyAsync(dst, src, bytes, k, S(stream)));
     });
 }

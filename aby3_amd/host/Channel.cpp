@@ -133,7 +133,8 @@ void RecvFuture::get() const {
         GPU_CALL(aby3g_set_device(g.device()));
         if (st.bytes) {
             GPU_CALL(aby3g_stream_wait_event(g.stream(), s->ready->get()));
-            GPU_CALL(aby3g_memcpy(st.dst, s->ptr, st.bytes, 3, g.stream()));
+            // same device: copy kernel; across devices: the runtime's peer copy
+            GPU_CALL(aby3g_memcpy(st.dst, s->ptr, st.bytes, s->device == g.device() ? 2 : 3, g.stream()));
         }
         if (!s->consumed) s->consumed = std::make_unique<Event>();
         s->consumed->record(g.stream());
@@ -207,7 +208,7 @@ void Channel::asyncSendDevice(const void* src, size_t bytes, Gpu& gpu) {
     GPU_CALL(aby3g_set_device(gpu.device()));
     Slot* s = mOut->acquire(bytes, gpu.device());
     if (s->consumedRecorded) GPU_CALL(aby3g_stream_wait_event(gpu.stream(), s->consumed->get()));
-    if (bytes) GPU_CALL(aby3g_memcpy(s->ptr, src, bytes, 3, gpu.stream()));
+    if (bytes) GPU_CALL(aby3g_memcpy(s->ptr, src, bytes, 2, gpu.stream()));  // staging slot on the sender's device
     s->ready->record(gpu.stream());
     Msg m;
     m.device = true;

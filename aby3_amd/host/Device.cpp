@@ -253,7 +253,8 @@ void toHost(void* dst, const void* src, size_t bytes, Gpu& gpu) {
     gpu.sync();
 }
 void d2d(void* dst, const void* src, size_t bytes, Gpu& gpu) {
-    GPU_CALL(aby3g_memcpy(dst, src, bytes, 3, gpu.stream()));
+    // both buffers are this party's (its device): the copy-kernel path
+    GPU_CALL(aby3g_memcpy(dst, src, bytes, 2, gpu.stream()));
 }
 
 }  // namespace aby3

@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--decimal", type=int, default=16)
     ap.add_argument("--binary-rows", type=int, default=1 << 20)
     ap.add_argument("--binary-steps", type=int, default=5)
+    ap.add_argument("--binary-cpu-rows", type=int, default=1 << 18, help="rows of the CPU baseline sample (C3)")
     ap.add_argument("--no-binary", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=10)
@@ -113,6 +114,23 @@ def timed(sess, steps, pg):
     t1 = time.perf_counter()
     barrier(pg)
     return allmax(pg, t1 - t0)
+
+
+def cpu_msb(nt, rows, reps):
+    """The oracle's 3-party fetch_msb on this host: evaluations per second
+    (cpu_baseline leg only)."""
+    import ctypes
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle as orc
+
+    args, keep = orc._cir_args(nt.circuit("int_comp_helper", 64))
+    f = orc.dll().orc_bench_fetch_msb
+    f.restype = ctypes.c_double
+    secs = f(*args, ctypes.c_uint64(rows), reps)
+    if secs < 0:
+        raise SystemExit("bench: oracle fetch_msb baseline failed: " + orc.dll().orc_last_error().decode())
+    return reps / secs
 
 
 def cpu_lr_ms(nt, iters):
@@ -272,7 +290,7 @@ def main():
             "and_words_per_step": binfo["and_words"],
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_bin_gates + k_bin_unpack",
+                "kernel": "k_bin_level (one launch per level: unpack of the received AND shares + the level's gate batches)",
                 "achieved": gbs,
                 "peak": PEAK_HBM_GBS,
                 "unit": "GB/s",
@@ -282,6 +300,18 @@ def main():
                 "bytes_per_step_per_party": binfo["gate_bytes"],
             },
         }
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_msb(nt, args.binary_cpu_rows, reps=1)
+            out["binary"]["cpu_baseline"] = {
+                "value": cpu * binfo["and_words"] * args.binary_cpu_rows / args.binary_rows,
+                "unit": "AND word-gates/s",
+                "cores": 1,
+                "kind": "port",
+                "sample": f"1 x cipher_gt over {args.binary_cpu_rows} rows: the oracle's 3-party fetch_msb "
+                          "(bit-sliced u64 gate loops, AES-NI z masks, reference Release flags), the three "
+                          "parties simulated in sequence on one thread, no network",
+            }
+            out["binary"]["speedup_vs_cpu_baseline"] = out["binary"]["value"] / out["binary"]["cpu_baseline"]["value"]
 
     if not args.no_extras:
         out["extras"] = extras(args, nt, dev, world, pg)

@@ -42,14 +42,19 @@ enum { ABY3G_OK = 0, ABY3G_EINVAL = 1, ABY3G_EHIP = 2, ABY3G_ENOMEM = 3 };
 const char* aby3g_last_error(void);
 int aby3g_version(void);
 int aby3g_device_count(int* n);
+/* The calling thread's current device. The library remembers the device
+ * each thread last set here (hipSetDevice / hipGetDevice serialise with other
+ * threads' launches), so a thread that drives the library switches devices
+ * only through aby3g_set_device. */
 int aby3g_set_device(int device);
 int aby3g_get_device(int* device);
 /* Host time the calling thread has spent inside aby3g_* calls, and their number. */
 int aby3g_api_time(double* us, uint64_t* calls);
 
 /* Memory, streams and events. The host runtime reaches the GPU only through
- * this header. kind: 0 host->device, 1 device->host, 2 device->device,
- * 3 let the runtime infer. */
+ * this header. kind: 0 host->device, 1 device->host, 2 device->device with
+ * both buffers readable / writable from the current device (a copy kernel),
+ * 3 let the runtime infer (also peer copies between devices). */
 int aby3g_malloc(void** ptr, size_t bytes);
 int aby3g_free(void* ptr);
 int aby3g_host_malloc(void** ptr, size_t bytes); /* pinned host memory */

@@ -331,6 +331,46 @@ double orc_bench_mul_trunc(int mode, uint64_t M, uint64_t K, uint64_t N, uint64_
 }
 
 
+// CPU baseline of cipher_gt / fetch_msb (bench.py binary cpu_baseline for C3,
+// BuildingBlocks.cpp:464-532): diff = B - A, the two-input binary resharing,
+// and the 64-bit MSB circuit evaluated by the three parties (bit-sliced u64
+// gate loops, AES-NI z masks, Sh3BinaryEvaluator.cpp:539-1464), simulated in
+// sequence on one thread (no network). Inputs: n random 62-bit pairs shared
+// by party 0 (untimed). Returns wall seconds for `reps` evaluations.
+double orc_bench_fetch_msb(uint32_t wires, const uint32_t* gates, uint64_t ngates, const uint32_t* levels,
+                           uint64_t nlevels, const uint32_t* inWires, const uint32_t* inSizes, uint64_t nin,
+                           const uint32_t* outWires, const uint32_t* outSizes, uint64_t nout, uint64_t n, int reps) {
+    try {
+        Circuit c = toCircuit(wires, gates, ngates, levels, nlevels, inWires, inSizes, nin, outWires, outSizes, nout);
+        auto enc = makeEncryptors(0);
+        auto ev = makeEvaluators(1);
+        Mat a(n, 1), b(n, 1);
+        u64 x = 88172645463325252ull;
+        for (u64 k = 0; k < n; ++k) {
+            x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+            a.v[k] = (i64)(x >> 2);
+            x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+            b.v[k] = (i64)(x >> 2);
+        }
+        Shared A = shareInt(enc, 0, a), B = shareInt(enc, 0, b);
+        auto t0 = std::chrono::steady_clock::now();
+        for (int r = 0; r < reps; ++r) {
+            Shared diff = A;
+            for (int p = 0; p < 3; ++p)
+                for (int s = 0; s < 2; ++s)
+                    for (u64 k = 0; k < n; ++k)
+                        diff[p].s[s].v[k] = (i64)((u64)B[p].s[s].v[k] - (u64)A[p].s[s].v[k]);
+            Shared res = fetchMsb(ev, c, diff);
+            if (res[0].s[0].v.empty()) throw std::runtime_error("empty result");
+        }
+        auto t1 = std::chrono::steady_clock::now();
+        return std::chrono::duration<double>(t1 - t0).count();
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
 // CPU baseline of one SGD_Logistic iteration (bench.py cpu_baseline for C4,
 // Regression.h:249-293): batch gather, xw = X_B w (GEMM + truncation D),
 // sigmoid piecewise (2 MSB circuits + OT products), err = f - Y_B,

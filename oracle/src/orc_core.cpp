@@ -350,6 +350,17 @@ static inline u64 gateLocal(u32 t, u64 a, u64 b) {
     }
 }
 
+// a[r] bit j <-> a[j] bit r (recursive block swaps, 6 x 32 steps)
+static void transpose64(u64* a) {
+    u64 m = 0x00000000FFFFFFFFull;
+    for (int j = 32; j; j >>= 1, m ^= m << j)
+        for (int k = 0; k < 64; k = ((k | j) + 1) & ~j) {
+            const u64 t = ((a[k] >> j) ^ a[k | j]) & m;
+            a[k] ^= t << j;
+            a[k | j] ^= t;
+        }
+}
+
 void evalLevel(const Circuit& cir, u64 gateBegin, u64 gateCount, u64 andBegin, std::vector<u64>& mem, u64 words,
                const std::vector<u64>& zFlat, std::vector<u64>& sendBuf) {
     // Gate formulas: Sh3BinaryEvaluator.cpp:700-1065. Gates of one level are
@@ -418,7 +429,8 @@ std::vector<Shared> evalCircuit(std::array<Party, 3>& ev, const Circuit& cir,
             z[p][2 * i] = bp[i].lo ^ bn[i].lo;
             z[p][2 * i + 1] = bp[i].hi ^ bn[i].hi;
         }
-        // setInput (:200-276): transpose rows x bits -> wire-major, zero pad
+        // setInput (:200-276): transpose rows x bits -> wire-major, zero pad;
+        // 64 x 64 bit blocks (as cryptoTools' transpose does it)
         mem[p].assign(2 * W * words, 0);
         for (size_t b = 0; b < cir.inputs.size(); ++b) {
             const SMat& in = (*inputs[b])[p];
@@ -426,13 +438,15 @@ std::vector<Shared> evalCircuit(std::array<Party, 3>& ev, const Circuit& cir,
             if (in.rows() != rows) throw std::runtime_error("input rows");
             if (in.cols() * 64 < wires.size()) throw std::runtime_error("input bits");
             for (int s = 0; s < 2; ++s)
-                for (size_t bit = 0; bit < wires.size(); ++bit) {
-                    u64* row = mem[p].data() + (s * W + wires[bit]) * words;
-                    for (u64 r = 0; r < rows; ++r) {
-                        u64 v = (u64)in.s[s].v[r * in.cols() + bit / 64];
-                        row[r / 64] |= ((v >> (bit % 64)) & 1ull) << (r % 64);
+                for (u64 rb = 0; rb * 64 < rows; ++rb)
+                    for (size_t c = 0; c * 64 < wires.size(); ++c) {
+                        u64 blk[64];
+                        for (u64 r = 0; r < 64; ++r)
+                            blk[r] = rb * 64 + r < rows ? (u64)in.s[s].v[(rb * 64 + r) * in.cols() + c] : 0;
+                        transpose64(blk);
+                        for (size_t j = 0; j < 64 && c * 64 + j < wires.size(); ++j)
+                            mem[p][(s * W + wires[c * 64 + j]) * words + rb] = blk[j];
                     }
-                }
         }
     }
 
@@ -466,13 +480,15 @@ std::vector<Shared> evalCircuit(std::array<Party, 3>& ev, const Circuit& cir,
         for (int p = 0; p < 3; ++p) {
             outs[o][p] = SMat(rows, cols);
             for (int s = 0; s < 2; ++s)
-                for (size_t bit = 0; bit < wires.size(); ++bit) {
-                    const u64* row = mem[p].data() + (s * W + wires[bit]) * words;
-                    for (u64 r = 0; r < rows; ++r) {
-                        u64 v = (row[r / 64] >> (r % 64)) & 1ull;
-                        outs[o][p].s[s].v[r * cols + bit / 64] |= (i64)(v << (bit % 64));
+                for (u64 rb = 0; rb * 64 < rows; ++rb)
+                    for (u64 c = 0; c < cols; ++c) {
+                        u64 blk[64];
+                        for (u64 j = 0; j < 64; ++j)
+                            blk[j] = c * 64 + j < wires.size() ? mem[p][(s * W + wires[c * 64 + j]) * words + rb] : 0;
+                        transpose64(blk);
+                        for (u64 r = 0; r < 64 && rb * 64 + r < rows; ++r)
+                            outs[o][p].s[s].v[(rb * 64 + r) * cols + c] = (i64)blk[r];
                     }
-                }
         }
     }
     return outs;

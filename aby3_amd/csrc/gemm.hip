@@ -551,15 +551,14 @@ __global__ void __launch_bounds__(512, 1)
             }
 }
 
-// Share-GEMM launches on one device run one at a time, in issue order,
-// whichever stream issues them: co-located parties' GEMMs all want the whole
-// chip's matrix cores, so overlapping them only stretches each launch, while
-// the parties' AES, copy and finalize kernels (VALU/LDS/HBM) keep running
-// beside whichever GEMM holds the turn. The turn is a device-wide event chain
-// (stream waits on the previous GEMM's completion event; no host sync).
+// Optional turn-taking of share-GEMM launches on one device (in issue order,
+// whichever stream issues them) through a device-wide event chain (stream
+// waits on the previous GEMM's completion event; no host sync). Measured
+// slower for co-located parties than letting their GEMMs overlap, so off.
 class MfmaTurn {
 public:
     explicit MfmaTurn(hipStream_t s) : s_(s) {
+        if (!enabled()) return;
         dev_ = current_device();
         mu().lock();
         hipEvent_t& last = events()[dev_];
@@ -572,6 +571,7 @@ public:
         }
     }
     ~MfmaTurn() {
+        if (!enabled()) return;
         hipEvent_t& last = events()[dev_];
         if (!last) (void)hipEventCreateWithFlags(&last, hipEventDisableTiming);
         if (last) (void)hipEventRecord(last, s_);
@@ -579,6 +579,16 @@ public:
     }
 
 private:
+    // off by default (ABY3G_MFMA_TURN=1 turns it on, for A/B runs): letting
+    // co-located parties' GEMMs overlap measured +6 % on C2 -- the next
+    // GEMM's workgroups fill the CUs that the previous one's tail frees
+    static bool enabled() {
+        static const bool on = [] {
+            const char* e = getenv("ABY3G_MFMA_TURN");
+            return e && e[0] == '1';
+        }();
+        return on;
+    }
     static std::mutex& mu() {
         static std::mutex m;
         return m;

@@ -105,7 +105,10 @@ def _mats(M, K, N, mode, seed):
 
 SHAPES = [(nt.MUL_HADAMARD, 128, 128, 128), (nt.MUL_HADAMARD, 7, 3, 3), (nt.MUL_GEMM, 10, 10, 10),
           (nt.MUL_GEMM, 33, 17, 65), (nt.MUL_GEMM, 256, 128, 1), (nt.MUL_GEMM, 128, 256, 1),
-          (nt.MUL_GEMM, 192, 512, 320), (nt.MUL_GEMM, 1024, 1024, 1024)]
+          (nt.MUL_GEMM, 192, 512, 320), (nt.MUL_GEMM, 1024, 1024, 1024),
+          # MFMA path with ragged edges (M, N off the 128 x 64 tile, K off 32),
+          # and a long K: 564 K'-stages over 32 split-K slabs
+          (nt.MUL_GEMM, 257, 200, 250), (nt.MUL_GEMM, 64, 9000, 64)]
 
 
 @pytest.mark.parametrize("mode,M,K,N", SHAPES)

@@ -141,6 +141,17 @@ __host__ __device__ __forceinline__ u32 xor3_uniform(u32 a, u32 b, u32 k) {
 #endif
 }
 
+// a ^ b ^ k in one VALU op with k in a VGPR (a key schedule held per lane)
+__host__ __device__ __forceinline__ u32 xor3_v(u32 a, u32 b, u32 k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    u32 r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(k));
+    return r;
+#else
+    return a ^ b ^ k;
+#endif
+}
+
 // S-box bytes of four T0 entries, packed little-endian: S[x] = byte 1 of T0[x]
 __host__ __device__ __forceinline__ u32 aes_sb4(u32 A, u32 B, u32 C, u32 D) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -207,6 +218,46 @@ __host__ __device__ __forceinline__ void aes_ctr_blocks(const u32* __restrict__ 
         hi[b] = (u64)o2 | ((u64)o3 << 32);
     }
 #undef ABY3G_TL
+}
+
+// A key schedule copied into VGPRs (44 per lane): a kernel that needs two
+// schedules in one wave keeps the second here instead of spilling SGPRs.
+struct AesKeyV {
+    u32 rk[44];
+};
+__device__ __forceinline__ AesKeyV key_to_vgprs(const AesKey& k) {
+    AesKeyV v;
+#pragma unroll
+    for (int i = 0; i < 44; ++i) asm volatile("v_mov_b32 %0, %1" : "=v"(v.rk[i]) : "s"(k.rk[i]));
+    return v;
+}
+
+// AES-128 CTR block as aes_ctr_blocks<1>, round keys from VGPRs
+__device__ __forceinline__ void aes_ctr_block_v(const u32* __restrict__ T, u32 lane32, const AesKeyV& k, u64 ctr,
+                                                u64& lo, u64& hi) {
+    const u8* Tb = reinterpret_cast<const u8*>(T);
+    const u32 L0 = lane32 << 2, L1 = L0 | 0x80u;
+#define ABY3G_TL(s, L, j) (*reinterpret_cast<const u32*>(Tb + aes_addr((s), (L), (j))))
+    u32 s0 = (u32)ctr ^ k.rk[0], s1 = (u32)(ctr >> 32) ^ k.rk[1], s2 = k.rk[2], s3 = k.rk[3];
+#pragma unroll
+    for (int r = 1; r < 10; ++r) {
+        const u32 t0 = xor3_v(ABY3G_TL(s0, L0, 0), ABY3G_TL(s1, L1, 1), k.rk[4 * r + 0]) ^
+                       rotl(ABY3G_TL(s2, L0, 2) ^ ABY3G_TL(s3, L1, 3), 16);
+        const u32 t1 = xor3_v(ABY3G_TL(s1, L0, 0), ABY3G_TL(s2, L1, 1), k.rk[4 * r + 1]) ^
+                       rotl(ABY3G_TL(s3, L0, 2) ^ ABY3G_TL(s0, L1, 3), 16);
+        const u32 t2 = xor3_v(ABY3G_TL(s2, L0, 0), ABY3G_TL(s3, L1, 1), k.rk[4 * r + 2]) ^
+                       rotl(ABY3G_TL(s0, L0, 2) ^ ABY3G_TL(s1, L1, 3), 16);
+        const u32 t3 = xor3_v(ABY3G_TL(s3, L0, 0), ABY3G_TL(s0, L1, 1), k.rk[4 * r + 3]) ^
+                       rotl(ABY3G_TL(s1, L0, 2) ^ ABY3G_TL(s2, L1, 3), 16);
+        s0 = t0, s1 = t1, s2 = t2, s3 = t3;
+    }
+    const u32 o0 = aes_sb4(ABY3G_TL(s0, L0, 0), ABY3G_TL(s1, L0, 1), ABY3G_TL(s2, L0, 2), ABY3G_TL(s3, L0, 3)) ^ k.rk[40];
+    const u32 o1 = aes_sb4(ABY3G_TL(s1, L0, 0), ABY3G_TL(s2, L0, 1), ABY3G_TL(s3, L0, 2), ABY3G_TL(s0, L0, 3)) ^ k.rk[41];
+    const u32 o2 = aes_sb4(ABY3G_TL(s2, L0, 0), ABY3G_TL(s3, L0, 1), ABY3G_TL(s0, L0, 2), ABY3G_TL(s1, L0, 3)) ^ k.rk[42];
+    const u32 o3 = aes_sb4(ABY3G_TL(s3, L0, 0), ABY3G_TL(s0, L0, 1), ABY3G_TL(s1, L0, 2), ABY3G_TL(s2, L0, 3)) ^ k.rk[43];
+#undef ABY3G_TL
+    lo = (u64)o0 | ((u64)o1 << 32);
+    hi = (u64)o2 | ((u64)o3 << 32);
 }
 
 __host__ __device__ __forceinline__ void aes_ctr_block(const u32* __restrict__ T, u32 lane32, const AesKey& k, u64 ctr,

@@ -51,35 +51,41 @@ __global__ void __launch_bounds__(kBlock, 4) k_prng_words(const u32* __restrict_
     }
 }
 
-// ShareGen draws (Sh3ShareGen.h:60-109): windows of kPairWin counters, both
-// keys' blocks staged in LDS (pair_windows; kk = (prev, next)), then one draw
-// per thread.
+// ShareGen draws (Sh3ShareGen.h:60-109). Draw j of either key is word j of
+// its AES-CTR stream, so a thread encrypts ONE counter c under both keys
+// (the prev schedule in SGPRs, the next one copied to VGPRs: two in SGPRs
+// spill) and emits draws 2c and 2c + 1 -- no LDS windows,
+// no barriers, and the grid-stride loop balances to one counter.
 __global__ void __launch_bounds__(kBlock, 4) k_share_draws(const u32* __restrict__ T0g, AesKeyPair kk, int kind,
                                                            u64 base, u64 n, const i64* __restrict__ addend,
                                                            i64* __restrict__ out0, i64* __restrict__ out1) {
     __shared__ u32 lds[kAesLdsWords];  // static: lookups fold the table base into ds_read's offset
     aes_fill_lds(lds, T0g);
-    __shared__ u64 wp[2 * kPairWin], wn[2 * kPairWin];
-    const u64 c_first = base >> 1, nc = ((base + n - 1) >> 1) - c_first + 1;
-    for (u64 w0 = (u64)blockIdx.x * kPairWin; w0 < nc; w0 += (u64)gridDim.x * kPairWin) {
-        __syncthreads();
-        const u32 m = (u32)min((u64)kPairWin, nc - w0);
-        pair_windows(lds, kk, c_first + w0, m, c_first + w0, m, wp, wn);
-        __syncthreads();
-        const u64 j = 2 * (c_first + w0) + threadIdx.x;
-        if (j < base || j - base >= n) continue;
-        const u64 i = j - base, p = wp[threadIdx.x], q = wn[threadIdx.x];
-        if (kind == ABY3G_DRAW_ARITH) {
-            u64 v = p - q;
-            if (addend) v += (u64)addend[i];
-            out0[i] = (i64)v;
-        } else if (kind == ABY3G_DRAW_BIN) {
-            u64 v = p ^ q;
-            if (addend) v ^= (u64)addend[i];
-            out0[i] = (i64)v;
-        } else {
-            out0[i] = (i64)q;
-            out1[i] = (i64)p;
+    const u32 lane32 = threadIdx.x & 31;
+    const AesKeyV kn = key_to_vgprs(kk.k[1]);
+    const u64 c_first = base >> 1, c_last = (base + n - 1) >> 1;
+    for (u64 c = c_first + (u64)blockIdx.x * blockDim.x + threadIdx.x; c <= c_last;
+         c += (u64)gridDim.x * blockDim.x) {
+        u64 p[2], q[2];
+        aes_ctr_block(lds, lane32, kk.k[0], c, p[0], p[1]);
+        aes_ctr_block_v(lds, lane32, kn, c, q[0], q[1]);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const u64 j = 2 * c + h;
+            if (j < base || j - base >= n) continue;
+            const u64 i = j - base;
+            if (kind == ABY3G_DRAW_ARITH) {
+                u64 v = p[h] - q[h];
+                if (addend) v += (u64)addend[i];
+                out0[i] = (i64)v;
+            } else if (kind == ABY3G_DRAW_BIN) {
+                u64 v = p[h] ^ q[h];
+                if (addend) v ^= (u64)addend[i];
+                out0[i] = (i64)v;
+            } else {
+                out0[i] = (i64)q[h];
+                out1[i] = (i64)p[h];
+            }
         }
     }
 }
@@ -219,8 +225,8 @@ void share_draws_launch(int kind, const u8* kprev, const u8* knext, u64 base, u6
     if (!n) return;
     const AesKeyPair kk{{expand_key(kprev), expand_key(knext)}};
     u64 counters = ((base + n - 1) >> 1) - (base >> 1) + 1;
-    launch(family, k_share_draws, dim3(aes_grid(counters, kPairWin)), dim3(kBlock), 0, s, aes_table(), kk, kind,
-           base, n, addend, out0, out1);
+    launch(family, k_share_draws, dim3(aes_grid(counters, kBlock)), dim3(kBlock), 0, s, aes_table(), kk, kind, base, n,
+           addend, out0, out1);
 }
 
 }  // namespace aby3g

@@ -73,3 +73,10 @@ for nb in (4096, 65536, n // 4, n, 8 * n):
     o = torch.empty(2 * nb, dtype=torch.int64, device="cuda")
     us = timed(lambda: L.aes_ctr(key, 0, nb, P(o), None))
     print(f"aes_ctr {nb} blocks: {us:.1f} us, {nb / us * 1e-3:.1f} G blocks/s", flush=True)
+
+kp = (ctypes.c_uint8 * 16)(*range(16))
+kn = (ctypes.c_uint8 * 16)(*range(1, 17))
+for nd in (2 * 491520 * 2, 8 * n):
+    o = torch.empty(nd, dtype=torch.int64, device="cuda")
+    us = timed(lambda: L.share_draws(nt.DRAW_BIN, kp, kn, 3, nd, None, P(o), None, None))
+    print(f"share_draws BIN {nd} draws: {us:.1f} us, {nd / us * 1e-3:.1f} G AES blocks/s (2 keys)", flush=True)

@@ -283,6 +283,21 @@ int aby3g_stream_wait_event(aby3g_stream stream, aby3g_event ev) {
 int aby3g_event_elapsed_ms(aby3g_event start, aby3g_event end, float* ms) {
     return guarded([&] { ABY3G_CHECK_HIP(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)end)); });
 }
+int aby3g_signal_alloc(uint64_t** word) {
+    return guarded([&] {
+        ABY3G_REQUIRE(word != nullptr, "null word");
+        ABY3G_CHECK_HIP(hipMalloc(word, sizeof(uint64_t)));
+        ABY3G_CHECK_HIP(hipMemset(*word, 0, sizeof(uint64_t)));
+        ABY3G_CHECK_HIP(hipDeviceSynchronize());
+    });
+}
+int aby3g_stream_write_value(aby3g_stream stream, uint64_t* word, uint64_t value) {
+    return guarded([&] { ABY3G_CHECK_HIP(hipStreamWriteValue64(S(stream), word, value, 0)); });
+}
+int aby3g_stream_wait_value(aby3g_stream stream, uint64_t* word, uint64_t value) {
+    return guarded(
+        [&] { ABY3G_CHECK_HIP(hipStreamWaitValue64(S(stream), word, value, hipStreamWaitValueGte, ~0ull)); });
+}
 
 int aby3g_aes_block_host(const uint8_t key[16], uint64_t ctr, uint8_t out[16]) {
     return guarded([&] {

@@ -22,6 +22,10 @@ struct Msg {
     size_t bytes = 0;
     std::shared_ptr<DeviceBuffer> shared;  // zero-copy payload
     std::shared_ptr<Event> ready;          // recorded on the sender's stream
+    // or, between parties on one device: the sender's stream writes sigValue
+    // to *sigWord when the payload is ready (cheaper than an event hand-off)
+    u64* sigWord = nullptr;
+    u64 sigValue = 0;
 };
 }  // namespace
 
@@ -36,6 +40,23 @@ struct Pipe {
     u64 sendSeq = 0, recvTicket = 0;
     std::vector<std::unique_ptr<Slot>> slots;
     u64 sent = 0, received = 0;
+    // sender and receiver on this device (-1: unknown / different): device
+    // payloads are then signalled through a stream-ordered word
+    int signalDevice = -1;
+    u64* word = nullptr;  // allocated by the sender on first use
+    u64 devSeq = 0;       // device payloads signalled so far (sender thread only)
+
+    // readiness of a device payload enqueued so far on `gpu`'s stream
+    void signalReady(Msg& m, Gpu& gpu, Event* fallback) {
+        if (signalDevice >= 0 && signalDevice == gpu.device()) {
+            if (!word) GPU_CALL(aby3g_signal_alloc(&word));
+            m.sigWord = word;
+            m.sigValue = ++devSeq;
+            GPU_CALL(aby3g_stream_write_value(gpu.stream(), word, m.sigValue));
+        } else {
+            fallback->record(gpu.stream());
+        }
+    }
 
     ~Pipe() {
         for (auto& s : slots)
@@ -44,6 +65,11 @@ struct Pipe {
                 aby3g_device_sync();
                 aby3g_free(s->ptr);
             }
+        if (word) {
+            aby3g_set_device(signalDevice);
+            aby3g_device_sync();
+            aby3g_free(word);
+        }
     }
 
     std::atomic<u64> published{0};  // messages pushed so far (sendSeq, readable without the lock)
@@ -132,7 +158,10 @@ void RecvFuture::get() const {
         Gpu& g = *st.gpu;
         GPU_CALL(aby3g_set_device(g.device()));
         if (st.bytes) {
-            GPU_CALL(aby3g_stream_wait_event(g.stream(), s->ready->get()));
+            if (m.sigWord)
+                GPU_CALL(aby3g_stream_wait_value(g.stream(), m.sigWord, m.sigValue));
+            else
+                GPU_CALL(aby3g_stream_wait_event(g.stream(), s->ready->get()));
             // same device: copy kernel; across devices: the runtime's peer copy
             GPU_CALL(aby3g_memcpy(st.dst, s->ptr, st.bytes, s->device == g.device() ? 2 : 3, g.stream()));
         }
@@ -155,7 +184,10 @@ std::shared_ptr<DeviceBuffer> RecvFuture::getShared() const {
         throw std::runtime_error("channel: message size mismatch (expected " + std::to_string(st.bytes) + ", got " +
                                  std::to_string(m.bytes) + ")");
     GPU_CALL(aby3g_set_device(st.gpu->device()));
-    GPU_CALL(aby3g_stream_wait_event(st.gpu->stream(), m.ready->get()));
+    if (m.sigWord)
+        GPU_CALL(aby3g_stream_wait_value(st.gpu->stream(), m.sigWord, m.sigValue));
+    else
+        GPU_CALL(aby3g_stream_wait_event(st.gpu->stream(), m.ready->get()));
     st.out = std::move(m.shared);
     st.done = true;
     return st.out;
@@ -169,8 +201,8 @@ void Channel::asyncSendShared(std::shared_ptr<DeviceBuffer> buf, size_t bytes, G
     m.device = true;
     m.bytes = bytes;
     m.shared = std::move(buf);
-    m.ready = std::make_shared<Event>();
-    m.ready->record(gpu.stream());
+    if (mOut->signalDevice != gpu.device()) m.ready = std::make_shared<Event>();
+    mOut->signalReady(m, gpu, m.ready.get());
     mOut->push(std::move(m));
 }
 
@@ -209,11 +241,11 @@ void Channel::asyncSendDevice(const void* src, size_t bytes, Gpu& gpu) {
     Slot* s = mOut->acquire(bytes, gpu.device());
     if (s->consumedRecorded) GPU_CALL(aby3g_stream_wait_event(gpu.stream(), s->consumed->get()));
     if (bytes) GPU_CALL(aby3g_memcpy(s->ptr, src, bytes, 2, gpu.stream()));  // staging slot on the sender's device
-    s->ready->record(gpu.stream());
     Msg m;
     m.device = true;
     m.slot = s;
     m.bytes = bytes;
+    mOut->signalReady(m, gpu, s->ready.get());
     mOut->push(std::move(m));
 }
 
@@ -232,12 +264,15 @@ void Channel::resetStats() {
 
 double recvWaitUs() { return t_recvWaitUs; }
 
-std::vector<CommPkg> makeLocalRing() {
+std::vector<CommPkg> makeLocalRing(const int* devices) {
     // pipe[i][j]: messages from party i to party j
     std::shared_ptr<Pipe> p[3][3];
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j)
-            if (i != j) p[i][j] = std::make_shared<Pipe>();
+            if (i != j) {
+                p[i][j] = std::make_shared<Pipe>();
+                if (devices && devices[i] == devices[j]) p[i][j]->signalDevice = devices[i];
+            }
     std::vector<CommPkg> c(3);
     for (int i = 0; i < 3; ++i) {
         int nx = (i + 1) % 3, pv = (i + 2) % 3;

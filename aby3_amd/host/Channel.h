@@ -88,7 +88,9 @@ struct CommPkg {
 double recvWaitUs();
 
 // Three in-process parties connected in a ring: result[i].mNext talks to
-// party i+1, result[i].mPrev to party i-1.
-std::vector<CommPkg> makeLocalRing();
+// party i+1, result[i].mPrev to party i-1. With `devices` (party i runs on
+// devices[i]), device payloads between parties on one device are signalled
+// through stream-ordered words instead of events.
+std::vector<CommPkg> makeLocalRing(const int* devices = nullptr);
 
 }  // namespace aby3

@@ -492,7 +492,12 @@ aby3h_session* aby3h_session_create(int job, const uint64_t* params, int nparams
             case ABY3H_JOB_MERGE_LAYER: s.job = std::make_unique<MergeLayerJob>(P(0, 1 << 20)); break;
             default: throw std::runtime_error("unknown job");
         }
-        s.comms = makeLocalRing();
+        {
+            int dv[3] = {0, 0, 0};
+            if (devices)
+                for (int i = 0; i < 3; ++i) dv[i] = devices[i];
+            s.comms = makeLocalRing(dv);
+        }
         s.colocated = !devices || devices[0] == devices[1] || devices[1] == devices[2] || devices[0] == devices[2];
         {
             std::unique_lock<std::mutex> lk(s.mu);

@@ -24,7 +24,8 @@ struct SimParty {
 };
 
 void run3(int device, const std::function<void(SimParty&)>& f) {
-    auto comms = makeLocalRing();
+    const int dv[3] = {device, device, device};
+    auto comms = makeLocalRing(dv);
     std::exception_ptr err[3];
     std::thread th[3];
     for (int i = 0; i < 3; ++i)

@@ -83,6 +83,9 @@ _SIGS = {
     "aby3g_event_sync": (c_int, [c_void_p]),
     "aby3g_stream_wait_event": (c_int, [c_void_p, c_void_p]),
     "aby3g_event_elapsed_ms": (c_int, [c_void_p, c_void_p, POINTER(c_float)]),
+    "aby3g_signal_alloc": (c_int, [POINTER(c_void_p)]),
+    "aby3g_stream_write_value": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "aby3g_stream_wait_value": (c_int, [c_void_p, c_void_p, c_uint64]),
     "aby3g_probe_enable": (c_int, [c_int]),
     "aby3g_probe_enable_mask": (c_int, [ctypes.c_uint32]),
     "aby3g_probe_read": (c_int, [c_int, POINTER(c_double), POINTER(c_uint64)]),

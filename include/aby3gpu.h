@@ -72,6 +72,14 @@ int aby3g_event_record(aby3g_event ev, aby3g_stream stream);
 int aby3g_event_sync(aby3g_event ev);
 int aby3g_stream_wait_event(aby3g_stream stream, aby3g_event ev);
 int aby3g_event_elapsed_ms(aby3g_event start, aby3g_event end, float* ms);
+/* Stream-ordered signal words (device memory, 8 bytes): `stream` writes
+ * `value` to *word once its earlier work is done / waits until *word >=
+ * value before its later work starts. A cross-stream hand-off on one device
+ * costs ~8 us this way against ~13.5 us for an event record + wait
+ * (scripts/pingpong.hip); the channels of co-located parties use it. */
+int aby3g_signal_alloc(uint64_t** word); /* zeroed, on the current device */
+int aby3g_stream_write_value(aby3g_stream stream, uint64_t* word, uint64_t value);
+int aby3g_stream_wait_value(aby3g_stream stream, uint64_t* word, uint64_t value);
 
 /* Kernel timing probe: when enabled, every kernel launched by this library on
  * the calling thread is bracketed by events; aby3g_probe_read() returns the

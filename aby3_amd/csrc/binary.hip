@@ -280,6 +280,46 @@ __global__ void __launch_bounds__(256) k_bits_to_wires_tiled(const i64* __restri
     }
 }
 
+// k_bits_to_wires_tiled over computed values: blockIdx.y = source
+struct WireSrcs {
+    aby3g_wire_src s[ABY3G_WIRE_SRC_MAX];
+};
+__global__ void __launch_bounds__(256) k_bits_to_wires_lin(WireSrcs ws, u64 rows, u64 words) {
+    __shared__ u64 tile[64 * kTilePitch];
+    const aby3g_wire_src& src = ws.s[blockIdx.y];
+    const u64 cols64 = src.cols64;
+    const u64 tilesPerCol = (words + kTileWords - 1) / kTileWords;
+    const u64 c = blockIdx.x / tilesPerCol, w0 = (blockIdx.x % tilesPerCol) * kTileWords;
+    if (c * 64 >= src.nbits) return;  // this source has fewer columns than the grid
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    u64 vv[16];
+#pragma unroll
+    for (u32 k = 0; k < 16; ++k) {
+        const u32 wl = wave * 16 + k;
+        const u64 r = (w0 + wl) * 64 + lane;
+        u64 v = 0;
+        if (w0 + wl < words && r < rows) {
+            const u64 i = r * cols64 + c;
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (src.term[t]) v += (u64)src.coef[t] * (u64)src.term[t][i];
+            if (src.copy_out) src.copy_out[i] = (i64)v;
+            if (src.term[0] || src.term[1] || src.term[2] || src.term[3]) v += (u64)src.constant;
+        }
+        vv[k] = v;
+    }
+    for (u32 k = 0; k < 16; ++k) {
+        const u32 wl = wave * 16 + k;
+        tile[lane * kTilePitch + wl] = transpose64(vv[k], lane);
+    }
+    __syncthreads();
+    for (u32 idx = threadIdx.x; idx < 64 * kTileWords; idx += 256) {
+        const u32 b = idx / kTileWords, wl = idx % kTileWords;
+        const u64 bit = c * 64 + b;
+        if (bit < src.nbits && w0 + wl < words) src.wire_rows[bit * words + w0 + wl] = tile[b * kTilePitch + wl];
+    }
+}
+
 __global__ void __launch_bounds__(256) k_wires_to_bits_tiled(const u64* __restrict__ mem, u64 shareStride,
                                                              const u32* __restrict__ wires, u32 nbits, u64 words,
                                                              i64* __restrict__ out, u64 rows) {
@@ -391,6 +431,27 @@ int aby3g_bits_to_wires2(const int64_t* in, uint64_t rows, uint64_t cols64, uint
         const u64 tiles = ((words + kTileWords - 1) / kTileWords) * ((nbits + 63) / 64);
         launch(PROBE_OTHER, k_bits_to_wires_tiled, dim3((u32)tiles, 2), dim3(256), 0, S(stream), in, rows, cols64,
                nbits, wire_rows, share_stride, words);
+    });
+}
+
+int aby3g_bits_to_wires_lin(const aby3g_wire_src* srcs, uint32_t nsrc, uint64_t rows, uint64_t words,
+                            aby3g_stream stream) {
+    return guarded([&] {
+        ABY3G_REQUIRE(nsrc <= ABY3G_WIRE_SRC_MAX, "too many sources");
+        ABY3G_REQUIRE(words * 64 >= rows, "words too small for rows");
+        if (!nsrc || !words) return;
+        WireSrcs ws{};
+        u64 cols = 0;
+        for (u32 k = 0; k < nsrc; ++k) {
+            ABY3G_REQUIRE(srcs[k].wire_rows != nullptr, "null wire rows");
+            ABY3G_REQUIRE(srcs[k].nbits <= srcs[k].cols64 * 64, "nbits exceeds input columns");
+            ws.s[k] = srcs[k];
+            cols = std::max<u64>(cols, (srcs[k].nbits + 63) / 64);
+        }
+        if (!cols) return;
+        const u64 tiles = ((words + kTileWords - 1) / kTileWords) * cols;
+        launch(PROBE_OTHER, k_bits_to_wires_lin, dim3((u32)tiles, nsrc), dim3(256), 0, S(stream), ws, (u64)rows,
+               (u64)words);
     });
 }
 

@@ -20,49 +20,43 @@ void evalCircuit(BetaCircuit* cir, const std::vector<const sbMatrix*>& in, const
         .get();
 }
 
-// Binary two-input sharing of an arithmetic value: c0 = (sign * (x0 + x2), 0, 0)
-// reshared by P0, c1 = (0, x1, 0) (BuildingBlocks.cpp:475-502, :709-735).
-static void arithToTwoBin(int pIdx, const si64Matrix& x, i64 sign, sbMatrix& c0, sbMatrix& c1, Sh3Runtime& rt) {
-    Gpu& g = rt.gpu();
-    const u64 n = x.size(), b8 = n * sizeof(i64);
-    c0.resize(n, 64);
-    c1.resize(n, 64);
-    c1.setZero();
-    if (pIdx == 0)
-        GPU_CALL(aby3g_i64_lincomb(n, sign, x.share(0), sign, x.share(1), 0, c0.share(0), g.stream()));
-    else
-        GPU_CALL(aby3g_memset(c0.share(0), 0, b8, g.stream()));
-    if (pIdx == 1) d2d(c1.share(0), x.share(0), b8, g);
-    if (pIdx == 2) d2d(c1.share(1), x.share(1), b8, g);
-    rt.mComm.mNext.asyncSendDevice(c0.share(0), b8, g);
-    rt.mComm.mPrev.asyncRecvDevice(c0.share(1), b8, g).get();
+// Binary two-input sharing of an arithmetic value x = sum of coef * X over
+// `x`'s terms, c0 = (sign * (x0 + x2), 0, 0) reshared by P0 and c1 =
+// (0, x1, 0) (BuildingBlocks.cpp:475-502, :709-735), fed straight into the
+// circuit's input wires (setTwoInputSharing: one launch, one message), then
+// the circuit (inputs c0, c1; output 0) evaluated into `res`.
+static void evalTwoInput(BetaCircuit* cir, int pIdx, const std::vector<std::pair<const si64Matrix*, i64>>& x, i64 sign,
+                         sbMatrix& res, Sh3Evaluator& eval, Sh3Runtime& rt) {
+    Sh3BinaryEvaluator binEng;
+    binEng.setCir(cir, x[0].first->size(), eval.mShareGen);
+    setTwoInputSharing(binEng, pIdx, x, sign, {0}, {0}, 1, rt.mComm, rt.gpu());
+    binEng.asyncEvaluate(rt.noDependencies())
+        .then([&](Sh3Task&) { binEng.getOutput(0, res); })
+        .get();
 }
 
 int fetch_msb(int pIdx, const si64Matrix& diffAB, sbMatrix& res, Sh3Evaluator& eval, Sh3Runtime& runtime) {
-    sbMatrix c0, c1;
-    arithToTwoBin(pIdx, diffAB, 1, c0, c1, runtime);
-    evalCircuit(basicLibrary().int_comp_helper(64), {&c0, &c1}, {&res}, eval, runtime);
+    evalTwoInput(basicLibrary().int_comp_helper(64), pIdx, {{&diffAB, 1}}, 1, res, eval, runtime);
     return 0;
 }
 
-static void sub(const si64Matrix& a, const si64Matrix& b, si64Matrix& out, Gpu& g) {
+static void checkShapes(const si64Matrix& a, const si64Matrix& b) {
     if (a.rows() != b.rows() || a.cols() != b.cols()) throw std::runtime_error("shape mismatch " LOCATION);
-    out.resize(a.rows(), a.cols());
-    GPU_CALL(aby3g_i64_lincomb(2 * a.size(), 1, a.data(), -1, b.data(), 0, out.data(), g.stream()));
 }
 
+// cipher_gt(A, B) = MSB(B - A) (BuildingBlocks.cpp:525-532); the difference
+// is folded into the input sharing
 int cipher_gt(int pIdx, const si64Matrix& A, const si64Matrix& B, sbMatrix& res, Sh3Evaluator& eval,
               Sh3Runtime& runtime) {
-    si64Matrix diff;
-    sub(B, A, diff, runtime.gpu());
-    return fetch_msb(pIdx, diff, res, eval, runtime);
+    checkShapes(A, B);
+    evalTwoInput(basicLibrary().int_comp_helper(64), pIdx, {{&B, 1}, {&A, -1}}, 1, res, eval, runtime);
+    return 0;
 }
 
 int cipher_ge(int pIdx, const si64Matrix& A, const si64Matrix& B, sbMatrix& res, Sh3Evaluator& eval,
               Sh3Runtime& runtime) {
-    si64Matrix diff;
-    sub(A, B, diff, runtime.gpu());
-    fetch_msb(pIdx, diff, res, eval, runtime);
+    checkShapes(A, B);
+    evalTwoInput(basicLibrary().int_comp_helper(64), pIdx, {{&A, 1}, {&B, -1}}, 1, res, eval, runtime);
     // flip bit 0 of both shares of every party: all three shares flip
     Gpu& g = runtime.gpu();
     DeviceBuffer ones(g, res.size() * 2 * 8);
@@ -74,11 +68,8 @@ int cipher_ge(int pIdx, const si64Matrix& A, const si64Matrix& B, sbMatrix& res,
 
 int circuit_cipher_eq(int pIdx, const si64Matrix& A, const si64Matrix& B, sbMatrix& res, Sh3Evaluator& eval,
                       Sh3Runtime& runtime) {
-    si64Matrix diff;
-    sub(A, B, diff, runtime.gpu());
-    sbMatrix c0, c1;
-    arithToTwoBin(pIdx, diff, -1, c0, c1, runtime);
-    evalCircuit(basicLibrary().int_eq(64), {&c0, &c1}, {&res}, eval, runtime);
+    checkShapes(A, B);
+    evalTwoInput(basicLibrary().int_eq(64), pIdx, {{&A, 1}, {&B, -1}}, -1, res, eval, runtime);
     return 0;
 }
 

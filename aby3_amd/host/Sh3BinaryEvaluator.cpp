@@ -102,6 +102,117 @@ void Sh3BinaryEvaluator::setInput(u64 i, const sbMatrix& in) {
     mLevel = 0;
 }
 
+void Sh3BinaryEvaluator::setInputs(const std::vector<WireInput>& in) {
+    if (!mCir) throw RTE_LOC;
+    Gpu& g = *mGpu;
+    const u64 W = mCir->mWireCount;
+    std::vector<aby3g_wire_src> srcs;
+    auto flush = [&] {
+        if (srcs.empty()) return;
+        GPU_CALL(aby3g_bits_to_wires_lin(srcs.data(), (u32)srcs.size(), mRows, mWords, g.stream()));
+        srcs.clear();
+    };
+    for (const WireInput& w : in) {
+        if (w.input >= mCir->mInputs.size()) throw std::invalid_argument("input index out of bounds");
+        if (w.share < 0 || w.share > 1) throw std::invalid_argument("share index");
+        const auto& wires = mCir->mInputs[w.input];
+        for (size_t k = 1; k < wires.size(); ++k)
+            if (wires[k] != wires[k - 1] + 1) throw std::runtime_error("expecting contiguous input wires. " LOCATION);
+        aby3g_wire_src s{};
+        for (int t = 0; t < 4; ++t) {
+            s.term[t] = w.term[t];
+            s.coef[t] = w.coef[t];
+        }
+        s.constant = w.constant;
+        s.cols64 = (wires.size() + 63) / 64;
+        s.nbits = (u32)wires.size();
+        s.wire_rows = mMem.as<u64>() + ((u64)w.share * W + wires[0]) * mWords;
+        s.copy_out = w.copyOut;
+        srcs.push_back(s);
+        if (srcs.size() == ABY3G_WIRE_SRC_MAX) flush();
+    }
+    flush();
+    mLevel = 0;
+}
+
+void setTwoInputSharing(Sh3BinaryEvaluator& eng, int pIdx, const std::vector<std::pair<const si64Matrix*, i64>>& x,
+                        i64 sign, const std::vector<u64>& in0, const std::vector<i64>& offsets, u64 in1, CommPkg& comm,
+                        Gpu& g) {
+    if (x.empty() || x.size() > 2 || in0.size() != offsets.size()) throw std::invalid_argument("setTwoInputSharing");
+    const u64 n = x[0].first->size(), b8 = n * sizeof(i64);
+    for (auto& t : x)
+        if (t.first->size() != n) throw std::invalid_argument("setTwoInputSharing: shapes");
+    using WI = Sh3BinaryEvaluator::WireInput;
+    std::vector<WI> w;
+    auto zero = [&](u64 input, int share) {
+        WI z;
+        z.input = input;
+        z.share = share;
+        w.push_back(z);
+    };
+    // sum over the terms of share s of x (times c)
+    auto xshare = [&](WI& d, int s, i64 c, int at) {
+        for (auto& t : x) {
+            d.term[at] = t.first->share(s);
+            d.coef[at++] = (i64)((u64)c * (u64)t.second);
+        }
+        return at;
+    };
+    std::shared_ptr<DeviceBuffer> v;
+    if (pIdx == 0) {
+        // in0 = (sign (x0 + x2) + off, 0); the share itself goes to P1
+        v = std::make_shared<DeviceBuffer>(g, b8);
+        for (size_t k = 0; k < in0.size(); ++k) {
+            WI d;
+            d.input = in0[k];
+            d.share = 0;
+            xshare(d, 1, sign, xshare(d, 0, sign, 0));
+            d.constant = offsets[k];
+            if (k == 0) d.copyOut = v->as<i64>();
+            w.push_back(d);
+            zero(in0[k], 1);
+        }
+        zero(in1, 0);
+        zero(in1, 1);
+        eng.setInputs(w);
+        comm.mNext.asyncSendShared(v, b8, g);
+    } else if (pIdx == 1) {
+        // in0 = (0, sign (x0 + x2) + off) received from P0, in1 = (x1, 0)
+        WI d1;
+        d1.input = in1;
+        d1.share = 0;
+        xshare(d1, 0, 1, 0);
+        w.push_back(d1);
+        zero(in1, 1);
+        v = comm.mPrev.asyncRecvShared(b8, g).getShared();
+        for (size_t k = 0; k < in0.size(); ++k) {
+            zero(in0[k], 0);
+            WI d;
+            d.input = in0[k];
+            d.share = 1;
+            d.term[0] = v->as<i64>();
+            d.coef[0] = 1;
+            d.constant = offsets[k];
+            w.push_back(d);
+        }
+        eng.setInputs(w);
+        v->fence(g.stream());
+    } else {
+        // in0 = (0, 0), in1 = (0, x1)
+        for (size_t k = 0; k < in0.size(); ++k) {
+            zero(in0[k], 0);
+            zero(in0[k], 1);
+        }
+        zero(in1, 0);
+        WI d1;
+        d1.input = in1;
+        d1.share = 1;
+        xshare(d1, 1, 1, 0);
+        w.push_back(d1);
+        eng.setInputs(w);
+    }
+}
+
 void Sh3BinaryEvaluator::setReplicatedInput(u64 i, const sbMatrix& in) {
     if (!mCir) throw RTE_LOC;
     if (i >= mCir->mInputs.size()) throw std::invalid_argument("input index out of bounds");

@@ -36,6 +36,18 @@ public:
     void setInput(u64 i, const sbMatrix& in);
     // a one-row shared input broadcast to every row (Sh3BinaryEvaluator.cpp:105-138)
     void setReplicatedInput(u64 i, const sbMatrix& in);
+    // Inputs straight from arithmetic shares, several in one launch (no
+    // sbMatrix in between): share `share` of circuit input `input` takes the
+    // value sum_t coef[t] * term[t][.] + constant (all terms null: zero).
+    struct WireInput {
+        u64 input = 0;
+        int share = 0;
+        const i64* term[4] = {nullptr, nullptr, nullptr, nullptr};
+        i64 coef[4] = {0, 0, 0, 0};
+        i64 constant = 0;
+        i64* copyOut = nullptr;  // optional: receives sum_t coef[t] * term[t][.]
+    };
+    void setInputs(const std::vector<WireInput>& in);
     Sh3Task asyncEvaluate(Sh3Task dep);
     Sh3Task asyncEvaluate(Sh3Task dep, BetaCircuit* cir, Sh3ShareGen& gen, std::vector<const sbMatrix*> inputs,
                           std::vector<sbMatrix*> outputs);
@@ -69,5 +81,15 @@ private:
     Gpu* mGpu = nullptr;
     void upload(Gpu& g);
 };
+
+// The two-input binary resharing of an arithmetic value x (BuildingBlocks.cpp
+// :475-502, Sh3Piecewise.cpp:392-470), written straight into `eng`'s input
+// wires: input in0[k] := sign * (x0 + x2) + offsets[k], reshared by P0 (the
+// one message, P0 -> P1, zero-copy), and input in1 := x1 (P1 and P2 hold it);
+// x's shares are sums of coef * X.share(s) over the (X, coef) terms (at most
+// two matrices). The circuit must already be set on `eng`.
+void setTwoInputSharing(Sh3BinaryEvaluator& eng, int pIdx, const std::vector<std::pair<const si64Matrix*, i64>>& x,
+                        i64 sign, const std::vector<u64>& in0, const std::vector<i64>& offsets, u64 in1, CommPkg& comm,
+                        Gpu& g);
 
 }  // namespace aby3

@@ -35,37 +35,20 @@ void Sh3Piecewise::eval(const std::vector<double>& inD, std::vector<double>& out
 void Sh3Piecewise::getInputRegions(const si64Matrix& inputs, u64 D, Sh3Runtime& rt, Sh3ShareGen& gen) {
     // Sh3Piecewise.cpp:381-516. P0 reshares x0 + x2 as the binary sharing
     // (x0 + x2, 0, 0); P1/P2 expose x1 as (0, x1, 0). Per threshold the
-    // circuit computes MSB((x0 + x2 - t) + x1) = [x < t].
-    Gpu& g = rt.gpu();
-    const u64 n = inputs.size(), b8 = n * sizeof(i64);
+    // circuit computes MSB((x0 + x2 - t) + x1) = [x < t]. The T shifted
+    // copies and x1 go straight into the circuit's input wires in one launch
+    // (setTwoInputSharing), with the one message P0 -> P1.
+    const u64 n = inputs.size();
     const u64 T = mThresholds.size();
-    const u64 p = rt.mPartyIdx;
-    circuitInput0.resize(T);
-    circuitInput0[0].resize(n, 64);
-    circuitInput1.resize(n, 64);
-    circuitInput1.setZero();
-    if (p == 0)
-        GPU_CALL(aby3g_i64_lincomb(n, 1, inputs.share(0), 1, inputs.share(1), 0, circuitInput0[0].share(0), g.stream()));
-    else
-        GPU_CALL(aby3g_memset(circuitInput0[0].share(0), 0, b8, g.stream()));
-    if (p == 1) d2d(circuitInput1.share(0), inputs.share(0), b8, g);
-    if (p == 2) d2d(circuitInput1.share(1), inputs.share(1), b8, g);
-    rt.mComm.mNext.asyncSendDevice(circuitInput0[0].share(0), b8, g);
-    rt.mComm.mPrev.asyncRecvDevice(circuitInput0[0].share(1), b8, g).get();
-
-    for (u64 t = 1; t < T; ++t) circuitInput0[t].copyFrom(circuitInput0[0]);
-    for (u64 t = 0; t < T; ++t) {
-        circuitInput0[t].resize(n, 64);
-        if (p < 2) {
-            i64 thr = mThresholds[t].getFixedPoint(D);
-            i64* v = circuitInput0[t].share((int)p);
-            GPU_CALL(aby3g_i64_lincomb(n, 1, v, 0, nullptr, (i64)(0 - (u64)thr), v, g.stream()));
-        }
-    }
     BetaCircuit* cir = lib.int_Sh3Piecewise_helper(64, T);
     binEng.setCir(cir, n, gen);
-    binEng.setInput(T, circuitInput1);
-    for (u64 t = 0; t < T; ++t) binEng.setInput(t, circuitInput0[t]);
+    std::vector<u64> in0(T);
+    std::vector<i64> off(T);
+    for (u64 t = 0; t < T; ++t) {
+        in0[t] = t;
+        off[t] = (i64)(0 - (u64)mThresholds[t].getFixedPoint(D));
+    }
+    setTwoInputSharing(binEng, (int)rt.mPartyIdx, {{&inputs, 1}}, 1, in0, off, T, rt.mComm, rt.gpu());
     mInputRegions.resize(T + 1);
     binEng.asyncEvaluate(rt.noDependencies())
         .then([&, T](Sh3Task&) {

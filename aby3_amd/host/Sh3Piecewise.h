@@ -63,8 +63,6 @@ private:
     void getFunctionValues(const si64Matrix& inputs, Sh3Runtime& rt, u64 D);
     CircuitLibrary lib;
     Sh3BinaryEvaluator binEng;
-    std::vector<sbMatrix> circuitInput0;
-    sbMatrix circuitInput1;
 };
 
 }  // namespace aby3

@@ -122,6 +122,7 @@ _SIGS = {
     "aby3g_wires_to_bits2": (c_int, [c_void_p, c_uint64, c_void_p, ctypes.c_uint32, c_uint64, c_void_p, c_uint64,
                                      c_void_p]),
     "aby3g_bin_unpack": (c_int, [c_void_p, c_void_p, c_uint32, c_void_p, c_uint64, c_uint64, c_void_p]),
+    "aby3g_bits_to_wires_lin": (c_int, [c_void_p, c_uint32, c_uint64, c_uint64, c_void_p]),
     "aby3g_bits_to_wires": (c_int, [c_void_p, c_uint64, c_uint64, c_uint32, c_void_p, c_uint64, c_void_p]),
     "aby3g_wires_to_bits": (c_int, [c_void_p, c_void_p, c_uint32, c_uint64, c_void_p, c_uint64, c_void_p]),
     "aby3g_i64_lincomb": (c_int, [c_uint64, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),

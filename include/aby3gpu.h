@@ -285,6 +285,27 @@ int aby3g_bits_to_wires2(const int64_t* in, uint64_t rows, uint64_t cols64, uint
 int aby3g_wires_to_bits2(const uint64_t* mem, uint64_t share_stride, const uint32_t* wires, uint32_t nbits,
                          uint64_t words, int64_t* out, uint64_t rows, aby3g_stream stream);
 
+/* setInput of shares that are linear combinations of arithmetic shares,
+ * several inputs / shares in one launch (the two-input binary resharing of
+ * fetch_msb and Sh3Piecewise::getInputRegions, BuildingBlocks.cpp:475-502,
+ * Sh3Piecewise.cpp:392-470): source k writes nbits wire rows of the value
+ * v[r] = sum_t coef[t] * term[t][r * cols64 + c] + constant (mod 2^64);
+ * all terms NULL writes zero wires. copy_out (optional) receives
+ * sum_t coef[t] * term[t][...] (without the constant), e.g. P0's share to
+ * send. At most ABY3G_WIRE_SRC_MAX sources per call. */
+#define ABY3G_WIRE_SRC_MAX 8
+typedef struct {
+    const int64_t* term[4];
+    int64_t coef[4];
+    int64_t constant;
+    uint64_t cols64;
+    uint32_t nbits;
+    uint64_t* wire_rows;
+    int64_t* copy_out;
+} aby3g_wire_src;
+int aby3g_bits_to_wires_lin(const aby3g_wire_src* srcs, uint32_t nsrc, uint64_t rows, uint64_t words,
+                            aby3g_stream stream);
+
 /* ------------------------------------------------ element-wise helpers -- */
 /* out[i] = ca*a[i] + cb*b[i] + c (mod 2^64); b may be NULL. Covers share
  * sums/differences (BuildingBlocks.cpp:475-480, Sh3Piecewise.cpp:403-470,

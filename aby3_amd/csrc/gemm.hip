@@ -18,6 +18,7 @@
 // row r is stored at slot g ^ (r & 15): the 16 lanes of each ds_read_b128
 // lane group read 16 different rows at the same chunk and land on 16
 // different bank slots.
+#include <atomic>
 #include <map>
 #include <mutex>
 #include "epilogue.h"
@@ -585,13 +586,17 @@ private:
     // off by default (ABY3G_MFMA_TURN=1 turns it on, for A/B runs): letting
     // co-located parties' GEMMs overlap measured +6 % on C2 -- the next
     // GEMM's workgroups fill the CUs that the previous one's tail frees
-    static bool enabled() {
-        static const bool on = [] {
+public:
+    static std::atomic<int>& mode() {
+        static std::atomic<int> on{[] {
             const char* e = getenv("ABY3G_MFMA_TURN");
-            return e && e[0] == '1';
-        }();
+            return (e && e[0] == '1') ? 1 : 0;
+        }()};
         return on;
     }
+
+private:
+    static bool enabled() { return mode().load(std::memory_order_relaxed) != 0; }
     static std::mutex& mu() {
         static std::mutex m;
         return m;
@@ -660,6 +665,10 @@ void check_ws(const GemmPlan& p, void* ws, size_t bytes) {
 using namespace aby3g;
 
 extern "C" {
+
+int aby3g_mfma_turn(int on) {
+    return guarded([&] { MfmaTurn::mode().store(on ? 1 : 0); });
+}
 
 int aby3g_mul_prefers_fused(int mode, uint64_t M, uint64_t K, uint64_t N) {
     return mode != ABY3G_MUL_GEMM || small_gemm(M, K, N);

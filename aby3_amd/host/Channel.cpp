@@ -1,5 +1,6 @@
 #include "Channel.h"
 #include <chrono>
+#include <cstdlib>
 #include <atomic>
 #include <map>
 
@@ -264,7 +265,23 @@ void Channel::resetStats() {
 
 double recvWaitUs() { return t_recvWaitUs; }
 
+// Stream-ordered signal words are waited for by a spinning blit kernel: a
+// tool that serialises kernels (rocprofv3 --pmc, AMD_SERIALIZE_KERNEL) would
+// run the waiting kernel alone and never the writer -- there the channels use
+// events. ABY3G_CHANNEL_SIGNAL=0 turns the signal words off explicitly.
+static bool signalWordsAllowed() {
+    static const bool ok = [] {
+        const char* e = getenv("ABY3G_CHANNEL_SIGNAL");
+        if (e && e[0] == '0') return false;
+        const char* ser = getenv("AMD_SERIALIZE_KERNEL");
+        if (ser && ser[0] && ser[0] != '0') return false;
+        return true;
+    }();
+    return ok;
+}
+
 std::vector<CommPkg> makeLocalRing(const int* devices) {
+    if (!signalWordsAllowed()) devices = nullptr;
     // pipe[i][j]: messages from party i to party j
     std::shared_ptr<Pipe> p[3][3];
     for (int i = 0; i < 3; ++i)

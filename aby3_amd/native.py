@@ -99,6 +99,7 @@ _SIGS = {
                                 POINTER(ZeroShare), c_void_p, c_size_t, c_void_p]),
     "aby3g_trunc_tuple": (c_int, [POINTER(TruncStreams), c_uint64, ctypes.c_uint, c_void_p, c_void_p, c_void_p]),
     "aby3g_mul_prefers_fused": (c_int, [c_int, c_uint64, c_uint64, c_uint64]),
+    "aby3g_mfma_turn": (c_int, [c_int]),
     "aby3g_mul_sub_local": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64,
                                     c_uint64, c_void_p, c_size_t, c_void_p]),
     "aby3g_mul_trunc_local": (c_int, [c_int, c_void_p, c_void_p, c_uint64, c_uint64, c_uint64, ctypes.c_uint,

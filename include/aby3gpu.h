@@ -149,6 +149,12 @@ typedef struct {
     uint64_t prev_off;
 } aby3g_trunc_streams;
 
+/* Share-GEMM launches on one device take turns (1) or may overlap (0, the
+ * default; ABY3G_MFMA_TURN=1 sets the initial mode): co-located parties'
+ * overlapping GEMMs finish sooner together, but a launch's span then includes
+ * the CUs spent on the others' -- bench.py's roofline pass takes turns. */
+int aby3g_mfma_turn(int on);
+
 /* 1 when the whole round-1 local part runs best as one fused launch
  * (aby3g_mul_trunc_local / aby3g_mul_local with zs): Hadamard, and GEMMs of
  * up to 2^23 product terms, which run on the VALU instead of the int8-MFMA

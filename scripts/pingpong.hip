@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 
 __global__ void k_tick(unsigned long long* p) {
     if (threadIdx.x == 0) *p += 1;
@@ -22,7 +23,8 @@ __global__ void k_tick(unsigned long long* p) {
         }                                                                      \
     } while (0)
 
-int main() {
+int main(int argc, char** argv) {
+    const int only = argc > 1 ? atoi(argv[1]) : -1;
     hipStream_t s[2];
     for (auto& x : s) CK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
     unsigned long long *d, *sig;
@@ -34,6 +36,7 @@ int main() {
     hipEvent_t ev[2];
     for (auto& evx : ev) CK(hipEventCreateWithFlags(&evx, hipEventDisableTiming));
     for (int mode = 0; mode < 4; ++mode) {
+        if (only >= 0 && mode != only) continue;
         for (int rep = 0; rep < 2; ++rep) {
             CK(hipDeviceSynchronize());
             auto t0 = std::chrono::steady_clock::now();

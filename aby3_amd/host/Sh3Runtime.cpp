@@ -93,11 +93,25 @@ void Scheduler::removeTask(i64 idx) {
             addUnique(cc->second.up, d);
         }
     }
-    for (i64 c : closures) {
-        auto cc = mTasks.find(c);
+    // Innermost closure first (the latest created): a task chained on an inner
+    // closure -- asyncEvaluate(self, ...).then(getOutput) inside a task whose
+    // closure the caller waits on (Sh3Converter.cpp:111) -- belongs to the
+    // outer closure too, so every outer closure also waits on the inner ones
+    // and through them on what is chained after them. (The reference's
+    // Task.h:263-271 releases both at once and can leave that task behind.)
+    std::vector<i64> cl = closures;
+    std::sort(cl.begin(), cl.end(), std::greater<i64>());
+    for (size_t a = 0; a < cl.size(); ++a) {
+        auto cc = mTasks.find(cl[a]);
         if (cc == mTasks.end()) continue;
+        for (size_t b = a + 1; b < cl.size(); ++b) {
+            auto outer = mTasks.find(cl[b]);
+            if (outer == mTasks.end()) continue;
+            addUnique(cc->second.closures, cl[b]);
+            addUnique(outer->second.up, cl[a]);
+        }
         removeOne(cc->second.up, idx);
-        if (cc->second.up.empty()) removeTask(c);
+        if (cc->second.up.empty()) removeTask(cl[a]);
     }
     mTasks.erase(idx);
 }

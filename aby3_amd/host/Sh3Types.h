@@ -95,6 +95,25 @@ private:
     u64 mBitCount = 0;
 };
 
+// sPackedBin (Sh3Types.h:451-560): the bit-transposed form of shareCount
+// values of bitCount bits -- bitCount rows of ceil(shareCount/64) words per
+// share (row b holds bit b of every value, 64 values per word).
+class sPackedBin : public SharedMat {
+public:
+    sPackedBin() = default;
+    sPackedBin(u64 shareCount, u64 bitCount) { reset(shareCount, bitCount); }
+    void reset(u64 shareCount, u64 bitCount) {
+        mShareCount = shareCount;
+        SharedMat::resize(bitCount, (shareCount + 63) / 64);
+    }
+    u64 shareCount() const { return mShareCount; }
+    u64 bitCount() const { return rows(); }
+    u64 simdWidth() const { return cols(); }
+
+private:
+    u64 mShareCount = 0;
+};
+
 // Fixed-point helpers (Sh3FixedPoint.h:21-112)
 inline i64 toFixed(double v, u64 D) { return (i64)(v * (double)(1ull << D)); }
 inline double fromFixed(i64 v, u64 D) { return (double)v / (double)(1ull << D); }

@@ -111,6 +111,13 @@ _SIGS = {
     "aby3g_bitmul_p2": (c_int, [c_void_p, c_void_p, c_uint64, POINTER(StreamPos), c_u8p, c_uint64, c_void_p,
                                 c_void_p, c_void_p, c_void_p]),
     "aby3g_ot_recv": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_int, c_void_p, c_void_p]),
+    "aby3g_a2b_reshare": (c_int, [POINTER(StreamPos), c_uint64, c_uint64, c_uint64, c_void_p, c_void_p, c_int,
+                                  c_void_p, c_void_p, c_void_p]),
+    "aby3g_bitinj_send": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, POINTER(StreamPos), POINTER(StreamPos),
+                                  c_u8p, c_uint64, c_u8p, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "aby3g_ot_help_bits": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_u8p, c_uint64, c_void_p, c_void_p]),
+    "aby3g_ot_recv_bits": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_uint64, c_uint64, c_void_p,
+                                   c_void_p]),
     "aby3g_pubmul_p0": (c_int, [c_int64, c_void_p, c_uint64, POINTER(ZeroShare), c_u8p, c_uint64, c_u8p, c_uint64,
                                 c_void_p, c_void_p, c_void_p]),
     "aby3g_pubmul_helper": (c_int, [c_void_p, c_uint64, POINTER(ZeroShare), c_u8p, c_uint64, c_void_p, c_void_p,

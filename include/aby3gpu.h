@@ -222,6 +222,40 @@ int aby3g_bitmul_p2(const int64_t* A, const int64_t* B, uint64_t n, const aby3g_
  * c_i = choice_src[i] & 1; accumulate != 0 adds into out (mod 2^64). */
 int aby3g_ot_recv(const int64_t* msgs, const int64_t* mc, const int64_t* choice_src, uint64_t n, int accumulate,
                   int64_t* out, aby3g_stream stream);
+
+/* ---- share conversions (aby3/sh3/Sh3Converter.cpp) ----------------------
+ * Choice bits come from packed binary rows: bit k of a [rows][cols64] share
+ * matrix with `bits` bits per row is bit k % bits of row k / bits
+ * (BitVector::append per row, Sh3Converter.cpp:240-247, 268-274).
+ *
+ * toBinaryMatrix's resharing (Sh3Converter.cpp:61-207), one party's part,
+ * one launch over n = rows * cols64 words: with r = the draws' stream words
+ * (mPrevCommon / mNextCommon.get<i64>() per element; `draws` may be NULL
+ * when neither out_r nor xor_draws is used),
+ *   out_r[e] = r[e] & m(e),  out_x[e] = ((a[e] + b[e]) ^ (xor_draws ? r[e] : 0)) & m(e),
+ * b optional, m(e) = last_mask on the last word of each row (the
+ * bitCount % 64 trim, :96-106), all ones elsewhere. Either output may be NULL. */
+int aby3g_a2b_reshare(const aby3g_stream_pos* draws, uint64_t n, uint64_t cols64, uint64_t last_mask,
+                      const int64_t* a, const int64_t* b, int xor_draws, int64_t* out_x, int64_t* out_r,
+                      aby3g_stream stream);
+/* bitInjection, party 2 = OT sender (Sh3Converter.cpp:319-361): `in` is P2's
+ * [2][rows][cols64] binary shares; per bit k: dest[0][k] = next stream word,
+ * dest[1][k] = prev stream word, b = bit k of in[0] ^ in[1],
+ * m[k][c] = -dest0 - dest1 + (c ^ b); msgs_a = SharedOT::send pads
+ * (key_a, ctr_a) ^ m, and msgs_b likewise with (key_b, ctr_b) when non-NULL
+ * (the one-round variant's second OT). dest is [2][rows * bits]. */
+int aby3g_bitinj_send(const int64_t* in, uint64_t rows, uint64_t cols64, uint64_t bits,
+                      const aby3g_stream_pos* next, const aby3g_stream_pos* prev, const uint8_t key_a[16],
+                      uint64_t ctr_a, const uint8_t key_b[16], uint64_t ctr_b, int64_t* dest, int64_t* msgs_a,
+                      int64_t* msgs_b, aby3g_stream stream);
+/* SharedOT::help with packed choice bits (SharedOT.cpp:30-94):
+ * mc[k] = half (bit k) of AES(ot_key, ctr + k). */
+int aby3g_ot_help_bits(const int64_t* choice_rows, uint64_t rows, uint64_t cols64, uint64_t bits,
+                       const uint8_t ot_key[16], uint64_t ctr, int64_t* mc, aby3g_stream stream);
+/* SharedOT::recv with packed choice bits: out[k] = msgs[k][bit k] ^ mc[k]. */
+int aby3g_ot_recv_bits(const int64_t* msgs, const int64_t* mc, const int64_t* choice_rows, uint64_t rows,
+                       uint64_t cols64, uint64_t bits, int64_t* out, aby3g_stream stream);
+
 /* asyncMul(i64 a, sbMatrix B, C) party 0 (Sh3Evaluator.cpp:430-447):
  * s0[bb] = getShare(), s0[bb^1] = a + that, bb = B0^B1;
  * msgs_next = pads(ot_next_key, ctr_next) ^ s0; msgs_prev = pads(ot_prev_key, ctr_prev) ^ s0. */

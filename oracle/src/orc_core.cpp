@@ -582,3 +582,111 @@ i64 fixedMulPlain(i64 a, i64 b, u64 D) {
 }
 
 }  // namespace orc
+
+// ---------------------------------------------------------------------------
+// Sh3Converter (aby3/sh3/Sh3Converter.cpp)
+// ---------------------------------------------------------------------------
+namespace orc {
+
+std::array<ConvParty, 3> converterInit(std::array<Party, 3>& ev) {
+    std::array<ConvParty, 3> cv;
+    cv[0].ot02.setSeed(ev[0].gen.prev.getBlock());  // Sh3Converter.h:31-32
+    cv[1].ot12.setSeed(ev[1].gen.next.getBlock());  // :33-34
+    cv[2].ot12.setSeed(ev[2].gen.prev.getBlock());  // :35-39
+    cv[2].ot02.setSeed(ev[2].gen.next.getBlock());
+    return cv;
+}
+
+static inline u8 bitAt(const Mat& m, u64 row, u64 bit) {
+    return (u8)(((u64)m(row, bit / 64) >> (bit % 64)) & 1);
+}
+
+SMat toPackedBin(const SMat& in, u64 bitCount) {
+    const u64 rows = in.rows(), simd = (rows + 63) / 64;
+    SMat out(bitCount, simd);
+    for (int s = 0; s < 2; ++s)
+        for (u64 i = 0; i < rows; ++i)
+            for (u64 j = 0; j < bitCount; ++j)
+                if (bitAt(in.s[s], i, j)) out.s[s](j, i / 64) |= (i64)(1ull << (i % 64));
+    return out;
+}
+
+SMat fromPackedBin(const SMat& packed, u64 shareCount, u64 bitCount) {
+    SMat out(shareCount, (bitCount + 63) / 64);
+    for (int s = 0; s < 2; ++s)
+        for (u64 j = 0; j < bitCount; ++j)
+            for (u64 i = 0; i < shareCount; ++i)
+                if (bitAt(packed.s[s], j, i)) out.s[s](i, j / 64) |= (i64)(1ull << (j % 64));
+    return out;
+}
+
+Shared toBinaryMatrix(std::array<Party, 3>& ev, const Circuit& addCir, const Shared& x, u64 bitCount) {
+    const u64 rows = x[0].rows(), cols64 = (bitCount + 63) / 64;
+    if (cols64 != x[0].cols()) throw std::runtime_error("toBinaryMatrix: ceil(bitCount/64) != in.cols()");
+    const u64 n = rows * cols64;
+    const u64 mask = bitCount % 64 ? (1ull << (bitCount % 64)) - 1 : ~0ull;
+    auto m = [&](u64 e) { return e % cols64 == cols64 - 1 ? mask : ~0ull; };
+    Shared c0, c1;
+    for (int p = 0; p < 3; ++p) {
+        c0[p] = SMat(rows, cols64);
+        c1[p] = SMat(rows, cols64);
+    }
+    for (u64 e = 0; e < n; ++e) {
+        // P0 (:90-106): r = prev stream word, x0 = ((in0 + in1) ^ r, r)
+        const u64 r = (u64)ev[0].gen.prev.getI64();
+        c0[0].s[1].v[e] = (i64)(r & m(e));
+        c0[0].s[0].v[e] = (i64)((((u64)x[0].s[0].v[e] + (u64)x[0].s[1].v[e]) ^ r) & m(e));
+    }
+    for (u64 e = 0; e < n; ++e) {
+        // P2 (:179-194): x0 = (r, 0) with the same words, x1 = (0, in1)
+        c0[2].s[0].v[e] = (i64)((u64)ev[2].gen.next.getI64() & m(e));
+        c1[2].s[1].v[e] = (i64)((u64)x[2].s[1].v[e] & m(e));
+        // P1 (:132-147): x0 = (0, P0's message), x1 = (in0, 0)
+        c1[1].s[0].v[e] = (i64)((u64)x[1].s[0].v[e] & m(e));
+    }
+    c0[1].s[1] = c0[0].s[0];  // P0 -> P1 (:108, :149)
+    auto out = evalCircuit(ev, addCir, {&c0, &c1});
+    return out[0];
+}
+
+Shared bitInjection(std::array<Party, 3>& ev, std::array<ConvParty, 3>& cv, const Shared& b, u64 bitCount,
+                    bool twoRounds) {
+    const u64 rows = b[0].rows(), n = rows * bitCount;
+    auto choices = [&](const Mat& m) {  // BitVector::append per row (:241-247)
+        std::vector<u8> c(n);
+        for (u64 i = 0, k = 0; i < rows; ++i)
+            for (u64 j = 0; j < bitCount; ++j, ++k) c[k] = bitAt(m, i, j);
+        return c;
+    };
+    Shared d;
+    for (int p = 0; p < 3; ++p) d[p] = SMat(rows, bitCount);
+    // P2, sender (:319-363)
+    std::vector<std::array<i64, 2>> m(n);
+    {
+        for (u64 k = 0; k < n; ++k) d[2].s[0].v[k] = ev[2].gen.next.getI64();
+        for (u64 k = 0; k < n; ++k) d[2].s[1].v[k] = ev[2].gen.prev.getI64();
+        auto c0 = choices(b[2].s[0]), c1 = choices(b[2].s[1]);
+        for (u64 k = 0; k < n; ++k) {
+            const u8 bb = c0[k] ^ c1[k];
+            m[k][0] = m[k][1] = (i64)(0 - (u64)d[2].s[0].v[k] - (u64)d[2].s[1].v[k]);
+            m[k][bb ^ 1] = (i64)((u64)m[k][bb ^ 1] + 1);
+        }
+    }
+    auto msgsTo0 = cv[2].ot12.send(m);                         // P2 -> P0
+    std::vector<std::array<i64, 2>> msgsTo1;
+    if (!twoRounds) msgsTo1 = cv[2].ot02.send(m);               // P2 -> P1
+    const auto ch0 = choices(b[0].s[0]), ch1 = choices(b[1].s[1]);  // P0's and P1's copy of share 0
+    auto help1 = cv[1].ot12.help(ch1);                          // P1 -> P0 (:290)
+    for (u64 k = 0; k < n; ++k) d[1].s[0].v[k] = ev[1].gen.next.getI64();  // :291
+    std::vector<i64> help0;
+    if (!twoRounds) help0 = cv[0].ot02.help(ch0);                // P0 -> P1 (:269)
+    for (u64 k = 0; k < n; ++k) d[0].s[1].v[k] = ev[0].gen.prev.getI64();  // :274
+    d[0].s[0].v = ot_recv(msgsTo0, help1, ch0);                 // :255-258
+    if (twoRounds)
+        d[1].s[1] = d[0].s[0];                                  // :262, :312
+    else
+        d[1].s[1].v = ot_recv(msgsTo1, help0, ch1);             // :303-306
+    return d;
+}
+
+}  // namespace orc

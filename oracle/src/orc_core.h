@@ -198,3 +198,37 @@ Shared boolNot(const Shared& x);
 i64 fixedMulPlain(i64 a, i64 b, u64 D);  // Sh3FixedPoint.cpp:8-20 (int128 divide)
 
 }  // namespace orc
+
+namespace orc {
+
+// --------------------------------------------------------------------------
+// Share conversions (aby3/sh3/Sh3Converter.h/.cpp).
+// --------------------------------------------------------------------------
+struct ConvParty {  // Sh3Converter::mOT12 / mOT02
+    SharedOT ot12, ot02;
+};
+// Sh3Converter::init (Sh3Converter.h:25-40): P0 seeds mOT02 from its prev
+// stream, P1 mOT12 from its next stream, P2 mOT12 from prev then mOT02 from
+// next; setSeed resets the counter to 0 (SharedOT.cpp:96-100).
+std::array<ConvParty, 3> converterInit(std::array<Party, 3>& ev);
+
+// toPackedBin / toBinaryMatrix(sPackedBin) (Sh3Converter.cpp:12-59): per
+// share a bit-matrix transpose (cryptoTools transpose over byte views):
+// packed row j (bitCount rows of ceil(rows/64) words) bit i = row i bit j.
+SMat toPackedBin(const SMat& in, u64 bitCount);
+SMat fromPackedBin(const SMat& packed, u64 shareCount, u64 bitCount);
+
+// toBinaryMatrix(si64Matrix -> sbMatrix) (Sh3Converter.cpp:61-207): P0 reshares
+// x0 + x2 binary-randomized with its prev stream, P2 draws the same words
+// from its next stream, P1/P2 expose x1; both trimmed to bitCount per row;
+// then the adder circuit `addCir` (getArithToBinCircuit, :372-410, supplied by
+// the product's circuit library, as for the piecewise helper).
+Shared toBinaryMatrix(std::array<Party, 3>& ev, const Circuit& addCir, const Shared& x, u64 bitCount);
+
+// bitInjection (Sh3Converter.cpp:209-370): every bit k of b (row k / bitCount,
+// bit k % bitCount) becomes an arithmetic 0/1 via P2's OTs; the result is
+// rows x bitCount.
+Shared bitInjection(std::array<Party, 3>& ev, std::array<ConvParty, 3>& cv, const Shared& b, u64 bitCount,
+                    bool twoRounds);
+
+}  // namespace orc

@@ -110,9 +110,32 @@ static void reentrancy_test() {
     CHECK(threw);
 }
 
+// A task chained on an inner closure inside a task (asyncEvaluate(self,
+// ...).then(getOutput), Sh3Converter.cpp:111) completes before the outer
+// closure does.
+static void nested_closure_test() {
+    Sh3Runtime rt;
+    CommPkg comm;
+    rt.init(0, comm, -1);
+    int counter = 0;
+    auto outer = rt.noDependencies()
+                     .then([&](CommPkg&, Sh3Task self) {
+                         auto inner = self.then([&](CommPkg&, Sh3Task s2) {
+                             s2.then([&](CommPkg&, Sh3Task s3) {
+                                 s3.then([&](CommPkg&, Sh3Task) { CHECK(counter++ == 0); }, "round-3");
+                             }, "round-2");
+                         }, "round-1");
+                         inner.getClosure().then([&](Sh3Task) { CHECK(counter++ == 1); }, "output");
+                     })
+                     .getClosure();
+    outer.get();
+    CHECK(counter == 2);
+}
+
 int main() {
     run("Task_schedule_test", task_schedule_test);
     run("Sh3_Runtime_schedule_test", runtime_schedule_test);
     run("Sh3_Runtime_reentrancy_test", reentrancy_test);
+    run("nested_closure_test", nested_closure_test);
     return failures ? 1 : 0;
 }

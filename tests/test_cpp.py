@@ -38,3 +38,8 @@ def test_arith_protocols_gpu():
 @pytest.mark.gpu
 def test_binary_protocols_gpu():
     _run("test_binary", 600)
+
+
+@pytest.mark.gpu
+def test_convert_protocols_gpu():
+    _run("test_convert", 600)

@@ -112,6 +112,34 @@ __global__ void k_ot_recv_bits(const i64* __restrict__ msgs, const i64* __restri
         out[i] = msgs[2 * i + packed_bit(in, i, bits, cols64)] ^ mc[i];
 }
 
+// bool2arith's correlated r (BoolBasic.cpp:530-545): PRNG(seed).get<int32_t>()
+// sign-extended, times `scale`; one counter (four int32 draws) per thread.
+__global__ void __launch_bounds__(kBlock, 4) k_prng_i32(const u32* __restrict__ T0g, AesKey k, u64 w0, u64 n,
+                                                       i64 scale, i64* __restrict__ out) {
+    __shared__ u32 lds[kAesLdsWords];
+    aes_fill_lds(lds, T0g);
+    const u32 lane32 = threadIdx.x & 31;
+    const u64 c_first = w0 >> 2, c_last = (w0 + n - 1) >> 2;
+    for (u64 c = c_first + (u64)blockIdx.x * blockDim.x + threadIdx.x; c <= c_last;
+         c += (u64)gridDim.x * blockDim.x) {
+        u64 lo, hi;
+        aes_ctr_block(lds, lane32, k, c, lo, hi);
+        const u32 w[4] = {(u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32)};
+#pragma unroll
+        for (u32 q = 0; q < 4; ++q) {
+            const u64 j = 4 * c + q;
+            if (j >= w0 && j - w0 < n) out[j - w0] = (i64)((u64)scale * (u64)(i64)(int32_t)w[q]);
+        }
+    }
+}
+
+// bool2arith, P2 (BoolBasic.cpp:573-587): c = c0 ^ c1 ^ recv, out = c - t
+__global__ void k_b2a_open(const i64* __restrict__ c0, const i64* __restrict__ c1, const i64* __restrict__ recv,
+                           const i64* __restrict__ t, u64 n, i64* __restrict__ out) {
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x)
+        out[i] = (i64)(((u64)c0[i] ^ (u64)c1[i] ^ (u64)recv[i]) - (u64)t[i]);
+}
+
 void check_packed(uint64_t rows, uint64_t cols64, uint64_t bits) {
     ABY3G_REQUIRE(bits >= 1 && (bits + 63) / 64 <= cols64, "bits per row exceed the packed row");
     ABY3G_REQUIRE(rows <= (~0ull) / bits, "rows x bits overflows");
@@ -184,6 +212,28 @@ int aby3g_ot_recv_bits(const int64_t* msgs, const int64_t* mc, const int64_t* ch
         if (!n) return;
         launch(PROBE_OTHER, k_ot_recv_bits, dim3(aes_grid(n, kBlock)), dim3(kBlock), 0, S(stream), msgs, mc,
                choice_rows, n, bits, cols64, out);
+    });
+}
+
+int aby3g_prng_i32(const aby3g_stream_pos* s, uint64_t n, int64_t scale, int64_t* out, aby3g_stream stream) {
+    return guarded([&] {
+        ABY3G_REQUIRE(s && out, "null argument");
+        ABY3G_REQUIRE(s->off % 4 == 0, "stream offset must be a multiple of 4");
+        if (!n) return;
+        AesKey k = expand_key(s->seed);
+        const u64 w0 = s->off / 4, items = ((w0 + n - 1) >> 2) - (w0 >> 2) + 1;
+        launch(PROBE_AES, k_prng_i32, dim3(aes_grid(items, kBlock)), dim3(kBlock), 0, S(stream), aes_table(), k, w0,
+               n, (i64)scale, out);
+    });
+}
+
+int aby3g_b2a_open(const int64_t* c0, const int64_t* c1, const int64_t* recv, const int64_t* t, uint64_t n,
+                   int64_t* out, aby3g_stream stream) {
+    return guarded([&] {
+        ABY3G_REQUIRE(c0 && c1 && recv && t && out, "null argument");
+        if (!n) return;
+        launch(PROBE_OTHER, k_b2a_open, dim3(aes_grid(n, kBlock)), dim3(kBlock), 0, S(stream), c0, c1, recv, t, n,
+               out);
     });
 }
 

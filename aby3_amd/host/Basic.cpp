@@ -1,5 +1,7 @@
 #include "Basic.h"
 #include <cmath>
+#include <cstring>
+#include <random>
 
 namespace aby3 {
 
@@ -224,6 +226,84 @@ int odd_even_multi_merge(std::vector<sbMatrix>& data, sbMatrix& sorted, int pIdx
     }
     sorted = std::move(data[0]);
     return 0;
+}
+
+}  // namespace aby3
+
+namespace aby3 {
+
+void bool2arith(int pIdx, const sbMatrix& boolInput, si64Matrix& res, Sh3Encryptor& enc, Sh3Evaluator& eval,
+                Sh3Runtime& runtime) {
+    const u64 len = boolInput.rows(), bitSize = boolInput.bitCount();
+    if (bitSize == 1) {  // pi_cb_mul(ones, boolInput) (:522-526)
+        eval.asyncMul(runtime.noDependencies(), (i64)1, boolInput, res, enc.mShareGen).get();
+        return;
+    }
+    // the reference copies `len` words per share (:538-545): one word per row
+    if (boolInput.cols() != 1) throw std::runtime_error("bool2arith: at most 64 bits per row " LOCATION);
+    Gpu& g = runtime.gpu();
+    const u64 b8 = len * sizeof(i64);
+    auto fresh = [](const block& seed) {  // PRNG prng(seed): a new generator, offset 0
+        aby3g_stream_pos p;
+        std::memcpy(p.seed, seed.data(), 16);
+        p.off = 0;
+        return p;
+    };
+    // 1) r, shared (r, 0, 0) by P0 (share 0) and P1 (share 1)
+    sbMatrix r(len, bitSize);
+    GPU_CALL(aby3g_memset(r.data(), 0, 2 * b8, g.stream()));
+    aby3g_stream_pos rpos = fresh(pIdx == 0 ? enc.mShareGen.mNextSeed : enc.mShareGen.mPrevSeed);
+    if (pIdx < 2 && len) GPU_CALL(aby3g_prng_i32(&rpos, len, 1, r.share(pIdx == 0 ? 0 : 1), g.stream()));
+    // 2) c = x + r
+    sbMatrix c;
+    bool_cipher_add(pIdx, boolInput, r, c, eval, runtime);
+    // 3) open c to P2, which reshares it
+    si64Matrix out(len, 1);
+    if (len)
+        runtime.noDependencies()
+            .then([&](CommPkg& comm, Sh3Task& self) {
+                aby3g_stream st = g.stream();
+                switch (pIdx) {
+                    case 0: {  // (-r, c - t)
+                        GPU_CALL(aby3g_prng_i32(&rpos, len, -1, out.share(0), st));
+                        auto f = comm.mPrev.asyncRecvDevice(out.share(1), b8, g);
+                        self.then([f](CommPkg&, Sh3Task&) { f.get(); });
+                        break;
+                    }
+                    case 1: {  // (t, -r)
+                        comm.mNext.asyncSendDevice(c.share(1), b8, g);
+                        GPU_CALL(aby3g_prng_i32(&rpos, len, -1, out.share(1), st));
+                        auto f = comm.mNext.asyncRecvDevice(out.share(0), b8, g);
+                        self.then([f](CommPkg&, Sh3Task&) { f.get(); });
+                        break;
+                    }
+                    case 2: {  // (c - t, t), t private to P2 (the reference's rand(), :580)
+                        auto recv = std::make_shared<DeviceBuffer>(g, b8);
+                        auto f = comm.mPrev.asyncRecvDevice(recv->data(), b8, g);
+                        self.then([&, f, recv](CommPkg& comm2, Sh3Task&) {
+                            f.get();
+                            static thread_local std::random_device rd;
+                            u8 seed[16];
+                            for (int k = 0; k < 4; ++k) {
+                                const u32 v = rd();
+                                std::memcpy(seed + 4 * k, &v, 4);
+                            }
+                            aby3g_stream st2 = g.stream();
+                            GPU_CALL(aby3g_prng_fill(seed, 0, b8, out.share(1), st2));
+                            GPU_CALL(aby3g_b2a_open(c.share(0), c.share(1), recv->as<i64>(), out.share(1), len,
+                                                    out.share(0), st2));
+                            comm2.mNext.asyncSendDevice(out.share(0), b8, g);
+                            comm2.mPrev.asyncSendDevice(out.share(1), b8, g);
+                        });
+                        break;
+                    }
+                    default:
+                        throw RTE_LOC;
+                }
+            })
+            .getClosure()
+            .get();
+    res = std::move(out);
 }
 
 }  // namespace aby3

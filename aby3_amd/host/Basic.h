@@ -52,6 +52,14 @@ void bool_cipher_max(int pIdx, const sbMatrix& A, const sbMatrix& B, sbMatrix& r
 void bool_cipher_min(int pIdx, const sbMatrix& A, const sbMatrix& B, sbMatrix& res, Sh3Evaluator& eval,
                      Sh3Runtime& runtime);
 
+// Boolean -> arithmetic (BoolBasic.cpp:517-593). One bit: the public-ones
+// product pi_cb_mul (zero shares from enc's generator). More bits (at most 64):
+// c = x + r with r = PRNG(P0's next seed).get<int32_t>() (P0 and P1 draw the
+// same r from a fresh PRNG of that seed), c opened to P2, which reshares it as
+// (c - t, t) with a private t; result shares (-r, t, c - t).
+void bool2arith(int pIdx, const sbMatrix& boolInput, si64Matrix& res, Sh3Encryptor& enc, Sh3Evaluator& eval,
+                Sh3Runtime& runtime);
+
 // ---- sort (Sort.cpp:327-437)
 // Batcher merge of two sorted arrays with the reference's round schedule.
 int odd_even_merge(const sbMatrix& data1, const sbMatrix& data2, sbMatrix& res, int pIdx, Sh3Evaluator& eval,

@@ -238,8 +238,12 @@ Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, const si64Matrix& A, const sbMatrix&
 }
 
 Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, i64 a, const sbMatrix& B, si64Matrix& C) {
+    return asyncMul(dep, a, B, C, mShareGen);
+}
+
+Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, i64 a, const sbMatrix& B, si64Matrix& C, Sh3ShareGen& zeroGen) {
     return dep
-        .then([this, a, &B, &C](CommPkg& comm, Sh3Task& self) {
+        .then([this, a, &B, &C, &zeroGen](CommPkg& comm, Sh3Task& self) {
             Gpu& g = self.getRuntime().gpu();
             if (B.bitCount() != 1) throw RTE_LOC;
             const u64 n = B.rows(), b8 = n * sizeof(i64);
@@ -248,7 +252,7 @@ Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, i64 a, const sbMatrix& B, si64Matrix
                 case 0: {  // (:430-447)
                     auto mn = std::make_shared<DeviceBuffer>(g, 2 * b8);
                     auto mp = std::make_shared<DeviceBuffer>(g, 2 * b8);
-                    aby3g_zero_share zs = mShareGen.zeroShare(mShareGen.takeDraws(n));
+                    aby3g_zero_share zs = zeroGen.zeroShare(zeroGen.takeDraws(n));
                     GPU_CALL(aby3g_pubmul_p0(a, B.data(), n, &zs, mOtNextKey.data(), mOtNextIdx, mOtPrevKey.data(),
                                              mOtPrevIdx, mn->as<i64>(), mp->as<i64>(), g.stream()));
                     mOtNextIdx += n;
@@ -267,7 +271,7 @@ Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, i64 a, const sbMatrix& B, si64Matrix
                 case 2: {  // (:452-487)
                     const bool p1 = self.getRuntime().mPartyIdx == 1;
                     auto help = std::make_shared<DeviceBuffer>(g, b8);
-                    aby3g_zero_share zs = mShareGen.zeroShare(mShareGen.takeDraws(n));
+                    aby3g_zero_share zs = zeroGen.zeroShare(zeroGen.takeDraws(n));
                     i64* mine = p1 ? C.share(1) : C.share(0);
                     const u8* key = p1 ? mOtNextKey.data() : mOtPrevKey.data();
                     u64& ctr = p1 ? mOtNextIdx : mOtPrevIdx;

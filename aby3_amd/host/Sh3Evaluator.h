@@ -51,6 +51,9 @@ public:
     Sh3Task asyncMul(Sh3Task dep, const si64Matrix& A, const sbMatrix& B, si64Matrix& C);
     // public i64 x shared bit (:418-501)
     Sh3Task asyncMul(Sh3Task dep, i64 a, const sbMatrix& B, si64Matrix& C);
+    // the same product with the zero shares drawn from `zeroGen` (pi_cb_mul,
+    // BuildingBlocks.cpp:334-391, draws them from the Encryptor's generator)
+    Sh3Task asyncMul(Sh3Task dep, i64 a, const sbMatrix& B, si64Matrix& C, Sh3ShareGen& zeroGen);
 
     TruncationPair getTruncationTuple(u64 rows, u64 cols, u64 d);
 

@@ -115,6 +115,8 @@ _SIGS = {
                                   c_void_p, c_void_p, c_void_p]),
     "aby3g_bitinj_send": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, POINTER(StreamPos), POINTER(StreamPos),
                                   c_u8p, c_uint64, c_u8p, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "aby3g_prng_i32": (c_int, [POINTER(StreamPos), c_uint64, c_int64, c_void_p, c_void_p]),
+    "aby3g_b2a_open": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p]),
     "aby3g_ot_help_bits": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_u8p, c_uint64, c_void_p, c_void_p]),
     "aby3g_ot_recv_bits": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_uint64, c_uint64, c_void_p,
                                    c_void_p]),

@@ -256,6 +256,14 @@ int aby3g_ot_help_bits(const int64_t* choice_rows, uint64_t rows, uint64_t cols6
 int aby3g_ot_recv_bits(const int64_t* msgs, const int64_t* mc, const int64_t* choice_rows, uint64_t rows,
                        uint64_t cols64, uint64_t bits, int64_t* out, aby3g_stream stream);
 
+/* bool2arith (aby3-Basic/BoolBasic.cpp:517-593): out[i] = scale * (i64) the
+ * i-th int32 of the PRNG stream from byte s->off (PRNG(seed).get<int32_t>(),
+ * sign-extended; :533-545 with scale 1, :562-569 with scale -1). */
+int aby3g_prng_i32(const aby3g_stream_pos* s, uint64_t n, int64_t scale, int64_t* out, aby3g_stream stream);
+/* bool2arith, party 2 (:573-587): out = (c0 ^ c1 ^ recv) - t. */
+int aby3g_b2a_open(const int64_t* c0, const int64_t* c1, const int64_t* recv, const int64_t* t, uint64_t n,
+                   int64_t* out, aby3g_stream stream);
+
 /* asyncMul(i64 a, sbMatrix B, C) party 0 (Sh3Evaluator.cpp:430-447):
  * s0[bb] = getShare(), s0[bb^1] = a + that, bb = B0^B1;
  * msgs_next = pads(ot_next_key, ctr_next) ^ s0; msgs_prev = pads(ot_prev_key, ctr_prev) ^ s0. */

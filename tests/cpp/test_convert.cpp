@@ -4,6 +4,7 @@
 // transposes, :285-353 arithmetic -> binary, :355-435 bit injection), with the
 // reference tests' converter seeds (gens[i].init(toBlock(i+1), toBlock(next+1)),
 // :314-316, :385-387).
+#include "Basic.h"
 #include "Sh3Converter.h"
 #include "harness.h"
 
@@ -162,6 +163,42 @@ static void bitInjection(u64 rows, u64 bits, bool twoRounds) {
             check(revealed[i * bits + j] == (((u64)x(i, j / 64) >> (j % 64)) & 1), "bitInjection revealed bit");
 }
 
+// bool2arith (BoolBasic.cpp:517-593): one bit through pi_cb_mul (shares
+// against the oracle's public-bit product with the Encryptor's zero shares),
+// 64 bits through the add / open-to-P2 path (revealed; P2's t is private
+// randomness, as the reference's rand(), so its shares are not reproducible).
+static void bool2arithTest(u64 rows, u64 bits) {
+    i64Matrix x = trimmed(randMat(rows, 1, rows * 3 + bits), bits);
+    ShareSink got;
+    std::vector<i64> revealed;
+    run3([&](harness::Party& p) {
+        sbMatrix X(rows, bits);
+        if (p.idx == 0)
+            p.enc.localBinMatrix(p.rt, x, X).get();
+        else
+            p.enc.remoteBinMatrix(p.rt, X).get();
+        si64Matrix Y;
+        bool2arith(p.idx, X, Y, p.enc, p.eval, p.rt);
+        check(Y.rows() == rows && Y.cols() == 1, "dest shape");
+        got.put(p.idx, Y);
+        i64Matrix r;
+        p.enc.revealAll(p.rt, Y, r).get();
+        if (p.idx == 0) revealed = r.mData;
+    });
+    check(revealed == x.mData, "bool2arith revealed value");
+    if (bits == 1) {
+        auto enc = orc::makeEncryptors(0);
+        auto ev = orc::makeEvaluators(1);
+        orc::Shared X = orc::shareBin(enc, 0, toOrc(x));
+        auto hyb = ev;
+        for (int p = 0; p < 3; ++p) hyb[p].gen = enc[p].gen;
+        got.expectEq(orc::mulPubBit(hyb, 1, X), "bool2arith (1 bit) shares");
+    } else {
+        // replicated consistency: party i's share 1 == party i-1's share 0
+        for (int p = 0; p < 3; ++p) check(got.s[p][1] == got.s[(p + 2) % 3][0], "bool2arith replicated shares");
+    }
+}
+
 int main() {
     test("packed_43x91 (Sh3_convert_sb64_sPackedBin_test)", [] { packedParity(43, 91); });
     test("packed_1x1", [] { packedParity(1, 1); });
@@ -176,5 +213,8 @@ int main() {
     test("bitinj_43x17_twoRounds", [] { bitInjection(43, 17, true); });
     test("bitinj_1000x64", [] { bitInjection(1000, 64, false); });
     test("bitinj_77x130_twoRounds", [] { bitInjection(77, 130, true); });
+    test("bool2arith_1000x64", [] { bool2arithTest(1000, 64); });
+    test("bool2arith_300x1 (pi_cb_mul)", [] { bool2arithTest(300, 1); });
+    test("bool2arith_5x64", [] { bool2arithTest(5, 64); });
     return g_failures ? 1 : 0;
 }

@@ -10,6 +10,7 @@
 #include <numeric>
 #include <thread>
 #include "Basic.h"
+#include "Sh3Converter.h"
 #include "aby3ML.h"
 
 namespace aby3 {
@@ -160,6 +161,88 @@ struct MsbJob : Job {
         o[ABY3H_INFO_AND_WORDS] = c->mAndCount * words;
         o[ABY3H_INFO_GATE_WORDS] = c->mGates.size() * words;
         o[ABY3H_INFO_GATE_BYTES] = gateBytes(*c) * padded;
+    }
+};
+
+// ---- share conversions (Sh3Converter.cpp) --------------------------------
+// seeds of the reference's converter tests (Sh3ConverterTests.cpp:314-316)
+struct ConvParty {
+    Sh3ShareGen gen;
+    Sh3Converter conv;
+    void init(PartyCtx& p) {
+        gen.init(toBlock(0, (u64)p.idx + 1), toBlock(0, (u64)(p.idx + 1) % 3 + 1));
+        conv.init(p.rt, gen);
+    }
+};
+
+// toBinaryMatrix(si64 -> sb) over rows x 1 values: one step = resharing +
+// 64-bit adder circuit (Sh3Converter.cpp:61-207)
+struct A2bJob : Job {
+    u64 rows;
+    i64Matrix a;
+    si64Matrix A[3];
+    sbMatrix R[3];
+    ConvParty cp[3];
+    explicit A2bJob(u64 r) : rows(r) { a = randomMat(rows, 1, 5, 0); }
+    void setup(PartyCtx& p) override {
+        A[p.idx].resize(rows, 1);
+        if (p.idx == 0)
+            p.enc.localIntMatrix(p.rt, a, A[0]).get();
+        else
+            p.enc.remoteIntMatrix(p.rt, A[p.idx]).get();
+        cp[p.idx].init(p);
+    }
+    void step(PartyCtx& p) override { cp[p.idx].conv.toBinaryMatrix(p.rt, A[p.idx], R[p.idx]).get(); }
+    bool check(PartyCtx& p) override {
+        i64Matrix r;
+        p.enc.revealAll(p.rt, R[p.idx], r).get();
+        return p.idx != 0 || r.mData == a.mData;
+    }
+    void info(double* o) override {
+        BetaCircuit* c = cp[0].conv.arithToBinCircuit(64);
+        const double words = std::ceil(rows / 64.0), padded = 32.0 * ((rows + 2047) / 2048);
+        o[ABY3H_INFO_MULTS_PER_STEP] = c->mAndCount * words;
+        o[ABY3H_INFO_AND_WORDS] = c->mAndCount * words;
+        o[ABY3H_INFO_GATE_WORDS] = c->mGates.size() * words;
+        o[ABY3H_INFO_GATE_BYTES] = gateBytes(*c) * padded;
+    }
+};
+
+// bitInjection(sb -> si64) of rows x bits: one step = the 3-party OTs of
+// every bit (Sh3Converter.cpp:209-370)
+struct BitInjJob : Job {
+    u64 rows, bits;
+    i64Matrix a;
+    sbMatrix A[3];
+    si64Matrix R[3];
+    ConvParty cp[3];
+    BitInjJob(u64 r, u64 b) : rows(r), bits(b) {
+        if (!bits || bits > 64) throw std::runtime_error("bitinj job: 1..64 bits");
+        a = randomMat(rows, 1, 6, 0);
+        if (bits < 64)
+            for (auto& v : a.mData) v &= (i64)((1ull << bits) - 1);
+    }
+    void setup(PartyCtx& p) override {
+        A[p.idx].resize(rows, bits);
+        if (p.idx == 0)
+            p.enc.localBinMatrix(p.rt, a, A[0]).get();
+        else
+            p.enc.remoteBinMatrix(p.rt, A[p.idx]).get();
+        cp[p.idx].init(p);
+    }
+    void step(PartyCtx& p) override { cp[p.idx].conv.bitInjection(p.rt, A[p.idx], R[p.idx]).get(); }
+    bool check(PartyCtx& p) override {
+        i64Matrix r;
+        p.enc.revealAll(p.rt, R[p.idx], r).get();
+        if (p.idx != 0) return true;
+        for (u64 i = 0; i < rows; ++i)
+            for (u64 j = 0; j < bits; ++j)
+                if ((u64)r(i, j) != (((u64)a(i, 0) >> j) & 1)) return false;
+        return true;
+    }
+    void info(double* o) override {
+        // one OT-based bit product per bit (the metric's unit for asyncMul(si64, sb))
+        o[ABY3H_INFO_MULTS_PER_STEP] = (double)rows * bits;
     }
 };
 
@@ -490,6 +573,8 @@ aby3h_session* aby3h_session_create(int job, const uint64_t* params, int nparams
                 s.job = std::make_unique<LrJob>(P(0, 1000000), P(1, 128), P(2, 256), P(3, 16), P(4, 11));
                 break;
             case ABY3H_JOB_MERGE_LAYER: s.job = std::make_unique<MergeLayerJob>(P(0, 1 << 20)); break;
+            case ABY3H_JOB_A2B: s.job = std::make_unique<A2bJob>(P(0, 1 << 20)); break;
+            case ABY3H_JOB_BITINJ: s.job = std::make_unique<BitInjJob>(P(0, 1 << 16), P(1, 64)); break;
             default: throw std::runtime_error("unknown job");
         }
         {

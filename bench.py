@@ -191,6 +191,29 @@ def extras(args, nt, dev, world, pg):
             "and_word_gates_per_s": world * 10 * info["and_words"] / dt,
             "est_full_merge_s": dt / 10 * 210,
         }
+    # share conversions, each checked on its revealed output
+    with nt.Session(nt.JOB_A2B, [1 << 20], devices=(dev,) * 3, probe=False) as s:
+        s.run(2)
+        dt = timed(s, 10, pg)
+        if not s.check():
+            raise SystemExit("bench: toBinaryMatrix output differs from the input")
+        info = s.info()
+        res["a2b"] = {
+            "workload": "Sh3Converter::toBinaryMatrix of 2^20 64-bit values (resharing + 64-bit adder circuit)",
+            "ms_per_conversion": dt / 10 * 1e3,
+            "values_per_s": world * 10 * (1 << 20) / dt,
+            "and_word_gates_per_s": world * 10 * info["and_words"] / dt,
+        }
+    with nt.Session(nt.JOB_BITINJ, [1 << 16, 64], devices=(dev,) * 3, probe=False) as s:
+        s.run(2)
+        dt = timed(s, 10, pg)
+        if not s.check():
+            raise SystemExit("bench: bitInjection output differs from the input bits")
+        res["bit_injection"] = {
+            "workload": "Sh3Converter::bitInjection of 2^16 x 64 bits (3-party OT per bit, one round + OT)",
+            "ms_per_conversion": dt / 10 * 1e3,
+            "bits_per_s": world * 10 * (1 << 16) * 64 / dt,
+        }
     return res
 
 

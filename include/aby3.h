@@ -39,7 +39,13 @@ enum {
     ABY3H_JOB_LR = 3,
     /* params: keys. One step = one compare-exchange layer of keys/2 pairs
      * of the merge network (Sort.cpp:366-398, fused cmp_swap circuit). */
-    ABY3H_JOB_MERGE_LAYER = 4
+    ABY3H_JOB_MERGE_LAYER = 4,
+    /* params: rows. One step = Sh3Converter::toBinaryMatrix of rows x 1
+     * 64-bit values (resharing + 64-bit adder, Sh3Converter.cpp:61-207). */
+    ABY3H_JOB_A2B = 5,
+    /* params: rows, bits (<= 64). One step = Sh3Converter::bitInjection of
+     * a rows x bits binary matrix (3-party OT per bit, :209-370). */
+    ABY3H_JOB_BITINJ = 6
 };
 
 /* info slots returned by aby3h_session_info */

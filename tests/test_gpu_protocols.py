@@ -112,6 +112,10 @@ def test_merge(gpu, lens):
     (nt.JOB_MSB, [1 << 20], 2),                         # C3 every row checked
     (nt.JOB_LR, [100000, 128, 256, 16, 11], 20),        # C4 shapes (dataset trimmed)
     (nt.JOB_MERGE_LAYER, [1 << 20], 2),                 # C5 one layer, 2^19 pairs
+    (nt.JOB_A2B, [1 << 20], 2),                         # toBinaryMatrix, every value checked
+    (nt.JOB_A2B, [1000], 3),                            # ragged rows
+    (nt.JOB_BITINJ, [1 << 16, 64], 2),                  # bitInjection, every bit checked
+    (nt.JOB_BITINJ, [777, 13], 3),                      # ragged rows, 13 bits
 ])
 def test_session_jobs(gpu, job, params, steps):
     with nt.Session(job, params, probe=False) as s:

@@ -156,6 +156,31 @@ def cpu_lr_ms(nt, iters):
     return secs / iters * 1e3
 
 
+def cpu_conversion_rates(nt):
+    """The oracle's toBinaryMatrix / bitInjection on this host (cpu_baseline legs
+    only): values/s and bits/s, three parties in sequence on one thread."""
+    import ctypes
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle as orc
+
+    u = ctypes.c_uint64
+    # the engine's A->B circuit for 64 bits is the one 64-bit adder (int_int_add)
+    args, keep = orc._cir_args(nt.circuit("int_int_add", 64))
+    f = orc.dll().orc_bench_a2b
+    f.restype = ctypes.c_double
+    a2b_n, a2b_reps = 1 << 20, 2
+    secs = f(*args, u(a2b_n), a2b_reps)
+    g = orc.dll().orc_bench_bitinj
+    g.restype = ctypes.c_double
+    bi_rows, bi_reps = 1 << 16, 2
+    secs2 = g(u(bi_rows), u(64), bi_reps)
+    if secs < 0 or secs2 < 0:
+        raise SystemExit("bench: oracle conversion baseline failed: " + orc.dll().orc_last_error().decode())
+    return (a2b_n * a2b_reps / secs, f"{a2b_reps} x toBinaryMatrix of {a2b_n} values"), \
+           (bi_rows * 64 * bi_reps / secs2, f"{bi_reps} x bitInjection of {bi_rows}x64 bits")
+
+
 def extras(args, nt, dev, world, pg):
     """C4 (one SGD_Logistic iteration, 10^6 x 128, B=256, D16) and C5 (one
     compare-exchange layer of the 2^20-key merge network), each checked."""
@@ -204,6 +229,15 @@ def extras(args, nt, dev, world, pg):
             "values_per_s": world * 10 * (1 << 20) / dt,
             "and_word_gates_per_s": world * 10 * info["and_words"] / dt,
         }
+    cpu_conv = None
+    if world == 1 and not args.no_cpu_baseline:
+        progress("conversion CPU baselines")
+        cpu_conv = cpu_conversion_rates(nt)
+        res["a2b"]["cpu_baseline"] = {
+            "value": cpu_conv[0][0], "unit": "values/s", "cores": 1, "kind": "port",
+            "sample": cpu_conv[0][1] + " (oracle restatement: AES-NI streams, bit-sliced adder, 3 parties on one thread)",
+        }
+        res["a2b"]["speedup_vs_cpu_baseline"] = res["a2b"]["values_per_s"] / cpu_conv[0][0]
     with nt.Session(nt.JOB_BITINJ, [1 << 16, 64], devices=(dev,) * 3, probe=False) as s:
         s.run(2)
         dt = timed(s, 10, pg)
@@ -214,6 +248,12 @@ def extras(args, nt, dev, world, pg):
             "ms_per_conversion": dt / 10 * 1e3,
             "bits_per_s": world * 10 * (1 << 16) * 64 / dt,
         }
+        if cpu_conv:
+            res["bit_injection"]["cpu_baseline"] = {
+                "value": cpu_conv[1][0], "unit": "bits/s", "cores": 1, "kind": "port",
+                "sample": cpu_conv[1][1] + " (oracle restatement: AES-NI OT pads, 3 parties on one thread)",
+            }
+            res["bit_injection"]["speedup_vs_cpu_baseline"] = res["bit_injection"]["bits_per_s"] / cpu_conv[1][0]
     return res
 
 

@@ -441,3 +441,62 @@ double orc_bench_lr(uint32_t wires, const uint32_t* gates, uint64_t ngates, cons
 }
 
 }  // extern "C"
+
+// CPU baselines of the share conversions (bench.py cpu_baseline legs for the
+// Sh3Converter lines): n random 64-bit values shared by party 0 (untimed),
+// then `reps` toBinaryMatrix calls (Sh3Converter.cpp:61-207, the adder circuit
+// passed in) / bitInjection calls (:209-370) of the three parties simulated in
+// sequence on one thread (no network). Return wall seconds.
+extern "C" double orc_bench_a2b(uint32_t wires, const uint32_t* gates, uint64_t ngates, const uint32_t* levels,
+                                uint64_t nlevels, const uint32_t* inWires, const uint32_t* inSizes, uint64_t nin,
+                                const uint32_t* outWires, const uint32_t* outSizes, uint64_t nout, uint64_t n,
+                                int reps) {
+    try {
+        Circuit c = toCircuit(wires, gates, ngates, levels, nlevels, inWires, inSizes, nin, outWires, outSizes, nout);
+        auto enc = makeEncryptors(0);
+        auto ev = makeEvaluators(1);
+        Mat a(n, 1);
+        u64 x = 0x2545F4914F6CDD1Dull;
+        for (u64 k = 0; k < n; ++k) {
+            x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+            a.v[k] = (i64)x;
+        }
+        Shared A = shareInt(enc, 0, a);
+        auto t0 = std::chrono::steady_clock::now();
+        for (int r = 0; r < reps; ++r) {
+            Shared res = toBinaryMatrix(ev, c, A, 64);
+            if (res[0].s[0].v.size() != n) throw std::runtime_error("a2b: result size");
+        }
+        auto t1 = std::chrono::steady_clock::now();
+        return std::chrono::duration<double>(t1 - t0).count();
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+extern "C" double orc_bench_bitinj(uint64_t rows, uint64_t bits, int reps) {
+    try {
+        if (!bits || bits > 64) throw std::runtime_error("bitinj: 1..64 bits");
+        auto enc = makeEncryptors(0);
+        auto ev = makeEvaluators(1);
+        Mat a(rows, 1);
+        u64 x = 0x9E3779B97F4A7C15ull;
+        for (u64 k = 0; k < rows; ++k) {
+            x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+            a.v[k] = bits < 64 ? (i64)(x & ((1ull << bits) - 1)) : (i64)x;
+        }
+        Shared A = shareBin(enc, 0, a);
+        auto cv = converterInit(ev);
+        auto t0 = std::chrono::steady_clock::now();
+        for (int r = 0; r < reps; ++r) {
+            Shared res = bitInjection(ev, cv, A, bits, false);
+            if (res[0].s[0].v.size() != rows * bits) throw std::runtime_error("bitinj: result size");
+        }
+        auto t1 = std::chrono::steady_clock::now();
+        return std::chrono::duration<double>(t1 - t0).count();
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return -1;
+    }
+}

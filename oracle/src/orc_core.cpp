@@ -631,15 +631,20 @@ Shared toBinaryMatrix(std::array<Party, 3>& ev, const Circuit& addCir, const Sha
         c0[p] = SMat(rows, cols64);
         c1[p] = SMat(rows, cols64);
     }
+    // P0 (:90-93) and P2 (:179-182) draw one stream word per element; the
+    // PRNG buffers whole blocks, so draw them in one call
+    std::vector<i64> r0(n), r2(n);
+    ev[0].gen.prev.get(r0.data(), 8 * n);
+    ev[2].gen.next.get(r2.data(), 8 * n);
     for (u64 e = 0; e < n; ++e) {
         // P0 (:90-106): r = prev stream word, x0 = ((in0 + in1) ^ r, r)
-        const u64 r = (u64)ev[0].gen.prev.getI64();
+        const u64 r = (u64)r0[e];
         c0[0].s[1].v[e] = (i64)(r & m(e));
         c0[0].s[0].v[e] = (i64)((((u64)x[0].s[0].v[e] + (u64)x[0].s[1].v[e]) ^ r) & m(e));
     }
     for (u64 e = 0; e < n; ++e) {
         // P2 (:179-194): x0 = (r, 0) with the same words, x1 = (0, in1)
-        c0[2].s[0].v[e] = (i64)((u64)ev[2].gen.next.getI64() & m(e));
+        c0[2].s[0].v[e] = (i64)((u64)r2[e] & m(e));
         c1[2].s[1].v[e] = (i64)((u64)x[2].s[1].v[e] & m(e));
         // P1 (:132-147): x0 = (0, P0's message), x1 = (in0, 0)
         c1[1].s[0].v[e] = (i64)((u64)x[1].s[0].v[e] & m(e));
@@ -663,8 +668,8 @@ Shared bitInjection(std::array<Party, 3>& ev, std::array<ConvParty, 3>& cv, cons
     // P2, sender (:319-363)
     std::vector<std::array<i64, 2>> m(n);
     {
-        for (u64 k = 0; k < n; ++k) d[2].s[0].v[k] = ev[2].gen.next.getI64();
-        for (u64 k = 0; k < n; ++k) d[2].s[1].v[k] = ev[2].gen.prev.getI64();
+        ev[2].gen.next.get(d[2].s[0].v.data(), 8 * n);  // mNextCommon.get(dest0) (:325)
+        ev[2].gen.prev.get(d[2].s[1].v.data(), 8 * n);  // mPrevCommon.get(dest1) (:326)
         auto c0 = choices(b[2].s[0]), c1 = choices(b[2].s[1]);
         for (u64 k = 0; k < n; ++k) {
             const u8 bb = c0[k] ^ c1[k];
@@ -677,10 +682,10 @@ Shared bitInjection(std::array<Party, 3>& ev, std::array<ConvParty, 3>& cv, cons
     if (!twoRounds) msgsTo1 = cv[2].ot02.send(m);               // P2 -> P1
     const auto ch0 = choices(b[0].s[0]), ch1 = choices(b[1].s[1]);  // P0's and P1's copy of share 0
     auto help1 = cv[1].ot12.help(ch1);                          // P1 -> P0 (:290)
-    for (u64 k = 0; k < n; ++k) d[1].s[0].v[k] = ev[1].gen.next.getI64();  // :291
+    ev[1].gen.next.get(d[1].s[0].v.data(), 8 * n);  // :291
     std::vector<i64> help0;
     if (!twoRounds) help0 = cv[0].ot02.help(ch0);                // P0 -> P1 (:269)
-    for (u64 k = 0; k < n; ++k) d[0].s[1].v[k] = ev[0].gen.prev.getI64();  // :274
+    ev[0].gen.prev.get(d[0].s[1].v.data(), 8 * n);  // :274
     d[0].s[0].v = ot_recv(msgsTo0, help1, ch0);                 // :255-258
     if (twoRounds)
         d[1].s[1] = d[0].s[0];                                  // :262, :312

@@ -9,13 +9,17 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from aby3_amd import native as nt  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--job", choices=["mul", "msb", "lr"], required=True)
+ap.add_argument("--job", choices=["mul", "msb", "lr", "a2b", "bitinj"], required=True)
 ap.add_argument("--steps", type=int, default=4)
 a = ap.parse_args()
 if a.job == "mul":
     s = nt.Session(nt.JOB_MUL_TRUNC, [1024, 1024, 1024, 16, 1], probe=False)
 elif a.job == "msb":
     s = nt.Session(nt.JOB_MSB, [1 << 20], probe=False)
+elif a.job == "a2b":
+    s = nt.Session(nt.JOB_A2B, [1 << 20], probe=False)
+elif a.job == "bitinj":
+    s = nt.Session(nt.JOB_BITINJ, [1 << 16, 64], probe=False)
 else:
     s = nt.Session(nt.JOB_LR, [100000, 128, 256, 16, 11], probe=False)
 s.run(a.steps)

@@ -62,6 +62,9 @@ __global__ void __launch_bounds__(kBlock, 4) k_a2b_reshare(const u32* __restrict
 // bitInjection, sender P2 (Sh3Converter.cpp:319-361): d0 = next word
 // (nw0 + k), d1 = prev word (pw0 + k); b = bit k of in0 ^ in1;
 // m[c] = -d0 - d1 + (c ^ b); msgs_x[k] = pad(key_x, ctr_x + k) ^ m.
+// One thread per next-stream block: its two words are bits k and k + 1, so
+// each stream block is encrypted once (the prev stream's two words share a
+// block too when both offsets have the same parity, the usual case).
 __global__ void __launch_bounds__(kBlock, 4) k_bitinj_send(const u32* __restrict__ T0g, const i64* __restrict__ in0,
                                                           const i64* __restrict__ in1, u64 n, u64 bits, u64 cols64,
                                                           AesKey kn, u64 nw0, AesKey kp, u64 pw0, AesKey ka, u64 ca,
@@ -71,22 +74,42 @@ __global__ void __launch_bounds__(kBlock, 4) k_bitinj_send(const u32* __restrict
     __shared__ u32 lds[kAesLdsWords];
     aes_fill_lds(lds, T0g);
     const u32 lane32 = threadIdx.x & 31;
-    for (u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (u64)gridDim.x * blockDim.x) {
-        const u32 b = packed_bit(in0, k, bits, cols64) ^ packed_bit(in1, k, bits, cols64);
+    const bool sameParity = ((nw0 ^ pw0) & 1) == 0;
+    const u64 c_first = nw0 >> 1, c_last = (nw0 + n - 1) >> 1;
+    for (u64 c = c_first + (u64)blockIdx.x * blockDim.x + threadIdx.x; c <= c_last;
+         c += (u64)gridDim.x * blockDim.x) {
+        const u64 kbase = 2 * c - nw0;  // bit of word 2c (wraps to ~0 when nw0 is odd and c == c_first)
+        const u64 pwb = pw0 + kbase;    // prev word of that bit
         u64 nv[2], pv[2];
-        aes_ctr_block2(lds, lane32, kn, (nw0 + k) >> 1, kp, (pw0 + k) >> 1, nv[0], nv[1], pv[0], pv[1]);
-        const u64 x0 = nv[(nw0 + k) & 1], x1 = pv[(pw0 + k) & 1];
-        d0[k] = (i64)x0;
-        d1[k] = (i64)x1;
-        const u64 base = 0 - x0 - x1;
-        const u64 m0 = base + b, m1 = base + (b ^ 1);
-        u64 alo, ahi, blo, bhi;
-        aes_ctr_block2(lds, lane32, ka, ca + k, kb, cb + k, alo, ahi, blo, bhi);
-        msgs_a[2 * k] = (i64)(alo ^ m0);
-        msgs_a[2 * k + 1] = (i64)(ahi ^ m1);
-        if (have_b) {
-            msgs_b[2 * k] = (i64)(blo ^ m0);
-            msgs_b[2 * k + 1] = (i64)(bhi ^ m1);
+        if (sameParity) {
+            aes_ctr_block2(lds, lane32, kn, c, kp, pwb >> 1, nv[0], nv[1], pv[0], pv[1]);
+        } else {  // prev words pwb (odd) and pwb + 1 straddle two blocks
+            u64 alo, ahi, blo, bhi;
+            aes_ctr_block(lds, lane32, kn, c, nv[0], nv[1]);
+            aes_ctr_block2(lds, lane32, kp, pwb >> 1, kp, (pwb >> 1) + 1, alo, ahi, blo, bhi);
+            pv[0] = ahi;
+            pv[1] = blo;
+        }
+#pragma unroll
+        for (u32 h = 0; h < 2; ++h) {
+            const u64 k = kbase + h;
+            if (k >= n) continue;
+            const u32 b = packed_bit(in0, k, bits, cols64) ^ packed_bit(in1, k, bits, cols64);
+            const u64 x0 = nv[h], x1 = pv[h];
+            d0[k] = (i64)x0;
+            d1[k] = (i64)x1;
+            const u64 base = 0 - x0 - x1;
+            const u64 m0 = base + b, m1 = base + (b ^ 1);
+            u64 alo, ahi, blo, bhi;
+            if (have_b) {
+                aes_ctr_block2(lds, lane32, ka, ca + k, kb, cb + k, alo, ahi, blo, bhi);
+                msgs_b[2 * k] = (i64)(blo ^ m0);
+                msgs_b[2 * k + 1] = (i64)(bhi ^ m1);
+            } else {
+                aes_ctr_block(lds, lane32, ka, ca + k, alo, ahi);
+            }
+            msgs_a[2 * k] = (i64)(alo ^ m0);
+            msgs_a[2 * k + 1] = (i64)(ahi ^ m1);
         }
     }
 }
@@ -184,7 +207,8 @@ int aby3g_bitinj_send(const int64_t* in, uint64_t rows, uint64_t cols64, uint64_
         if (!n) return;
         AesKey kn = expand_key(next->seed), kp = expand_key(prev->seed), ka = expand_key(key_a);
         AesKey kb = msgs_b ? expand_key(key_b) : ka;
-        launch(PROBE_AES, k_bitinj_send, dim3(aes_grid(n, kBlock)), dim3(kBlock), 0, S(stream), aes_table(), in,
+        const u64 nw0 = next->off / 8, items = ((nw0 + n - 1) >> 1) - (nw0 >> 1) + 1;
+        launch(PROBE_AES, k_bitinj_send, dim3(aes_grid(items, kBlock)), dim3(kBlock), 0, S(stream), aes_table(), in,
                in + rows * cols64, n, bits, cols64, kn, next->off / 8, kp, prev->off / 8, ka, ctr_a, kb, ctr_b,
                (int)(msgs_b != nullptr), dest, dest + n, msgs_a, msgs_b);
     });

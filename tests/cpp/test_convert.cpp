@@ -163,6 +163,45 @@ static void bitInjection(u64 rows, u64 bits, bool twoRounds) {
             check(revealed[i * bits + j] == (((u64)x(i, j / 64) >> (j % 64)) & 1), "bitInjection revealed bit");
 }
 
+// toBinaryMatrix of an odd number of words advances only P0's prev / P2's
+// next stream, so the bitInjection that follows sees the two streams at
+// offsets of different parity (the sender kernel's straddling path).
+static void a2bThenBitInjection(u64 rows, u64 bits) {
+    i64Matrix x = randMat(rows, 1, 4242 + rows);
+    i64Matrix xb = trimmed(randMat(rows, 1, 4343 + rows), bits);
+    ShareSink gotB, gotI;
+    BetaCircuit cir;
+    Sh3Converter::buildArithToBinCircuit(cir, 64, 64);
+    cir.levelByAndDepth();
+    run3([&](harness::Party& p) {
+        si64Matrix X(rows, 1);
+        sbMatrix XB(rows, bits);
+        if (p.idx == 0) {
+            p.enc.localIntMatrix(p.rt, x, X).get();
+            p.enc.localBinMatrix(p.rt, xb, XB).get();
+        } else {
+            p.enc.remoteIntMatrix(p.rt, X).get();
+            p.enc.remoteBinMatrix(p.rt, XB).get();
+        }
+        Sh3ShareGen gen;
+        gen.init(convPrevSeed(p.idx), convNextSeed(p.idx));
+        Sh3Converter conv;
+        conv.init(p.rt, gen);
+        sbMatrix Y;
+        conv.toBinaryMatrix(p.rt.noDependencies(), X, Y).get();
+        si64Matrix Z;
+        conv.bitInjection(p.rt.noDependencies(), XB, Z).get();
+        gotB.put(p.idx, Y);
+        gotI.put(p.idx, Z);
+    });
+    auto enc = orc::makeEncryptors(0);
+    auto gens = orcConvGens();
+    orc::Shared X = orc::shareInt(enc, 0, toOrc(x)), XB = orc::shareBin(enc, 0, toOrc(xb));
+    auto cv = orc::converterInit(gens);
+    gotB.expectEq(orc::toBinaryMatrix(gens, toOrc(cir), X, 64), "toBinaryMatrix shares");
+    gotI.expectEq(orc::bitInjection(gens, cv, XB, bits, false), "bitInjection shares after it");
+}
+
 // bool2arith (BoolBasic.cpp:517-593): one bit through pi_cb_mul (shares
 // against the oracle's public-bit product with the Encryptor's zero shares),
 // 64 bits through the add / open-to-P2 path (revealed; P2's t is private
@@ -213,6 +252,8 @@ int main() {
     test("bitinj_43x17_twoRounds", [] { bitInjection(43, 17, true); });
     test("bitinj_1000x64", [] { bitInjection(1000, 64, false); });
     test("bitinj_77x130_twoRounds", [] { bitInjection(77, 130, true); });
+    test("a2b_333_then_bitinj_21x7 (stream parities differ)", [] { a2bThenBitInjection(333, 7); });
+    test("a2b_334_then_bitinj_21x7", [] { a2bThenBitInjection(334, 7); });
     test("bool2arith_1000x64", [] { bool2arithTest(1000, 64); });
     test("bool2arith_300x1 (pi_cb_mul)", [] { bool2arithTest(300, 1); });
     test("bool2arith_5x64", [] { bool2arithTest(5, 64); });

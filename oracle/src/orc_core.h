@@ -14,6 +14,7 @@
 #pragma once
 #include "orc_aes.h"
 #include <array>
+#include <cstring>
 #include <vector>
 #include <string>
 #include <stdexcept>
@@ -31,8 +32,30 @@ namespace orc {
 struct Stream {  // oc::PRNG restated as (key, byte offset)
     u8 seed[16];
     u64 off = 0;
-    void init(const u8 s[16]) { std::copy(s, s + 16, seed); off = 0; }
-    void get(void* dst, u64 nbytes) { prng_bytes(seed, off, nbytes, (u8*)dst); off += nbytes; }
+    // the current block under the expanded key: small draws cost one AES-NI
+    // block per 16 bytes, as the reference's buffered PRNG (PRNG.cpp refill)
+    AesNI aes;
+    Block cur{};
+    u64 curIdx = ~0ull;
+    void init(const u8 s[16]) {
+        std::copy(s, s + 16, seed);
+        off = 0;
+        aes.setKey(seed);
+        curIdx = ~0ull;
+    }
+    void get(void* dst, u64 nbytes) {
+        const u64 b = off / 16;
+        if (nbytes <= 16 - off % 16 && aesni_available()) {
+            if (b != curIdx) {
+                cur = aes.encrypt(toBlock(b));
+                curIdx = b;
+            }
+            std::memcpy(dst, reinterpret_cast<const u8*>(&cur) + off % 16, nbytes);
+        } else {
+            prng_bytes(seed, off, nbytes, (u8*)dst);
+        }
+        off += nbytes;
+    }
     Block getBlock() { Block b; get(&b, 16); return b; }
     i64 getI64() { i64 v; get(&v, 8); return v; }
 };

@@ -43,3 +43,8 @@ def test_binary_protocols_gpu():
 @pytest.mark.gpu
 def test_convert_protocols_gpu():
     _run("test_convert", 600)
+
+
+def test_convert_oracle_revealed():
+    # the oracle's share conversions against the reference tests' revealed checks (CPU)
+    _run("test_convert_oracle", 120)

@@ -352,6 +352,113 @@ __global__ void __launch_bounds__(256) k_wires_to_bits_tiled(const u64* __restri
     }
 }
 
+// Row p of a merge round's compare-exchange list -> row of the merge array
+// (aby3g_rowmap). 32-bit division whenever the operands fit.
+__device__ __forceinline__ u64 map_row(const aby3g_rowmap& m, u64 p) {
+    const u64 q = m.first + p;
+    if (m.idx) return m.idx[q];
+    u64 rep, k;
+    if (((q | m.per_rep) >> 32) == 0) {
+        const u32 qq = (u32)q, pr = (u32)m.per_rep, r32 = qq / pr;
+        rep = r32;
+        k = qq - r32 * pr;
+    } else {
+        rep = q / m.per_rep;
+        k = q - rep * m.per_rep;
+    }
+    return m.start + rep * m.rep_stride + k * m.step;
+}
+
+// k_bits_to_wires_tiled over mapped source rows (the round's gather fused
+// into setInput). Rows mapped outside the source read as zero.
+__global__ void __launch_bounds__(256) k_bits_to_wires_map(const i64* __restrict__ in, u64 inRows, u64 cols64,
+                                                           u32 nbits, aby3g_rowmap map, u64 rows,
+                                                           u64* __restrict__ wrows, u64 shareStride, u64 words) {
+    __shared__ u64 tile[64 * kTilePitch];
+    in += (u64)blockIdx.y * inRows * cols64;
+    wrows += (u64)blockIdx.y * shareStride;
+    const u64 tilesPerCol = (words + kTileWords - 1) / kTileWords;
+    const u64 c = blockIdx.x / tilesPerCol, w0 = (blockIdx.x % tilesPerCol) * kTileWords;
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    u64 vv[16];
+#pragma unroll
+    for (u32 k = 0; k < 16; ++k) {
+        const u32 wl = wave * 16 + k;
+        const u64 r = (w0 + wl) * 64 + lane;
+        u64 v = 0;
+        if (w0 + wl < words && r < rows) {
+            const u64 src = map_row(map, r);
+            if (src < inRows) v = (u64)in[src * cols64 + c];
+        }
+        vv[k] = v;
+    }
+    for (u32 k = 0; k < 16; ++k) {
+        const u32 wl = wave * 16 + k;
+        tile[lane * kTilePitch + wl] = transpose64(vv[k], lane);
+    }
+    __syncthreads();
+    for (u32 idx = threadIdx.x; idx < 64 * kTileWords; idx += 256) {
+        const u32 b = idx / kTileWords, wl = idx % kTileWords;
+        const u64 bit = c * 64 + b;
+        if (bit < nbits && w0 + wl < words) wrows[bit * words + w0 + wl] = tile[b * kTilePitch + wl];
+    }
+}
+
+// k_wires_to_bits_tiled scattering circuit row p to row map(p) of `out`
+// (the round's scatter fused into getOutput).
+__global__ void __launch_bounds__(256) k_wires_to_bits_map(const u64* __restrict__ mem, u64 shareStride,
+                                                           const u32* __restrict__ wires, u32 nbits, u64 words,
+                                                           i64* __restrict__ out, u64 outRows, aby3g_rowmap map,
+                                                           u64 rows) {
+    __shared__ u64 tile[64 * kTilePitch];
+    const u64 cols = (nbits + 63) / 64;
+    mem += (u64)blockIdx.y * shareStride;
+    out += (u64)blockIdx.y * outRows * cols;
+    const u64 rw = (rows + 63) / 64;
+    const u64 tilesPerCol = (rw + kTileWords - 1) / kTileWords;
+    const u64 c = blockIdx.x / tilesPerCol, w0 = (blockIdx.x % tilesPerCol) * kTileWords;
+    u64 vv[16];
+#pragma unroll
+    for (u32 j = 0; j < 16; ++j) {
+        const u32 idx = threadIdx.x + 256 * j, b = idx / kTileWords, wl = idx % kTileWords;
+        const u64 bit = c * 64 + b;
+        vv[j] = (bit < nbits && w0 + wl < rw) ? mem[(u64)wires[bit] * words + w0 + wl] : 0;
+    }
+#pragma unroll
+    for (u32 j = 0; j < 16; ++j) {
+        const u32 idx = threadIdx.x + 256 * j;
+        tile[(idx / kTileWords) * kTilePitch + idx % kTileWords] = vv[j];
+    }
+    __syncthreads();
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (u32 k = 0; k < 16; ++k) {
+        const u32 wl = wave * 16 + k;
+        const u64 mine = transpose64(tile[lane * kTilePitch + wl], lane);
+        const u64 row = (w0 + wl) * 64 + lane;
+        if (w0 + wl < rw && row < rows) {
+            const u64 dst = map_row(map, row);
+            if (dst < outRows) out[dst * cols + c] = (i64)mine;
+        }
+    }
+}
+
+// Largest row an affine map reaches over p < rows (strides are unsigned, so
+// the maximum is at the last element of the last or the next-to-last rep).
+static u64 affine_max_row(const aby3g_rowmap& m, u64 rows) {
+    const u64 q0 = m.first, q1 = m.first + rows - 1;
+    const u64 r0 = q0 / m.per_rep, r1 = q1 / m.per_rep;
+    u64 mx = m.start + r1 * m.rep_stride + (q1 % m.per_rep) * m.step;
+    if (r1 > r0) mx = std::max(mx, m.start + (r1 - 1) * m.rep_stride + (m.per_rep - 1) * m.step);
+    return mx;
+}
+
+static void check_map(const aby3g_rowmap* map, u64 rows, u64 limit) {
+    ABY3G_REQUIRE(map != nullptr, "null row map");
+    if (map->idx || !rows) return;  // explicit maps: out-of-range rows are skipped by the kernels
+    ABY3G_REQUIRE(map->per_rep > 0, "row map: per_rep must be positive");
+    ABY3G_REQUIRE(affine_max_row(*map, rows) < limit, "row map reaches past the matrix");
+}
+
 }  // namespace
 
 }  // namespace aby3g
@@ -468,6 +575,33 @@ int aby3g_wires_to_bits2(const uint64_t* mem, uint64_t share_stride, const uint3
         const u64 tiles = (((rows + 63) / 64 + kTileWords - 1) / kTileWords) * ((nbits + 63) / 64);
         launch(PROBE_OTHER, k_wires_to_bits_tiled, dim3((u32)tiles, 2), dim3(256), 0, S(stream), mem, share_stride,
                wires, nbits, words, out, rows);
+    });
+}
+
+int aby3g_bits_to_wires_map(const int64_t* in, uint64_t in_rows, uint64_t cols64, uint32_t nbits,
+                            const aby3g_rowmap* map, uint64_t rows, uint64_t* wire_rows, uint64_t share_stride,
+                            uint64_t words, aby3g_stream stream) {
+    return guarded([&] {
+        ABY3G_REQUIRE(nbits <= cols64 * 64, "nbits exceeds input columns");
+        ABY3G_REQUIRE(words * 64 >= rows, "words too small for rows");
+        check_map(map, rows, in_rows);
+        if (!nbits || !words) return;
+        const u64 tiles = ((words + kTileWords - 1) / kTileWords) * ((nbits + 63) / 64);
+        launch(PROBE_OTHER, k_bits_to_wires_map, dim3((u32)tiles, 2), dim3(256), 0, S(stream), in, (u64)in_rows,
+               (u64)cols64, nbits, *map, (u64)rows, wire_rows, (u64)share_stride, (u64)words);
+    });
+}
+
+int aby3g_wires_to_bits_map(const uint64_t* mem, uint64_t share_stride, const uint32_t* wires, uint32_t nbits,
+                            uint64_t words, int64_t* out, uint64_t out_rows, const aby3g_rowmap* map, uint64_t rows,
+                            aby3g_stream stream) {
+    return guarded([&] {
+        ABY3G_REQUIRE(words * 64 >= rows, "words too small for rows");
+        check_map(map, rows, out_rows);
+        if (!nbits || !rows) return;
+        const u64 tiles = (((rows + 63) / 64 + kTileWords - 1) / kTileWords) * ((nbits + 63) / 64);
+        launch(PROBE_OTHER, k_wires_to_bits_map, dim3((u32)tiles, 2), dim3(256), 0, S(stream), mem,
+               (u64)share_stride, wires, nbits, (u64)words, out, (u64)out_rows, *map, (u64)rows);
     });
 }
 

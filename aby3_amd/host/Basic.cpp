@@ -138,96 +138,6 @@ void bool_cipher_min(int pIdx, const sbMatrix& A, const sbMatrix& B, sbMatrix& r
     bool_cipher_max_min_split(pIdx, A, B, mx, res, eval, runtime);
 }
 
-// gather rows idx of a 64-bit sbMatrix (both shares)
-static void gatherRows(const sbMatrix& src, const std::vector<u32>& idx, sbMatrix& dst, Gpu& g) {
-    const u64 n = idx.size(), R = src.rows();
-    dst.resize(n, 64);
-    DeviceBuffer di(g, n * 4);
-    toDevice(di.data(), idx.data(), n * 4, g);
-    for (int s = 0; s < 2; ++s)
-        GPU_CALL(aby3g_u64_gather(n, di.as<u32>(), (const u64*)src.share(s), (u64*)dst.share(s), g.stream()));
-    (void)R;
-}
-static void scatterRows(const sbMatrix& src, const std::vector<u32>& idx, sbMatrix& dst, Gpu& g) {
-    const u64 n = idx.size();
-    DeviceBuffer di(g, n * 4);
-    toDevice(di.data(), idx.data(), n * 4, g);
-    for (int s = 0; s < 2; ++s)
-        GPU_CALL(aby3g_u64_scatter(n, di.as<u32>(), (const u64*)src.share(s), (u64*)dst.share(s), g.stream()));
-}
-
-int odd_even_merge(const sbMatrix& data1, const sbMatrix& data2, sbMatrix& res, int pIdx, Sh3Evaluator& eval,
-                   Sh3Runtime& runtime) {
-    // Sort.cpp:327-406
-    Gpu& g = runtime.gpu();
-    const u64 L1 = data1.rows(), L2 = data2.rows(), length = std::max(L1, L2);
-    if (data1.bitCount() != 64 || data2.bitCount() != 64) throw std::runtime_error("64-bit keys expected");
-    // pad with max(last1, last2)
-    std::vector<u32> i1{(u32)(L1 - 1)}, i2{(u32)(L2 - 1)};
-    sbMatrix max1, max2, maxEle;
-    gatherRows(data1, i1, max1, g);
-    gatherRows(data2, i2, max2, g);
-    bool_cipher_max(pIdx, max1, max2, maxEle, eval, runtime);
-    sbMatrix result(2 * length, 64);
-    {
-        std::vector<u32> zeros(2 * length, 0);
-        gatherRows(maxEle, zeros, result, g);
-        std::vector<u32> even(L1), odd(L2);
-        for (u64 i = 0; i < L1; ++i) even[i] = (u32)(2 * i);
-        for (u64 i = 0; i < L2; ++i) odd[i] = (u32)(2 * i + 1);
-        scatterRows(data1, even, result, g);
-        scatterRows(data2, odd, result, g);
-    }
-    size_t t = (size_t)std::ceil(std::log2((double)length) + 1);
-    size_t q = (size_t)1 << (t - 1);
-    size_t d = 1, r = 0;
-    while (d > 0) {
-        std::vector<u32> xm, ym;
-        for (size_t i = r; i + d < 2 * length; i += 2) {
-            xm.push_back((u32)i);
-            ym.push_back((u32)(i + d));
-        }
-        if (!xm.empty()) {
-            sbMatrix X, Y, mx, mn;
-            gatherRows(result, xm, X, g);
-            gatherRows(result, ym, Y, g);
-            bool_cipher_max_min_split(pIdx, X, Y, mx, mn, eval, runtime);
-            scatterRows(mn, xm, result, g);
-            scatterRows(mx, ym, result, g);
-        }
-        d = q - 1;
-        q >>= 1;
-        r = 1;
-    }
-    std::vector<u32> head(L1 + L2);
-    for (u64 i = 0; i < L1 + L2; ++i) head[i] = (u32)i;
-    gatherRows(result, head, res, g);
-    return 0;
-}
-
-int odd_even_multi_merge(std::vector<sbMatrix>& data, sbMatrix& sorted, int pIdx, Sh3Evaluator& eval,
-                         Sh3Runtime& runtime) {
-    // Sort.cpp:413-437
-    size_t k = data.size();
-    while (k != 1) {
-        if (k % 2) {
-            sbMatrix res;
-            odd_even_merge(data[k - 2], data[k - 1], res, pIdx, eval, runtime);
-            data[k - 2] = std::move(res);
-            k -= 1;
-        } else {
-            for (size_t i = 0; i < k; i += 2) {
-                sbMatrix res;
-                odd_even_merge(data[i], data[i + 1], res, pIdx, eval, runtime);
-                data[i / 2] = std::move(res);
-            }
-            k >>= 1;
-        }
-    }
-    sorted = std::move(data[0]);
-    return 0;
-}
-
 }  // namespace aby3
 
 namespace aby3 {

@@ -5,6 +5,7 @@
 #include "Sh3BinaryEvaluator.h"
 #include "Sh3Encryptor.h"
 #include "Sh3Evaluator.h"
+#include "Sort.h"
 
 namespace aby3 {
 
@@ -60,12 +61,7 @@ void bool_cipher_min(int pIdx, const sbMatrix& A, const sbMatrix& B, sbMatrix& r
 void bool2arith(int pIdx, const sbMatrix& boolInput, si64Matrix& res, Sh3Encryptor& enc, Sh3Evaluator& eval,
                 Sh3Runtime& runtime);
 
-// ---- sort (Sort.cpp:327-437)
-// Batcher merge of two sorted arrays with the reference's round schedule.
-int odd_even_merge(const sbMatrix& data1, const sbMatrix& data2, sbMatrix& res, int pIdx, Sh3Evaluator& eval,
-                   Sh3Runtime& runtime);
-int odd_even_multi_merge(std::vector<sbMatrix>& data, sbMatrix& sorted, int pIdx, Sh3Evaluator& eval,
-                         Sh3Runtime& runtime);
+// ---- sort: Sort.h (odd_even_merge, odd_even_multi_merge, high_dimensional_*)
 
 // Evaluate one library circuit on sbMatrix inputs (shared helper).
 void evalCircuit(BetaCircuit* cir, const std::vector<const sbMatrix*>& in, const std::vector<sbMatrix*>& out,

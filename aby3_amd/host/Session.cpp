@@ -335,75 +335,50 @@ struct LrJob : Job {
     void info(double* o) override { o[ABY3H_INFO_MULTS_PER_STEP] = 2.0 * B * d; }
 };
 
-// ---- C5: one compare-exchange layer of the merge network ------------------
-struct MergeLayerJob : Job {
-    u64 keys;
+// ---- C5: odd-even merge sort of `keys` 64-bit keys ------------------------
+struct SortJob : Job {
+    u64 n;
     i64Matrix k;
-    sbMatrix S[3], X[3], Y[3], Mn[3], Mx[3];
+    sbMatrix S[3], R[3];
     CircuitLibrary lib;
-    std::vector<u32> xi, yi;
-    DeviceBuffer dx[3], dy[3];
-    explicit MergeLayerJob(u64 n) : keys(n) {
-        k.resize(keys, 1);
+    explicit SortJob(u64 keys) : n(keys) {
+        if (!n || n > (1ull << 20)) throw std::runtime_error("sort job: 1 .. 2^20 keys");
+        // distinct keys below 2^63, the low 20 bits an index tag (tag_append,
+        // BoolBasic.cpp:992-1004): signed and unsigned order agree
+        k.resize(n, 1);
         u64 x = 7;
-        for (u64 i = 0; i < keys; ++i) k(i, 0) = (i64)(((xorshift(x) % (1ull << 43)) << 20) | i);
-        for (u64 i = 0; i + 1 < keys; i += 2) {
-            xi.push_back((u32)i);
-            yi.push_back((u32)(i + 1));
-        }
+        for (u64 i = 0; i < n; ++i) k(i, 0) = (i64)(((xorshift(x) % (1ull << 43)) << 20) | i);
     }
     void setup(PartyCtx& p) override {
-        S[p.idx].resize(keys, 64);
+        S[p.idx].resize(n, 64);
         if (p.idx == 0)
             p.enc.localBinMatrix(p.rt, k, S[0]).get();
         else
             p.enc.remoteBinMatrix(p.rt, S[p.idx]).get();
-        Gpu& g = p.rt.gpu();
-        const u64 m = xi.size();
-        dx[p.idx].reset(g, m * 4);
-        dy[p.idx].reset(g, m * 4);
-        toDevice(dx[p.idx].data(), xi.data(), m * 4, g);
-        toDevice(dy[p.idx].data(), yi.data(), m * 4, g);
-        g.sync();
     }
-    void step(PartyCtx& p) override {
-        Gpu& g = p.rt.gpu();
-        const u64 m = xi.size();
-        DeviceBuffer &dx = this->dx[p.idx], &dy = this->dy[p.idx];
-        sbMatrix &s = S[p.idx], &x = X[p.idx], &y = Y[p.idx];
-        x.resize(m, 64);
-        y.resize(m, 64);
-        for (int sh = 0; sh < 2; ++sh) {
-            GPU_CALL(aby3g_u64_gather(m, dx.as<u32>(), (const u64*)s.share(sh), (u64*)x.share(sh), g.stream()));
-            GPU_CALL(aby3g_u64_gather(m, dy.as<u32>(), (const u64*)s.share(sh), (u64*)y.share(sh), g.stream()));
-        }
-        bool_cipher_max_min_split(p.idx, x, y, Mx[p.idx], Mn[p.idx], p.eval, p.rt);
-        for (int sh = 0; sh < 2; ++sh) {
-            GPU_CALL(aby3g_u64_scatter(m, dx.as<u32>(), (const u64*)Mn[p.idx].share(sh), (u64*)s.share(sh), g.stream()));
-            GPU_CALL(aby3g_u64_scatter(m, dy.as<u32>(), (const u64*)Mx[p.idx].share(sh), (u64*)s.share(sh), g.stream()));
-        }
-    }
-    // after any number of layers over the same pairs: every pair ordered
-    // (signed), and the keys a permutation of the input (the layer is idempotent)
+    void step(PartyCtx& p) override { odd_even_merge_sort(S[p.idx], R[p.idx], p.idx, p.eval, p.rt); }
+    // every key, in order: the revealed output equals std::sort of the input
     bool check(PartyCtx& p) override {
         i64Matrix r;
-        p.enc.revealAll(p.rt, S[p.idx], r).get();
+        p.enc.revealAll(p.rt, R[p.idx], r).get();
         if (p.idx != 0) return true;
-        for (u64 i = 0; i < xi.size(); ++i)
-            if (r(xi[i], 0) > r(yi[i], 0)) return false;
-        std::vector<i64> a(r.mData), b(k.mData);
-        std::sort(a.begin(), a.end());
+        std::vector<i64> b(k.mData);
         std::sort(b.begin(), b.end());
-        return a == b;
+        return r.mData == b;
     }
     void info(double* o) override {
         BetaCircuit* c = lib.cmp_swap(64);
-        const u64 m = keys / 2;
-        const double words = std::ceil(m / 64.0), padded = 32.0 * ((m + 2047) / 2048);
-        o[ABY3H_INFO_MULTS_PER_STEP] = c->mAndCount * words;
-        o[ABY3H_INFO_AND_WORDS] = c->mAndCount * words;
-        o[ABY3H_INFO_GATE_WORDS] = c->mGates.size() * words;
-        o[ABY3H_INFO_GATE_BYTES] = gateBytes(*c) * padded;
+        double andW = 0, gateW = 0, bytes = 0;
+        for (u64 rows : multiMergeEvalRows(std::vector<u64>(n, 1))) {
+            const double words = std::ceil(rows / 64.0), padded = 32.0 * ((rows + 2047) / 2048);
+            andW += c->mAndCount * words;
+            gateW += c->mGates.size() * words;
+            bytes += gateBytes(*c) * padded;
+        }
+        o[ABY3H_INFO_MULTS_PER_STEP] = andW;
+        o[ABY3H_INFO_AND_WORDS] = andW;
+        o[ABY3H_INFO_GATE_WORDS] = gateW;
+        o[ABY3H_INFO_GATE_BYTES] = bytes;
     }
 };
 
@@ -572,7 +547,7 @@ aby3h_session* aby3h_session_create(int job, const uint64_t* params, int nparams
             case ABY3H_JOB_LR:
                 s.job = std::make_unique<LrJob>(P(0, 1000000), P(1, 128), P(2, 256), P(3, 16), P(4, 11));
                 break;
-            case ABY3H_JOB_MERGE_LAYER: s.job = std::make_unique<MergeLayerJob>(P(0, 1 << 20)); break;
+            case ABY3H_JOB_SORT: s.job = std::make_unique<SortJob>(P(0, 1 << 20)); break;
             case ABY3H_JOB_A2B: s.job = std::make_unique<A2bJob>(P(0, 1 << 20)); break;
             case ABY3H_JOB_BITINJ: s.job = std::make_unique<BitInjJob>(P(0, 1 << 16), P(1, 64)); break;
             default: throw std::runtime_error("unknown job");

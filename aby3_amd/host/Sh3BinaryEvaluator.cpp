@@ -102,6 +102,20 @@ void Sh3BinaryEvaluator::setInput(u64 i, const sbMatrix& in) {
     mLevel = 0;
 }
 
+void Sh3BinaryEvaluator::setInput(u64 i, const sbMatrix& in, const aby3g_rowmap& map) {
+    if (!mCir) throw RTE_LOC;
+    if (i >= mCir->mInputs.size()) throw std::invalid_argument("input index out of bounds");
+    const auto& wires = mCir->mInputs[i];
+    if (in.bitCount() != wires.size()) throw std::invalid_argument("input data wrong size");
+    for (size_t k = 1; k < wires.size(); ++k)
+        if (wires[k] != wires[k - 1] + 1) throw std::runtime_error("expecting contiguous input wires. " LOCATION);
+    Gpu& g = *mGpu;
+    const u64 W = mCir->mWireCount;
+    GPU_CALL(aby3g_bits_to_wires_map(in.data(), in.rows(), in.i64Cols(), (u32)wires.size(), &map, mRows,
+                                     mMem.as<u64>() + wires[0] * mWords, W * mWords, mWords, g.stream()));
+    mLevel = 0;
+}
+
 void Sh3BinaryEvaluator::setInputs(const std::vector<WireInput>& in) {
     if (!mCir) throw RTE_LOC;
     Gpu& g = *mGpu;
@@ -305,6 +319,17 @@ void Sh3BinaryEvaluator::getOutput(u64 i, sbMatrix& out) {
     const u32* dw = mCur->allOutputWires + mCur->outputOffsets[i];
     GPU_CALL(aby3g_wires_to_bits2(mMem.as<u64>(), W * mWords, dw, (u32)wires.size(), mWords, out.data(), mRows,
                                   g.stream()));
+}
+
+void Sh3BinaryEvaluator::getOutput(u64 i, sbMatrix& out, const aby3g_rowmap& map) {
+    if (i >= mCir->mOutputs.size()) throw RTE_LOC;
+    const auto& wires = mCir->mOutputs[i];
+    if (out.bitCount() != wires.size()) throw std::invalid_argument("output matrix wrong size");
+    Gpu& g = *mGpu;
+    const u64 W = mCir->mWireCount;
+    const u32* dw = mCur->allOutputWires + mCur->outputOffsets[i];
+    GPU_CALL(aby3g_wires_to_bits_map(mMem.as<u64>(), W * mWords, dw, (u32)wires.size(), mWords, out.data(), out.rows(),
+                                     &map, mRows, g.stream()));
 }
 
 }  // namespace aby3

@@ -34,6 +34,9 @@ public:
     void setCir(BetaCircuit* cir, u64 width, Sh3ShareGen& gen);
     void setCir(BetaCircuit* cir, u64 width, block prevSeed, block nextSeed);
     void setInput(u64 i, const sbMatrix& in);
+    // setInput from mapped rows of `in` (circuit row p <- row map(p)): the
+    // compare-exchange gather of a merge round fused into the transpose
+    void setInput(u64 i, const sbMatrix& in, const aby3g_rowmap& map);
     // a one-row shared input broadcast to every row (Sh3BinaryEvaluator.cpp:105-138)
     void setReplicatedInput(u64 i, const sbMatrix& in);
     // Inputs straight from arithmetic shares, several in one launch (no
@@ -52,6 +55,9 @@ public:
     Sh3Task asyncEvaluate(Sh3Task dep, BetaCircuit* cir, Sh3ShareGen& gen, std::vector<const sbMatrix*> inputs,
                           std::vector<sbMatrix*> outputs);
     void getOutput(u64 i, sbMatrix& out);
+    // getOutput into mapped rows of an existing `out` (row map(p) <- circuit
+    // row p; other rows untouched): the round's scatter
+    void getOutput(u64 i, sbMatrix& out, const aby3g_rowmap& map);
 
     bool hasMoreRounds() const { return mLevel <= mCir->mLevelCounts.size(); }
     void roundCallback(CommPkg& comm, Sh3Task task);

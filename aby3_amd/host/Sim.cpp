@@ -224,22 +224,66 @@ int aby3h_sim_cipher_gt(int device, const int64_t* a, const int64_t* b, uint64_t
     });
 }
 
-int aby3h_sim_merge(int device, const uint64_t* lens, uint64_t nlists, const int64_t* keys, int64_t* out_sorted) {
+int aby3h_sim_merge(int device, int mode, const uint64_t* lens, uint64_t nlists, uint64_t dim, const int64_t* keys,
+                    int64_t* out_sorted, int64_t* out_shares) {
     return guarded([&] {
+        if (mode < 0 || mode > 3) throw std::runtime_error("unknown merge mode");
+        if (!nlists) throw std::runtime_error("no lists");
         std::vector<i64Matrix> lists;
         u64 off = 0;
         for (u64 k = 0; k < nlists; ++k) {
             lists.push_back(hostMat(keys + off, lens[k], 1));
             off += lens[k];
         }
+        const u64 total = off;
+        if (mode >= 2 && (!dim || nlists % dim)) throw std::runtime_error("nlists must be a multiple of dim");
+        if (mode == 3 && nlists != 2 * dim) throw std::runtime_error("high_dimensional_odd_even_merge: 2 lists per dim");
         run3(device, [&](SimParty& p) {
-            std::vector<sbMatrix> data(nlists);
-            for (u64 k = 0; k < nlists; ++k) {
-                data[k].resize(lens[k], 64);
-                shareBinIn(p, lists[k], data[k]);
-            }
             sbMatrix sorted;
-            odd_even_multi_merge(data, sorted, p.idx, p.eval, p.rt);
+            if (mode == 0) {
+                std::vector<sbMatrix> data(nlists);
+                for (u64 k = 0; k < nlists; ++k) {
+                    data[k].resize(lens[k], 64);
+                    shareBinIn(p, lists[k], data[k]);
+                }
+                odd_even_multi_merge(data, sorted, p.idx, p.eval, p.rt);
+            } else if (mode == 1) {
+                sbMatrix flat(total, 64);
+                shareBinIn(p, hostMat(keys, total, 1), flat);
+                if (nlists == total)
+                    odd_even_merge_sort(flat, sorted, p.idx, p.eval, p.rt);
+                else
+                    odd_even_multi_merge(flat, std::vector<u64>(lens, lens + nlists), sorted, p.idx, p.eval, p.rt);
+            } else {
+                const u64 k = nlists / dim;
+                std::vector<std::vector<sbMatrix>> data(dim);
+                for (u64 i = 0; i < dim; ++i) {
+                    data[i].resize(k);
+                    for (u64 j = 0; j < k; ++j) {
+                        data[i][j].resize(lens[i * k + j], 64);
+                        shareBinIn(p, lists[i * k + j], data[i][j]);
+                    }
+                }
+                std::vector<sbMatrix> out;
+                if (mode == 2) {
+                    high_dimensional_odd_even_multi_merge(data, out, p.idx, p.eval, p.rt);
+                } else {
+                    std::vector<sbMatrix> d1(dim), d2(dim);
+                    for (u64 i = 0; i < dim; ++i) {
+                        d1[i] = std::move(data[i][0]);
+                        d2[i] = std::move(data[i][1]);
+                    }
+                    high_dimensional_odd_even_merge(d1, d2, out, p.idx, p.eval, p.rt);
+                }
+                sorted.resize(total, 64);
+                u64 o = 0;
+                for (auto& x : out) {
+                    for (int s = 0; s < 2; ++s)
+                        if (x.rows()) d2d(sorted.share(s) + o, x.share(s), x.rows() * 8, p.rt.gpu());
+                    o += x.rows();
+                }
+            }
+            putShares(p.idx, sorted, out_shares);
             i64Matrix r;
             p.enc.revealAll(p.rt, sorted, r).get();
             if (p.idx == 0 && out_sorted) std::memcpy(out_sorted, r.mData.data(), 8 * r.size());

@@ -54,6 +54,13 @@ class Gate(ctypes.Structure):
                 ("z_row", c_uint32), ("send_row", c_uint32)]
 
 
+class RowMap(ctypes.Structure):
+    """aby3g_rowmap: element p -> idx[first + p], or the affine
+    start + rep * rep_stride + k * step with (rep, k) = divmod(first + p, per_rep)."""
+    _fields_ = [("first", c_uint64), ("start", c_uint64), ("step", c_uint64), ("per_rep", c_uint64),
+                ("rep_stride", c_uint64), ("idx", c_void_p)]
+
+
 def key16(b: bytes):
     assert len(b) == 16
     return (ctypes.c_uint8 * 16)(*b)
@@ -131,6 +138,10 @@ _SIGS = {
                                      c_void_p]),
     "aby3g_wires_to_bits2": (c_int, [c_void_p, c_uint64, c_void_p, ctypes.c_uint32, c_uint64, c_void_p, c_uint64,
                                      c_void_p]),
+    "aby3g_bits_to_wires_map": (c_int, [c_void_p, c_uint64, c_uint64, ctypes.c_uint32, POINTER(RowMap), c_uint64,
+                                        c_void_p, c_uint64, c_uint64, c_void_p]),
+    "aby3g_wires_to_bits_map": (c_int, [c_void_p, c_uint64, c_void_p, ctypes.c_uint32, c_uint64, c_void_p, c_uint64,
+                                        POINTER(RowMap), c_uint64, c_void_p]),
     "aby3g_bin_unpack": (c_int, [c_void_p, c_void_p, c_uint32, c_void_p, c_uint64, c_uint64, c_void_p]),
     "aby3g_bits_to_wires_lin": (c_int, [c_void_p, c_uint32, c_uint64, c_uint64, c_void_p]),
     "aby3g_bits_to_wires": (c_int, [c_void_p, c_uint64, c_uint64, c_uint32, c_void_p, c_uint64, c_void_p]),
@@ -177,7 +188,7 @@ class _Lib:
         return call
 
 
-JOB_MUL_TRUNC, JOB_MUL, JOB_MSB, JOB_LR, JOB_MERGE_LAYER, JOB_A2B, JOB_BITINJ = range(7)
+JOB_MUL_TRUNC, JOB_MUL, JOB_MSB, JOB_LR, JOB_SORT, JOB_A2B, JOB_BITINJ = range(7)
 INFO = dict(mults_per_step=0, gemm_int8_ops=1, and_words=2, gate_words=3, gate_bytes=4, bytes_sent=5,
             host_enqueue_us=6, host_drain_us=7, host_recv_wait_us=8, host_api_us=9, host_api_calls=10)
 
@@ -199,7 +210,7 @@ _HOST_SIGS = {
     "aby3h_sim_circuit": (c_int, [c_int, c_char_p, c_uint64, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p]),
     "aby3h_sim_piecewise": (c_int, [c_int, c_int, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p]),
     "aby3h_sim_cipher_gt": (c_int, [c_int, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p]),
-    "aby3h_sim_merge": (c_int, [c_int, c_void_p, c_uint64, c_void_p, c_void_p]),
+    "aby3h_sim_merge": (c_int, [c_int, c_int, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p]),
 }
 
 _host = None
@@ -380,13 +391,20 @@ class sim:
         return sh.reshape(3, 2, -1), plain
 
     @classmethod
-    def merge(cls, lists, device=0):
+    def merge(cls, lists, mode=0, dim=0, shares=False, device=0):
+        """The merge network (aby3h_sim_merge): mode 0 odd_even_multi_merge of
+        separately shared lists, 1 the flat form (singletons: the sort),
+        2 high_dimensional_odd_even_multi_merge (lists [dim][k], flattened),
+        3 high_dimensional_odd_even_merge. Returns the revealed result, and
+        with shares=True also every party's shares [3][2][n]."""
         np = cls._np()
         lens = np.asarray([len(x) for x in lists], np.uint64)
         keys = np.ascontiguousarray(np.concatenate([np.asarray(x, np.int64) for x in lists]))
         out = np.zeros(len(keys), np.int64)
-        cls._call("aby3h_sim_merge", device, cls._p(lens), len(lists), cls._p(keys), cls._p(out))
-        return out
+        sh = np.zeros(6 * len(keys), np.int64) if shares else None
+        cls._call("aby3h_sim_merge", device, mode, cls._p(lens), len(lists), dim, cls._p(keys), cls._p(out),
+                  cls._p(sh) if shares else None)
+        return (out, sh.reshape(3, 2, len(keys))) if shares else out
 
 
 _lib = None

@@ -29,6 +29,7 @@ The JSON line also carries:
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -181,9 +182,48 @@ def cpu_conversion_rates(nt):
            (bi_rows * 64 * bi_reps / secs2, f"{bi_reps} x bitInjection of {bi_rows}x64 bits")
 
 
+def cpu_sort_rate(nt):
+    """The oracle's batched odd-even merge sort on this host (cpu_baseline leg
+    only), AND word-gates/s over a 2^16-key sort, three parties in sequence
+    on one thread."""
+    import ctypes
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle as orc
+
+    import numpy as np
+
+    n = 1 << 16
+    args, keep = orc._cir_args(nt.circuit("cmp_swap", 64))
+    f = orc.dll().orc_bench_sort
+    f.restype = ctypes.c_double
+    secs = f(*args, ctypes.c_uint64(n))
+    if secs < 0:
+        raise SystemExit("bench: oracle sort baseline failed: " + orc.dll().orc_last_error().decode())
+    cir = nt.circuit("cmp_swap", 64)
+    ands = sum(1 for g in np.asarray(cir["gates"]).reshape(-1, 4) if g[3] in (2, 3, 4, 5))
+    words = 0
+    for lv in range(16):  # 2^(15 - lv) merges of two lists of 2^lv keys, 1 + lv rounds
+        L = 1 << lv
+        words += sum(math.ceil((1 << (15 - lv)) * c / 64) for c in _round_pairs(L))
+    return ands * words / secs, (f"1 x odd_even_merge_sort of {n} keys (oracle restatement: bit-sliced u64 "
+                                 "cmp_swap rounds, AES-NI z masks, 3 parties on one thread)")
+
+
+def _round_pairs(L):
+    """Pairs per merge in each round of the merge of two lists of L keys
+    (Sort.cpp:361-398)."""
+    t = math.ceil(math.log2(L) + 1)
+    q, d, r, out = 2 ** (t - 1), 1, 0, []
+    while d > 0:
+        out.append(max(0, (2 * L - d - r + 1) // 2))
+        d, q, r = q - 1, q >> 1, 1
+    return out
+
+
 def extras(args, nt, dev, world, pg):
-    """C4 (one SGD_Logistic iteration, 10^6 x 128, B=256, D16) and C5 (one
-    compare-exchange layer of the 2^20-key merge network), each checked."""
+    """C4 (one SGD_Logistic iteration, 10^6 x 128, B=256, D16) and C5 (the
+    whole odd-even merge sort of 2^20 keys), each checked."""
     res = {}
     with nt.Session(nt.JOB_LR, [args.lr_rows, 128, 256, 16, 11], devices=(dev,) * 3, probe=False) as s:
         s.run(5)
@@ -204,18 +244,30 @@ def extras(args, nt, dev, world, pg):
                           "D16, aB 11), the three parties simulated in sequence on one thread, no network",
             }
             res["lr_iteration"]["speedup_vs_cpu_baseline"] = cpu_ms / (dt / 50 * 1e3)
-    with nt.Session(nt.JOB_MERGE_LAYER, [1 << 20], devices=(dev,) * 3, probe=False) as s:
-        s.run(2)
-        dt = timed(s, 10, pg)
+    with nt.Session(nt.JOB_SORT, [1 << 20], devices=(dev,) * 3, probe=False) as s:
+        s.run(1)
+        reps = 2
+        dt = timed(s, reps, pg)
         if not s.check():
-            raise SystemExit("bench: merge layer not ordered")
+            raise SystemExit("bench: merge sort output differs from std::sort of the keys")
         info = s.info()
-        res["merge_layer"] = {
-            "workload": "one odd-even merge layer: cmp_swap on 2^19 pairs of 64-bit keys (gather, circuit, scatter)",
-            "ms_per_layer": dt / 10 * 1e3,
-            "and_word_gates_per_s": world * 10 * info["and_words"] / dt,
-            "est_full_merge_s": dt / 10 * 210,
+        res["merge_sort"] = {
+            "workload": "odd_even_merge_sort of 2^20 64-bit keys: 20 multi-merge levels, 210 rounds, every round "
+                        "one cmp_swap evaluation over its 2^19 compare-exchanges (gather/scatter fused into the "
+                        "transposes), 3 parties",
+            "ms_per_sort": dt / reps * 1e3,
+            "keys_per_s": world * reps * (1 << 20) / dt,
+            "and_words_per_sort": info["and_words"],
+            "and_word_gates_per_s": world * reps * info["and_words"] / dt,
         }
+        if world == 1 and not args.no_cpu_baseline:
+            progress("C5 CPU baseline")
+            rate, sample = cpu_sort_rate(nt)
+            res["merge_sort"]["cpu_baseline"] = {
+                "value": rate, "unit": "AND word-gates/s", "cores": 1, "kind": "port", "sample": sample,
+                "est_full_sort_s": info["and_words"] / rate,
+            }
+            res["merge_sort"]["speedup_vs_cpu_baseline"] = res["merge_sort"]["and_word_gates_per_s"] / rate
     # share conversions, each checked on its revealed output
     with nt.Session(nt.JOB_A2B, [1 << 20], devices=(dev,) * 3, probe=False) as s:
         s.run(2)

@@ -37,9 +37,10 @@ enum {
      * SGD_Logistic iteration (aby3-ML/Regression.h:249-293): xw = X_B w,
      * sigmoid (Sh3Piecewise), err = f - Y_B, w -= X_B^T err >> (D + aB). */
     ABY3H_JOB_LR = 3,
-    /* params: keys. One step = one compare-exchange layer of keys/2 pairs
-     * of the merge network (Sort.cpp:366-398, fused cmp_swap circuit). */
-    ABY3H_JOB_MERGE_LAYER = 4,
+    /* params: keys. One step = odd_even_merge_sort of `keys` 64-bit keys
+     * (distinct, (U[0, 2^43) << 20) | i): the multi-merge of singleton lists,
+     * every round of every level one cmp_swap evaluation (Sort.cpp:413-628). */
+    ABY3H_JOB_SORT = 4,
     /* params: rows. One step = Sh3Converter::toBinaryMatrix of rows x 1
      * 64-bit values (resharing + 64-bit adder, Sh3Converter.cpp:61-207). */
     ABY3H_JOB_A2B = 5,
@@ -117,9 +118,17 @@ int aby3h_sim_piecewise(int device, int kind, const int64_t* x, uint64_t n, uint
 /* cipher_gt(A, B) = MSB(B - A) (BuildingBlocks.cpp:525-532), 1-bit result */
 int aby3h_sim_cipher_gt(int device, const int64_t* a, const int64_t* b, uint64_t n, int64_t* out_plain,
                         int64_t* out_shares);
-/* odd_even_multi_merge of nlists sorted lists (Sort.cpp:327-437); keys
- * concatenated, out_sorted receives the revealed merged list */
-int aby3h_sim_merge(int device, const uint64_t* lens, uint64_t nlists, const int64_t* keys, int64_t* out_sorted);
+/* The merge network (Sort.cpp:327-628, batched as aby3_amd/host/Sort.h) on
+ * nlists sorted lists of 64-bit keys (concatenated in `keys`):
+ * mode 0 odd_even_multi_merge(vector<sbMatrix>), each list shared on its own;
+ * mode 1 the flat odd_even_multi_merge, all keys shared as one matrix
+ *        (all lists of length 1: odd_even_merge_sort);
+ * mode 2 high_dimensional_odd_even_multi_merge, lists [dim][nlists / dim];
+ * mode 3 high_dimensional_odd_even_merge (nlists = 2 * dim).
+ * out_sorted: the revealed merged list(s) back to back; out_shares
+ * [party][share][total] of the same (either may be NULL). */
+int aby3h_sim_merge(int device, int mode, const uint64_t* lens, uint64_t nlists, uint64_t dim, const int64_t* keys,
+                    int64_t* out_sorted, int64_t* out_shares);
 
 #ifdef __cplusplus
 }

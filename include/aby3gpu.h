@@ -333,6 +333,31 @@ int aby3g_bits_to_wires2(const int64_t* in, uint64_t rows, uint64_t cols64, uint
 int aby3g_wires_to_bits2(const uint64_t* mem, uint64_t share_stride, const uint32_t* wires, uint32_t nbits,
                          uint64_t words, int64_t* out, uint64_t rows, aby3g_stream stream);
 
+/* Row maps of the merge network's compare-exchange rounds (aby3-Basic
+ * Sort.cpp:361-398 x_mask / y_mask and the gathers around
+ * bool_cipher_max_min_split, :375-392; batched over merges as
+ * high_dimensional_odd_even_merge, :506-570). Element p of a circuit input or
+ * output is row map(p) of a row-major sbMatrix:
+ *   idx != NULL : idx[first + p]                       (explicit, DEVICE array)
+ *   otherwise   : q = first + p, rep = q / per_rep, k = q % per_rep,
+ *                 start + rep * rep_stride + k * step  (affine)
+ * The struct is passed by host pointer and copied into the launch. */
+typedef struct {
+    uint64_t first, start, step, per_rep, rep_stride;
+    const uint32_t* idx;
+} aby3g_rowmap;
+/* setInput from mapped rows: circuit row p (p < rows) of both shares takes
+ * row map(p) of `in` ([2][in_rows][cols64]); rows >= rows are zero. */
+int aby3g_bits_to_wires_map(const int64_t* in, uint64_t in_rows, uint64_t cols64, uint32_t nbits,
+                            const aby3g_rowmap* map, uint64_t rows, uint64_t* wire_rows, uint64_t share_stride,
+                            uint64_t words, aby3g_stream stream);
+/* getOutput into mapped rows: row map(p) of `out` ([2][out_rows][ceil(nbits/64)])
+ * of both shares takes circuit row p, for p < rows; other rows of `out` are
+ * untouched (the compare-exchange's scatter back into the merge array). */
+int aby3g_wires_to_bits_map(const uint64_t* mem, uint64_t share_stride, const uint32_t* wires, uint32_t nbits,
+                            uint64_t words, int64_t* out, uint64_t out_rows, const aby3g_rowmap* map, uint64_t rows,
+                            aby3g_stream stream);
+
 /* setInput of shares that are linear combinations of arithmetic shares,
  * several inputs / shares in one launch (the two-input binary resharing of
  * fetch_msb and Sh3Piecewise::getInputRegions, BuildingBlocks.cpp:475-502,

@@ -285,6 +285,69 @@ int orc_sim_fetch_msb(uint32_t wires, const uint32_t* gates, uint64_t ngates, co
     });
 }
 
+// The merge network (Sort.cpp:327-628) on binary-shared 64-bit keys, with the
+// supplied cmp_swap circuit. mode 0: odd_even_multi_merge, each of the nlists
+// lists shared on its own; 1: the same over all keys shared as one matrix;
+// 2: high_dimensional_odd_even_multi_merge, lists [dim][nlists / dim] shared
+// in that order; 3: high_dimensional_odd_even_merge (nlists = 2 * dim).
+// out_sorted / out_shares: the merged list(s) back to back.
+int orc_sim_merge(uint32_t wires, const uint32_t* gates, uint64_t ngates, const uint32_t* levels, uint64_t nlevels,
+                  const uint32_t* inWires, const uint32_t* inSizes, uint64_t nin, const uint32_t* outWires,
+                  const uint32_t* outSizes, uint64_t nout, int mode, const uint64_t* lens, uint64_t nlists,
+                  uint64_t dim, const int64_t* keys, int64_t* out_sorted, int64_t* out_shares) {
+    return guard([&] {
+        Circuit c = toCircuit(wires, gates, ngates, levels, nlevels, inWires, inSizes, nin, outWires, outSizes, nout);
+        auto enc = makeEncryptors(0);
+        auto ev = makeEvaluators(1);
+        u64 total = 0;
+        for (u64 k = 0; k < nlists; ++k) total += lens[k];
+        Shared res;
+        if (mode == 0 || mode == 1) {
+            Shared flat;
+            if (mode == 1) {
+                flat = shareBin(enc, 0, toMat(keys, total, 1));
+            } else {
+                for (int p = 0; p < 3; ++p) flat[p] = SMat(total, 1);
+                u64 off = 0;
+                for (u64 k = 0; k < nlists; ++k) {
+                    Shared x = shareBin(enc, 0, toMat(keys + off, lens[k], 1));
+                    for (int p = 0; p < 3; ++p)
+                        for (int s = 0; s < 2; ++s)
+                            std::copy(x[p].s[s].v.begin(), x[p].s[s].v.end(), flat[p].s[s].v.begin() + off);
+                    off += lens[k];
+                }
+            }
+            res = multiMerge(ev, c, flat, std::vector<u64>(lens, lens + nlists));
+        } else if (mode == 2 || mode == 3) {
+            if (!dim || nlists % dim) throw std::runtime_error("nlists must be a multiple of dim");
+            const u64 k = nlists / dim;
+            if (mode == 3 && k != 2) throw std::runtime_error("high_dimensional_odd_even_merge takes two lists per dim");
+            std::vector<std::vector<Shared>> data(dim, std::vector<Shared>(k));
+            u64 off = 0, li = 0;
+            for (u64 i = 0; i < dim; ++i)
+                for (u64 j = 0; j < k; ++j, ++li) {
+                    data[i][j] = shareBin(enc, 0, toMat(keys + off, lens[li], 1));
+                    off += lens[li];
+                }
+            auto sorted = hdMultiMerge(ev, c, data);
+            for (int p = 0; p < 3; ++p) res[p] = SMat(total, 1);
+            off = 0;
+            for (auto& x : sorted) {
+                for (int p = 0; p < 3; ++p)
+                    for (int s = 0; s < 2; ++s)
+                        std::copy(x[p].s[s].v.begin(), x[p].s[s].v.end(), res[p].s[s].v.begin() + off);
+                off += x[0].rows();
+            }
+        } else {
+            throw std::runtime_error("unknown merge mode");
+        }
+        if (!consistent(res)) throw std::runtime_error("inconsistent shares");
+        Mat m = revealBin(res);
+        if (out_sorted) memcpy(out_sorted, m.v.data(), 8 * total);
+        if (out_shares) putShared(res, out_shares);
+    });
+}
+
 // CPU baseline of asyncMul + truncation (bench.py cpu_baseline): the three
 // parties' round-1 local compute (three scalar i64 GEMMs as Eigen evaluates
 // A0*B0 + A0*B1 + A1*B0, Sh3Evaluator.cpp:662-665, plus the truncation tuple
@@ -494,6 +557,36 @@ extern "C" double orc_bench_bitinj(uint64_t rows, uint64_t bits, int reps) {
             if (res[0].s[0].v.size() != rows * bits) throw std::runtime_error("bitinj: result size");
         }
         auto t1 = std::chrono::steady_clock::now();
+        return std::chrono::duration<double>(t1 - t0).count();
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+// CPU baseline of the C5 sort: the oracle's batched odd-even merge sort of n
+// distinct keys ((x mod 2^43) << 20 | i), three parties simulated in sequence
+// on one thread. Returns seconds, -1 on error.
+extern "C" double orc_bench_sort(uint32_t wires, const uint32_t* gates, uint64_t ngates, const uint32_t* levels,
+                                 uint64_t nlevels, const uint32_t* inWires, const uint32_t* inSizes, uint64_t nin,
+                                 const uint32_t* outWires, const uint32_t* outSizes, uint64_t nout, uint64_t n) {
+    try {
+        Circuit c = toCircuit(wires, gates, ngates, levels, nlevels, inWires, inSizes, nin, outWires, outSizes, nout);
+        auto enc = makeEncryptors(0);
+        auto ev = makeEvaluators(1);
+        Mat a(n, 1);
+        u64 x = 7;
+        for (u64 k = 0; k < n; ++k) {
+            x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+            a.v[k] = (i64)(((x % (1ull << 43)) << 20) | k);
+        }
+        Shared A = shareBin(enc, 0, a);
+        auto t0 = std::chrono::steady_clock::now();
+        Shared res = multiMerge(ev, c, A, std::vector<u64>(n, 1));
+        auto t1 = std::chrono::steady_clock::now();
+        Mat r = revealBin(res);
+        for (u64 k = 1; k < n; ++k)
+            if (r.v[k - 1] > r.v[k]) throw std::runtime_error("sort baseline: output not sorted");
         return std::chrono::duration<double>(t1 - t0).count();
     } catch (const std::exception& e) {
         g_err = e.what();

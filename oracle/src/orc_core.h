@@ -255,3 +255,26 @@ Shared bitInjection(std::array<Party, 3>& ev, std::array<ConvParty, 3>& cv, cons
                     bool twoRounds);
 
 }  // namespace orc
+
+namespace orc {
+
+// --------------------------------------------------------------------------
+// Merge network (aby3-Basic/Sort.cpp:327-628), batched the way the GPU
+// engine runs it (aby3_amd/host/Sort.h): a batch of merges runs its rounds
+// together, round j = ONE evaluation of the supplied cmp_swap circuit
+// (outputs min, max) over every merge's round-j pairs (merge-major, then
+// pair order), chunked at MAX_SENDING_SIZE = 2^25 rows (Sort.cpp:4,
+// :522-543); the padding maxima (Sort.cpp:335-347) are one evaluation over
+// the merges, only when some merge has lists of different lengths.
+// --------------------------------------------------------------------------
+struct MergeSpec { u64 offA, lenA, lenB; };  // lists adjacent in `data`
+// (d, r) of each round for lists of `length` (Sort.cpp:361-398)
+std::vector<std::pair<u64, u64>> mergeRounds(u64 length);
+void mergeBatch(std::array<Party, 3>& ev, const Circuit& cmpSwap, Shared& data, const std::vector<MergeSpec>& ms);
+// odd_even_multi_merge over lists stored back to back (Sort.cpp:413-437)
+Shared multiMerge(std::array<Party, 3>& ev, const Circuit& cmpSwap, const Shared& flat, std::vector<u64> lens);
+// high_dimensional_odd_even_multi_merge (Sort.cpp:585-628): data[dim][k]
+std::vector<Shared> hdMultiMerge(std::array<Party, 3>& ev, const Circuit& cmpSwap,
+                                 std::vector<std::vector<Shared>> data);
+
+}  // namespace orc

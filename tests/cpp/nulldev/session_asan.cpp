@@ -22,7 +22,7 @@ int main() {
         {ABY3H_JOB_MUL_TRUNC, {64, 48, 80, 16, 1}, 3}, {ABY3H_JOB_MUL_TRUNC, {64, 64, 64, 8, 0}, 3},
         {ABY3H_JOB_MUL, {32, 32, 32, 0}, 3},           {ABY3H_JOB_MUL, {32, 16, 8, 1}, 3},
         {ABY3H_JOB_MSB, {3000}, 2},                    {ABY3H_JOB_LR, {2048, 16, 64, 16, 11}, 3},
-        {ABY3H_JOB_MERGE_LAYER, {4096}, 2},            {ABY3H_JOB_MUL_TRUNC, {64, 48, 80, 16, 1}, 2},
+        {ABY3H_JOB_SORT, {4096}, 1},                  {ABY3H_JOB_MUL_TRUNC, {64, 48, 80, 16, 1}, 2},
     };
     for (int round = 0; round < 2; ++round)
         for (auto& j : jobs) {
@@ -39,6 +39,14 @@ int main() {
     if (aby3h_sim_mul(0, 1, 1, 16, a.data(), b.data(), 64, 48, 80, sh.data(), pl.data())) return fail("sim_mul");
     std::vector<int64_t> x(300, 1), y(300, 2), o(300), osh(6 * 300);
     if (aby3h_sim_cipher_gt(0, x.data(), y.data(), 300, o.data(), osh.data())) return fail("sim_cipher_gt");
+    // the merge network: general shapes (padding, explicit row lists) and
+    // the high-dimensional forms
+    const uint64_t lens[] = {5, 7, 8, 3, 2, 6};
+    std::vector<int64_t> keys(31, 1), sorted(31), msh(6 * 31);
+    for (int mode = 0; mode < 4; ++mode) {
+        const uint64_t n = mode == 3 ? 4 : 6, dim = mode >= 2 ? 2 : 0;
+        if (aby3h_sim_merge(0, mode, lens, n, dim, keys.data(), sorted.data(), msh.data())) return fail("sim_merge");
+    }
     std::printf("session_asan: ok\n");
     return 0;
 }

@@ -142,6 +142,20 @@ def merge(st):
     for fx, lens in (("merge_8_8", [8, 8]), ("multi_merge_5_7_8_3", [5, 7, 8, 3])):
         lists = [np.sort((st.i64(n).view(np.uint64) >> np.uint64(21)).view(np.int64)) for n in lens]
         out[fx] = dict(lists=[L(v) for v in lists], sorted=L(np.sort(np.concatenate(lists))))
+    # share level: the batched network (aby3_amd/host/Sort.h) with the cmp_swap
+    # circuit, the reference tests' seeds; a 16-key sort (mode 1) and a
+    # two-dimensional multi-merge of odd list count (mode 2)
+    cir = nt.circuit("cmp_swap", 64)
+    for fx, mode, dim, lens in (("sort_16", 1, 0, [1] * 16), ("hd_multi_merge_2x3", 2, 2, [4, 2, 3, 5, 1, 4])):
+        lists = [np.sort((st.i64(n).view(np.uint64) >> np.uint64(21)).view(np.int64)) for n in lens]
+        plain, sh = orc.sim_merge(cir, lists, mode, dim, with_shares=True)
+        if mode == 1:
+            exp = np.sort(np.concatenate(lists))
+        else:
+            k = len(lens) // dim
+            exp = np.concatenate([np.sort(np.concatenate(lists[i * k:(i + 1) * k])) for i in range(dim)])
+        assert np.array_equal(plain, exp)
+        out[fx] = dict(lists=[L(v) for v in lists], mode=mode, dim=dim, sorted=L(plain), shares=L(sh))
     return out
 
 

@@ -170,3 +170,19 @@ def sim_fetch_msb(cir, a: np.ndarray, b: np.ndarray, with_shares: bool = False):
     sh = np.zeros(6 * n, dtype=np.int64)
     _check(dll().orc_sim_fetch_msb(*args, _p(a), _p(b), c_uint64(n), _p(out), _p(sh)))
     return (out, sh.reshape(3, 2, n)) if with_shares else out
+
+
+def sim_merge(cir, lists, mode: int = 0, dim: int = 0, with_shares: bool = False):
+    """The batched merge network (orc_sim_merge): mode 0 odd_even_multi_merge
+    of separately shared lists, 1 all keys shared as one matrix, 2
+    high_dimensional_odd_even_multi_merge ([dim][k] lists, flattened), 3
+    high_dimensional_odd_even_merge. cir: the cmp_swap(64) circuit."""
+    args, keep = _cir_args(cir)
+    lens = np.asarray([len(x) for x in lists], dtype=np.uint64)
+    keys = np.ascontiguousarray(np.concatenate([np.asarray(x, dtype=np.int64) for x in lists]))
+    n = len(keys)
+    out = np.zeros(n, dtype=np.int64)
+    sh = np.zeros(6 * n, dtype=np.int64)
+    _check(dll().orc_sim_merge(*args, c_int(mode), _p(lens), c_uint64(len(lists)), c_uint64(dim), _p(keys), _p(out),
+                               _p(sh)))
+    return (out, sh.reshape(3, 2, n)) if with_shares else out

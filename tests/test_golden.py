@@ -111,12 +111,29 @@ def test_piecewise_gpu(gpu, name, fx):
 
 @pytest.mark.parametrize("name,fx", cases("merge"))
 def test_merge_fixture_is_sorted_union(name, fx):
-    allv = np.sort(np.concatenate([A(v) for v in fx["lists"]]))
-    assert np.array_equal(allv, A(fx["sorted"]))
-    assert all(np.all(np.diff(A(v)) >= 0) for v in fx["lists"])
+    lists = [A(v) for v in fx["lists"]]
+    assert all(np.all(np.diff(v) >= 0) for v in lists)
+    dim = fx.get("dim", 0)
+    if fx.get("mode", 0) == 2:
+        k = len(lists) // dim
+        exp = np.concatenate([np.sort(np.concatenate(lists[i * k:(i + 1) * k])) for i in range(dim)])
+    else:
+        exp = np.sort(np.concatenate(lists))
+    assert np.array_equal(exp, A(fx["sorted"]))
+
+
+@pytest.mark.parametrize("name,fx", [c for c in cases("merge") if "shares" in c[1]])
+def test_merge_oracle(name, fx):
+    plain, sh = orc.sim_merge(nt.circuit("cmp_swap", 64), [A(v) for v in fx["lists"]], fx["mode"], fx["dim"],
+                              with_shares=True)
+    assert np.array_equal(plain, A(fx["sorted"]))
+    assert np.array_equal(sh.reshape(-1), A(fx["shares"]))
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,fx", cases("merge"))
 def test_merge_gpu(gpu, name, fx):
-    assert np.array_equal(nt.sim.merge([A(v) for v in fx["lists"]]), A(fx["sorted"]))
+    plain, sh = nt.sim.merge([A(v) for v in fx["lists"]], fx.get("mode", 0), fx.get("dim", 0), shares=True)
+    assert np.array_equal(plain, A(fx["sorted"]))
+    if "shares" in fx:
+        assert np.array_equal(sh.reshape(-1), A(fx["shares"]))

@@ -258,6 +258,54 @@ def test_transposes_both_shares(gpu, rows, nbits):
     assert np.array_equal(host(out).reshape(2, rows, cols), x)
 
 
+def _map_rows(first, start, step, per_rep, rep_stride, n):
+    q = first + np.arange(n, dtype=np.int64)
+    return start + (q // per_rep) * rep_stride + (q % per_rep) * step
+
+
+@pytest.mark.parametrize("in_rows,rows,mp", [
+    (4096, 2048, (0, 0, 1, 1024, 2048)),      # merge round 0: first halves of 2 lists of 1024
+    (4096, 1500, (0, 1, 2, 1500, 4096)),      # odd slots, one rep
+    (5000, 1999, (17, 3, 2, 7, 16)),          # chunk offset, short reps
+    (300, 300, None),                          # explicit index list (a permutation)
+    (2049, 1, (0, 2048, 1, 1, 0)),
+])
+def test_transposes_mapped(gpu, in_rows, rows, mp):
+    """bits_to_wires_map / wires_to_bits_map (the merge rounds' fused gather
+    and scatter) against numpy; the scatter leaves unmapped rows untouched."""
+    import torch
+
+    x = rnd(in_rows + rows, 2 * in_rows).reshape(2, in_rows, 1)
+    if mp is None:
+        src = np.random.default_rng(rows).permutation(in_rows)[:rows].astype(np.int64)
+        idx = torch.from_numpy(src.astype(np.uint32).view(np.int32)).cuda()
+        rm = nt.RowMap(0, 0, 0, 1, 0, idx.data_ptr())
+    else:
+        src = _map_rows(*mp, rows)
+        rm = nt.RowMap(*mp, None)
+    words = 32 * ((rows + 2047) // 2048)
+    mem = empty(2 * 64 * words)
+    gpu.bits_to_wires_map(P(dev(x)), in_rows, 1, 64, ctypes.byref(rm), rows, P(mem), 64 * words, words, None)
+    m = host(mem).view(np.uint64).reshape(2, 64, words)
+    for s in range(2):
+        assert np.array_equal(m[s], _bits_ref(x[s, src], 64, words))
+    ids = torch.arange(64, dtype=torch.int32, device="cuda")
+    out_np = rnd(in_rows, 2 * in_rows).reshape(2, in_rows, 1)
+    out = dev(out_np)
+    gpu.wires_to_bits_map(P(mem), 64 * words, P(ids), 64, words, P(out), in_rows, ctypes.byref(rm), rows, None)
+    exp = out_np.copy()
+    exp[:, src] = x[:, src]
+    assert np.array_equal(host(out).reshape(2, in_rows, 1), exp)
+
+
+def test_transposes_mapped_rejects_out_of_range(gpu):
+    x = empty(2 * 100)
+    mem = empty(2 * 64 * 32)
+    rm = nt.RowMap(0, 50, 1, 100, 0, None)  # rows 50 .. 149 of a 100-row matrix
+    with pytest.raises(nt.NativeError, match="past the matrix"):
+        gpu.bits_to_wires_map(P(x), 100, 1, 64, ctypes.byref(rm), 100, P(mem), 64 * 32, 32, None)
+
+
 def _gate_ref(t, x0, x1, y0, y1, z):
     if t == 0:
         return x0 ^ y0, x1 ^ y1

@@ -7,7 +7,7 @@ points (include/aby3.h):
 * aby3h_session_*: every bench job at BASELINE.json's sizes, checked through
   size-independent properties (the revealed product against exact
   arithmetic / the truncation bound; every MSB row; the LR model against a
-  plaintext fixed-point restatement; merge layers ordered and a permutation).
+  plaintext fixed-point restatement; the 2^20-key sort equal to std::sort).
 """
 import numpy as np
 import pytest
@@ -96,11 +96,39 @@ def test_cipher_gt_vs_oracle(gpu):
     assert np.array_equal(sh_g, sh_o) and np.array_equal(p_g, p_o)
 
 
-@pytest.mark.parametrize("lens", [[1, 1], [64] * 8, [100, 3, 17, 250, 9]])
-def test_merge(gpu, lens):
-    rng = np.random.default_rng(sum(lens))
-    lists = [np.sort(rng.integers(-(2**40), 2**40, size=n, dtype=np.int64)) for n in lens]
-    assert np.array_equal(nt.sim.merge(lists), np.sort(np.concatenate(lists)))
+MERGE_CASES = [
+    # mode, dim, list lengths
+    (0, 0, [1, 1]),
+    (0, 0, [8, 8]),                   # SortTest.cpp odd_even_merge
+    (0, 0, [5, 7, 8, 3]),             # SortTest.cpp odd_even_multi_merge
+    (0, 0, [64] * 8),
+    (0, 0, [100, 3, 17, 250, 9]),     # odd count, unequal lengths (padding)
+    (1, 0, [1] * 4096),               # the sort, 12 levels, 78 rounds
+    (1, 0, [1] * 1000),               # sort of a non-power-of-two count
+    (1, 0, [3, 1, 4, 1, 5, 9, 2, 6]),
+    (2, 3, [16] * 12),                # high_dimensional_odd_even_multi_merge, 3 x 4 lists
+    (2, 2, [4, 2, 3, 5, 1, 4]),       # 2 x 3 lists (odd k)
+    (3, 4, [8] * 8),                  # high_dimensional_odd_even_merge, 4 dims
+    (3, 2, [5, 9, 2, 2]),
+]
+
+
+@pytest.mark.parametrize("mode,dim,lens", MERGE_CASES)
+def test_merge_vs_oracle(gpu, mode, dim, lens):
+    """Every party's shares of the merged output equal the oracle's batched
+    restatement (oracle/src/orc_sort.cpp), and the revealed lists are sorted."""
+    rng = np.random.default_rng(sum(lens) + mode)
+    lists = [np.sort(rng.integers(-(2**62), 2**62, size=n, dtype=np.int64)) for n in lens]
+    p_g, sh_g = nt.sim.merge(lists, mode, dim, shares=True)
+    p_o, sh_o = orc.sim_merge(nt.circuit("cmp_swap", 64), lists, mode, dim, with_shares=True)
+    assert np.array_equal(sh_g, sh_o)
+    assert np.array_equal(p_g, p_o)
+    if mode >= 2:
+        k = len(lists) // dim
+        exp = np.concatenate([np.sort(np.concatenate(lists[i * k:(i + 1) * k])) for i in range(dim)])
+    else:
+        exp = np.sort(np.concatenate(lists))
+    assert np.array_equal(p_g, exp)
 
 
 # ---- bench jobs at the BASELINE.json sizes --------------------------------
@@ -111,7 +139,8 @@ def test_merge(gpu, lens):
     (nt.JOB_MUL, [128, 128, 128, 1], 3),                # C1 GEMM
     (nt.JOB_MSB, [1 << 20], 2),                         # C3 every row checked
     (nt.JOB_LR, [100000, 128, 256, 16, 11], 20),        # C4 shapes (dataset trimmed)
-    (nt.JOB_MERGE_LAYER, [1 << 20], 2),                 # C5 one layer, 2^19 pairs
+    (nt.JOB_SORT, [1 << 20], 1),                        # C5 the whole 2^20-key sort, every key checked
+    (nt.JOB_SORT, [777], 2),                            # sort of a ragged count
     (nt.JOB_A2B, [1 << 20], 2),                         # toBinaryMatrix, every value checked
     (nt.JOB_A2B, [1000], 3),                            # ragged rows
     (nt.JOB_BITINJ, [1 << 16, 64], 2),                  # bitInjection, every bit checked

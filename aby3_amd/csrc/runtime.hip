@@ -299,21 +299,41 @@ int aby3g_stream_wait_value(aby3g_stream stream, uint64_t* word, uint64_t value)
         [&] { ABY3G_CHECK_HIP(hipStreamWaitValue64(S(stream), word, value, hipStreamWaitValueGte, ~0ull)); });
 }
 
+// the T-table image the AES round function reads, built once on the host
+static const std::vector<u32>& host_aes_tables() {
+    static const std::vector<u32> rep = [] {
+        std::vector<u32> r(kAesLdsWords);
+        for (int i = 0; i < kAesLdsWords; ++i) {
+            const u32 v = tables().T0[i >> 6];
+            r[i] = (i & 32) ? rotl(v, 8) : v;
+        }
+        return r;
+    }();
+    return rep;
+}
+
 int aby3g_aes_block_host(const uint8_t key[16], uint64_t ctr, uint8_t out[16]) {
     return guarded([&] {
-        static std::vector<u32> rep = [] {
-            std::vector<u32> r(kAesLdsWords);
-            for (int i = 0; i < kAesLdsWords; ++i) {
-                const u32 v = tables().T0[i >> 6];
-                r[i] = (i & 32) ? rotl(v, 8) : v;
-            }
-            return r;
-        }();
+        const std::vector<u32>& rep = host_aes_tables();
         AesKey k = expand_key(key);
         u64 lo, hi;
         aes_ctr_block(rep.data(), 0, k, ctr, lo, hi);
         std::memcpy(out, &lo, 8);
         std::memcpy(out + 8, &hi, 8);
+    });
+}
+
+int aby3g_aes_ctr_host(const uint8_t key[16], uint64_t ctr_base, uint64_t nblocks, uint8_t* out) {
+    return guarded([&] {
+        ABY3G_REQUIRE(key && (out || !nblocks), "null key or output");
+        const std::vector<u32>& rep = host_aes_tables();
+        AesKey k = expand_key(key);
+        for (u64 i = 0; i < nblocks; ++i) {
+            u64 lo, hi;
+            aes_ctr_block(rep.data(), 0, k, ctr_base + i, lo, hi);
+            std::memcpy(out + 16 * i, &lo, 8);
+            std::memcpy(out + 16 * i + 8, &hi, 8);
+        }
     });
 }
 

@@ -10,6 +10,7 @@
 #include <thread>
 #include "Basic.h"
 #include "Sh3Piecewise.h"
+#include "aby3ML.h"
 
 namespace aby3 {
 namespace {
@@ -23,7 +24,7 @@ struct SimParty {
     Sh3Evaluator eval;
 };
 
-void run3(int device, const std::function<void(SimParty&)>& f) {
+void run3(int device, const std::function<void(SimParty&)>& f, bool mlSeeded = false) {
     const int dv[3] = {device, device, device};
     auto comms = makeLocalRing(dv);
     std::exception_ptr err[3];
@@ -34,8 +35,14 @@ void run3(int device, const std::function<void(SimParty&)>& f) {
                 SimParty p;
                 p.idx = i;
                 p.rt.init(i, comms[i], device);
-                p.enc.init(i, toBlock(0, i), toBlock(0, (i + 1) % 3));
-                p.eval.init(i, toBlock(1, i), toBlock(1, (i + 1) % 3));
+                if (mlSeeded) {  // aby3ML::init (aby3ML.cpp:4-17)
+                    const MlSeeds ms = mlSeeds(i);
+                    p.enc.init(i, ms.encPrev, ms.encNext);
+                    p.eval.init(i, ms.evalPrev, ms.evalNext);
+                } else {
+                    p.enc.init(i, toBlock(0, i), toBlock(0, (i + 1) % 3));
+                    p.eval.init(i, toBlock(1, i), toBlock(1, (i + 1) % 3));
+                }
                 f(p);
                 p.rt.gpu().sync();
             } catch (...) {
@@ -288,6 +295,61 @@ int aby3h_sim_merge(int device, int mode, const uint64_t* lens, uint64_t nlists,
             p.enc.revealAll(p.rt, sorted, r).get();
             if (p.idx == 0 && out_sorted) std::memcpy(out_sorted, r.mData.data(), 8 * r.size());
         });
+    });
+}
+
+int aby3h_sim_lr(int device, uint64_t n, uint64_t d, uint64_t B, uint64_t D, uint64_t aB, uint64_t iters,
+                 const int64_t* X, const int64_t* Y, const uint64_t* batches, int64_t* out_w_shares,
+                 int64_t* out_w_plain) {
+    return guarded([&] {
+        if (!n || !d || !B) throw std::runtime_error("empty LR shapes");
+        i64Matrix xm = hostMat(X, n, d), ym = hostMat(Y, n, 1), w0(d, 1);
+        std::vector<u32> idx(iters * B);
+        for (u64 i = 0; i < idx.size(); ++i) {
+            if (batches[i] >= n) throw std::runtime_error("batch index out of range");
+            idx[i] = (u32)batches[i];
+        }
+        run3(
+            device,
+            [&](SimParty& p) {
+                si64Matrix sX(n, d), sY(n, 1), sW(d, 1);
+                shareIn(p, xm, sX);
+                shareIn(p, ym, sY);
+                shareIn(p, w0, sW);
+                aby3ML ml(p.rt, p.enc, p.eval, D);
+                SgdState st;
+                for (u64 t = 0; t < iters; ++t)
+                    sgdLogisticStep(ml, sX, sY, sW, std::vector<u32>(idx.begin() + t * B, idx.begin() + (t + 1) * B),
+                                    aB, st);
+                putShares(p.idx, sW, out_w_shares);
+                i64Matrix r;
+                p.enc.revealAll(p.rt, sW, r).get();
+                if (p.idx == 0 && out_w_plain) std::memcpy(out_w_plain, r.mData.data(), 8 * d);
+            },
+            true);
+    });
+}
+
+int aby3h_lr_dataset(uint64_t n, uint64_t dim, uint64_t D, int64_t* X, int64_t* Y, double* model) {
+    return guarded([&] {
+        auto m = logisticModel(dim);
+        if (model) std::memcpy(model, m.data(), 8 * dim);
+        if (!X && !Y) return;
+        i64Matrix x, y;
+        logisticModelGen(m, n, D, x, y);
+        if (X) std::memcpy(X, x.data(), 8 * x.size());
+        if (Y) std::memcpy(Y, y.data(), 8 * n);
+    });
+}
+
+int aby3h_lr_batches(uint64_t n, uint64_t B, uint64_t iters, uint64_t* out) {
+    return guarded([&] {
+        BatchSampler s(n);
+        std::vector<u64> b(B);
+        for (u64 t = 0; t < iters; ++t) {
+            s.next(b);
+            std::memcpy(out + t * B, b.data(), 8 * B);
+        }
     });
 }
 

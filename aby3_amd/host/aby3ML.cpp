@@ -1,4 +1,6 @@
 #include "aby3ML.h"
+#include <algorithm>
+#include <random>
 
 namespace aby3 {
 
@@ -46,6 +48,82 @@ void sgdLogisticStep(aby3ML& ml, const si64Matrix& X, const si64Matrix& Y, si64M
     if (st.idx.bytes() < B * 4) st.idx.reset(g, B * 4);
     toDevice(st.idx.data(), batchIdx.data(), B * 4, g);
     sgdLogisticStep(ml, X, Y, w, st.idx.as<u32>(), B, aB, st);
+}
+
+void HostPrng::get(void* dst, u64 nbytes) {
+    constexpr u64 kBlocks = 256;
+    u8* out = static_cast<u8*>(dst);
+    while (nbytes) {
+        const u64 b = mOff / 16;
+        if (mBufBlock == ~0ull || b < mBufBlock || b >= mBufBlock + kBlocks) {
+            mBuf.resize(16 * kBlocks);
+            GPU_CALL(aby3g_aes_ctr_host(mSeed.data(), b, kBlocks, mBuf.data()));
+            mBufBlock = b;
+        }
+        const u64 at = mOff - 16 * mBufBlock, take = std::min<u64>(nbytes, 16 * kBlocks - at);
+        std::memcpy(out, mBuf.data() + at, take);
+        out += take;
+        mOff += take;
+        nbytes -= take;
+    }
+}
+
+std::vector<double> logisticModel(u64 dim) {
+    HostPrng prng(toBlock(1));
+    std::vector<double> model(dim, 0.0);
+    for (u64 i = 0; i < std::min<u64>(dim, 10); ++i) model[i] = prng.get<int>() % 10;
+    return model;
+}
+
+void logisticModelGen(const std::vector<double>& model, u64 n, u64 D, i64Matrix& X, i64Matrix& Y) {
+    const u64 dim = model.size();
+    std::default_random_engine generator(234345);
+    std::normal_distribution<double> distribution(1.0, 1.0);
+    X.resize(n, dim);
+    Y.resize(n, 1);
+    const double scale = (double)(1ull << D);
+    std::vector<double> row(dim);
+    for (u64 i = 0; i < n; ++i) {
+        for (u64 j = 0; j < dim; ++j) row[j] = distribution(generator);
+        const double noise = distribution(generator);
+        double y = 0;
+        for (u64 j = 0; j < dim; ++j) y += row[j] * model[j];
+        y += noise;
+        for (u64 j = 0; j < dim; ++j) X(i, j) = (i64)(row[j] * scale);
+        Y(i, 0) = (i64)((y > 0 ? 1.0 : 0.0) * scale);
+    }
+}
+
+BatchSampler::BatchSampler(u64 n) : mPool(n), mIter(n), mPrng(toBlock(234543234)) {
+    for (u64 i = 0; i < n; ++i) mPool[i] = i;
+}
+
+void BatchSampler::next(std::vector<u64>& dest) {
+    u64 d = 0;
+    while (d != dest.size()) {
+        const u64 step = std::min<u64>(mPool.size() - mIter, dest.size() - d);
+        std::copy(mPool.begin() + mIter, mPool.begin() + mIter + step, dest.begin() + d);
+        mIter += step;
+        d += step;
+        if (mIter == mPool.size()) {
+            for (u64 i = 1; i < mPool.size(); ++i) {
+                const u64 j = mPrng.get<u64>() % (i + 1);
+                if (i != j) std::swap(mPool[i], mPool[j]);
+            }
+            mIter = 0;
+        }
+    }
+}
+
+MlSeeds mlSeeds(int pIdx) {
+    block enc[3], ev[3];
+    for (u64 i = 0; i < 3; ++i) {
+        HostPrng prng(toBlock(i));
+        enc[i] = prng.get<block>();
+        ev[i] = prng.get<block>();
+    }
+    const int prev = (pIdx + 2) % 3;
+    return MlSeeds{enc[prev], enc[pIdx], ev[prev], ev[pIdx]};
 }
 
 }  // namespace aby3

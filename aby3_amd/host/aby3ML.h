@@ -4,6 +4,7 @@
 #include "Sh3Encryptor.h"
 #include "Sh3Evaluator.h"
 #include "Sh3Piecewise.h"
+#include <vector>
 
 namespace aby3 {
 
@@ -41,5 +42,61 @@ void sgdLogisticStep(aby3ML& ml, const si64Matrix& X, const si64Matrix& Y, si64M
 // Host-index convenience form: uploads the indices (and waits for the upload).
 void sgdLogisticStep(aby3ML& ml, const si64Matrix& X, const si64Matrix& Y, si64Matrix& w,
                      const std::vector<u32>& batchIdx, u64 aB, SgdState& st);
+
+// ---- the C4 driver around the iteration (host side) -----------------------
+
+// oc::PRNG(seed) on the host: the AES-CTR byte stream under `seed`, consumed
+// contiguously, refilled 256 blocks at a time (cryptoTools PRNG.cpp) through
+// aby3g_aes_ctr_host.
+class HostPrng {
+public:
+    explicit HostPrng(block seed) : mSeed(seed) {}
+    void get(void* dst, u64 nbytes);
+    template <class T>
+    T get() {
+        T v;
+        get(&v, sizeof(T));
+        return v;
+    }
+
+private:
+    block mSeed;
+    u64 mOff = 0;          // bytes consumed
+    u64 mBufBlock = ~0ull;  // first block held in mBuf
+    std::vector<u8> mBuf;
+};
+
+// main-logistic.cpp:82-92: model(i) = PRNG(toBlock(1)).get<int>() % 10 for
+// i < min(dim, 10); the reference leaves the rest uninitialized (0 here).
+std::vector<double> logisticModel(u64 dim);
+// LogisticModelGen::sample (LinearModelGen.cpp:49-93) with setModel's
+// defaults noise = sd = 1 (LinearModelGen.h:36): libstdc++
+// default_random_engine(234345) and normal_distribution(1, 1), row-major
+// feature draws then one noise draw per row, Y = [X model + noise > 0];
+// stored as fixed point D (fp<i64, D> = i64(v * 2^D), Sh3FixedPoint.h:94-97).
+void logisticModelGen(const std::vector<double>& model, u64 n, u64 D, i64Matrix& X, i64Matrix& Y);
+// getSubset (Regression.h:24-40): mini-batches without replacement from the
+// pool 0..n-1, reshuffled with std::random_shuffle (for i = 1..n-1: swap with
+// j = r(i + 1)) when exhausted, r(m) = PRNG(toBlock(234543234)).get<u64>() % m
+// (the reference's functor type is unpinned; parity rests on the committed
+// batch list tests/golden/lr.json).
+class BatchSampler {
+public:
+    explicit BatchSampler(u64 n);
+    void next(std::vector<u64>& dest);
+
+private:
+    std::vector<u64> mPool;
+    u64 mIter;
+    HostPrng mPrng;
+};
+// aby3ML::init (aby3ML.cpp:4-17): party i's seed toBlock(i); PRNG(seed)'s
+// first block is its Sh3Encryptor seed, the second its Sh3Evaluator seed,
+// each exchanged with the neighbours (Sh3ShareGen.h:25-31): returns the
+// (prevSeed, nextSeed) pairs {enc, eval} party pIdx initialises with.
+struct MlSeeds {
+    block encPrev, encNext, evalPrev, evalNext;
+};
+MlSeeds mlSeeds(int pIdx);
 
 }  // namespace aby3

@@ -98,6 +98,7 @@ _SIGS = {
     "aby3g_probe_read": (c_int, [c_int, POINTER(c_double), POINTER(c_uint64)]),
     "aby3g_probe_reset": (c_int, []),
     "aby3g_aes_block_host": (c_int, [c_u8p, c_uint64, c_u8p]),
+    "aby3g_aes_ctr_host": (c_int, [c_u8p, c_uint64, c_uint64, c_void_p]),
     "aby3g_aes_ctr": (c_int, [c_u8p, c_uint64, c_uint64, c_void_p, c_void_p]),
     "aby3g_prng_fill": (c_int, [c_u8p, c_uint64, c_uint64, c_void_p, c_void_p]),
     "aby3g_share_draws": (c_int, [c_int, c_u8p, c_u8p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -210,6 +211,10 @@ _HOST_SIGS = {
     "aby3h_sim_circuit": (c_int, [c_int, c_char_p, c_uint64, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p]),
     "aby3h_sim_piecewise": (c_int, [c_int, c_int, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p]),
     "aby3h_sim_cipher_gt": (c_int, [c_int, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p]),
+    "aby3h_sim_lr": (c_int, [c_int, c_uint64, c_uint64, c_uint64, c_uint64, c_uint64, c_uint64, c_void_p, c_void_p,
+                             c_void_p, c_void_p, c_void_p]),
+    "aby3h_lr_dataset": (c_int, [c_uint64, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p]),
+    "aby3h_lr_batches": (c_int, [c_uint64, c_uint64, c_uint64, c_void_p]),
     "aby3h_sim_merge": (c_int, [c_int, c_int, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p]),
 }
 
@@ -391,6 +396,22 @@ class sim:
         return sh.reshape(3, 2, -1), plain
 
     @classmethod
+    def lr(cls, X, Y, batches, D=16, aB=11, device=0):
+        """SGD_Logistic iterations on (X [n][d], Y [n]) fixed point, one per row
+        of batches [iters][B]; returns (w shares [3][2][d], revealed w)."""
+        np = cls._np()
+        X = np.ascontiguousarray(X, np.int64)
+        Y = np.ascontiguousarray(Y, np.int64).reshape(-1)
+        batches = np.ascontiguousarray(batches, np.uint64)
+        n, d = X.shape
+        iters, B = batches.shape
+        sh = np.zeros(6 * d, np.int64)
+        w = np.zeros(d, np.int64)
+        cls._call("aby3h_sim_lr", device, n, d, B, D, aB, iters, cls._p(X), cls._p(Y), cls._p(batches), cls._p(sh),
+                  cls._p(w))
+        return sh.reshape(3, 2, d), w
+
+    @classmethod
     def merge(cls, lists, mode=0, dim=0, shares=False, device=0):
         """The merge network (aby3h_sim_merge): mode 0 odd_even_multi_merge of
         separately shared lists, 1 the flat form (singletons: the sort),
@@ -408,6 +429,29 @@ class sim:
 
 
 _lib = None
+
+
+def lr_dataset(n: int, dim: int = 128, D: int = 16):
+    """The C4 dataset (LogisticModelGen, fixed point D): (X [n][dim], Y [n], model [dim])."""
+    import numpy as np
+
+    X = np.zeros((n, dim), np.int64)
+    Y = np.zeros(n, np.int64)
+    m = np.zeros(dim, np.float64)
+    if host().aby3h_lr_dataset(n, dim, D, X.ctypes.data_as(c_void_p), Y.ctypes.data_as(c_void_p),
+                               m.ctypes.data_as(c_void_p)):
+        raise NativeError(host().aby3h_sim_last_error().decode())
+    return X, Y, m
+
+
+def lr_batches(n: int, B: int = 256, iters: int = 1):
+    """getSubset's first `iters` mini-batches of B rows over n: [iters][B]."""
+    import numpy as np
+
+    out = np.zeros((iters, B), np.uint64)
+    if host().aby3h_lr_batches(n, B, iters, out.ctypes.data_as(c_void_p)):
+        raise NativeError(host().aby3h_sim_last_error().decode())
+    return out
 
 
 def lib() -> _Lib:

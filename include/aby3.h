@@ -129,6 +129,20 @@ int aby3h_sim_cipher_gt(int device, const int64_t* a, const int64_t* b, uint64_t
  * [party][share][total] of the same (either may be NULL). */
 int aby3h_sim_merge(int device, int mode, const uint64_t* lens, uint64_t nlists, uint64_t dim, const int64_t* keys,
                     int64_t* out_sorted, int64_t* out_shares);
+/* `iters` SGD_Logistic iterations (aby3-ML/Regression.h:249-293) by three
+ * parties seeded as aby3ML::init (aby3ML.cpp:4-17): party 0 shares X [n][d],
+ * Y [n] (fixed point D) and w = 0 [d], iteration t uses the B row indices
+ * batches[t * B ...]. out_w_shares [party][share][d], out_w_plain [d]. */
+int aby3h_sim_lr(int device, uint64_t n, uint64_t d, uint64_t B, uint64_t D, uint64_t aB, uint64_t iters,
+                 const int64_t* X, const int64_t* Y, const uint64_t* batches, int64_t* out_w_shares,
+                 int64_t* out_w_plain);
+
+/* The C4 driver's host side (CPU only, no GPU): the LogisticModelGen dataset
+ * of main-logistic.cpp:82-100 in fixed point D (X [n][dim], Y [n], the model
+ * [dim]; NULL outputs skipped) and getSubset's first `iters` mini-batches of
+ * B rows over n (Regression.h:24-40), out [iters][B]. */
+int aby3h_lr_dataset(uint64_t n, uint64_t dim, uint64_t D, int64_t* X, int64_t* Y, double* model);
+int aby3h_lr_batches(uint64_t n, uint64_t B, uint64_t iters, uint64_t* out);
 
 #ifdef __cplusplus
 }

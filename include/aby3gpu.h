@@ -102,6 +102,11 @@ int aby3g_aes_ctr(const uint8_t key[16], uint64_t ctr_base, uint64_t nblocks, vo
  * it only to derive keys from the first blocks of a PRNG stream
  * (Sh3ShareGen.h:19-20, Sh3Evaluator.cpp:13-14, Sh3BinaryEvaluator.h:96-102). */
 int aby3g_aes_block_host(const uint8_t key[16], uint64_t ctr, uint8_t out[16]);
+/* Host-side AES-CTR of n counter blocks (one key schedule): the host PRNG
+ * of the aby3-ML driver's setup -- the data model's PRNG(toBlock(1)) and
+ * SGD_Logistic's mini-batch PRNG(toBlock(234543234)) (main-logistic.cpp:
+ * 82-92, Regression.h:24-40, 255). CPU only. */
+int aby3g_aes_ctr_host(const uint8_t key[16], uint64_t ctr_base, uint64_t nblocks, uint8_t* out);
 
 /* oc::PRNG(seed) bytes [byte_off, byte_off + nbytes) (both multiples of 8).
  * Replaces mPrevCommon/mNextCommon.get(...) (Sh3Evaluator.cpp:526-527,

@@ -128,9 +128,12 @@ __attribute__((target("aes,sse2"))) void AesNI::ctr(u64 base, u64 n, Block* out)
 }
 
 bool aesni_available() {
-    unsigned a, b, c, d;
-    if (!__get_cpuid(1, &a, &b, &c, &d)) return false;
-    return (c & bit_AES) != 0;
+    static const bool has = [] {  // cpuid traps under virtualisation: ask once
+        unsigned a, b, c, d;
+        if (!__get_cpuid(1, &a, &b, &c, &d)) return false;
+        return (c & bit_AES) != 0;
+    }();
+    return has;
 }
 
 void prng_bytes(const u8 seed[16], u64 byte_off, u64 nbytes, u8* out) {

@@ -435,72 +435,91 @@ double orc_bench_fetch_msb(uint32_t wires, const uint32_t* gates, uint64_t ngate
 }
 
 // CPU baseline of one SGD_Logistic iteration (bench.py cpu_baseline for C4,
-// Regression.h:249-293): batch gather, xw = X_B w (GEMM + truncation D),
-// sigmoid piecewise (2 MSB circuits + OT products), err = f - Y_B,
-// X_B^T err >> (D + aB), w -= update. Three parties simulated in sequence on
-// one thread (no network). Dataset `n` x `d` fixed-point rows; returns wall
-// seconds for `iters` iterations (after one untimed iteration).
+// Regression.h:249-293) on the LogisticModelGen dataset (n x d, fixed point
+// D) with aby3ML's seeds and getSubset's batches: batch gather, xw = X_B w
+// (GEMM + truncation D), sigmoid piecewise (2 MSB circuits + OT products),
+// err = f - Y_B, X_B^T err >> (D + aB), w -= update. Three parties simulated in
+// sequence on one thread (no network). Returns wall seconds for `iters`
+// iterations (after one untimed iteration).
 double orc_bench_lr(uint32_t wires, const uint32_t* gates, uint64_t ngates, const uint32_t* levels, uint64_t nlevels,
                     const uint32_t* inWires, const uint32_t* inSizes, uint64_t nin, const uint32_t* outWires,
                     const uint32_t* outSizes, uint64_t nout, uint64_t n, uint64_t d, uint64_t B, uint64_t D,
                     uint64_t aB, int iters) {
     try {
         Circuit c = toCircuit(wires, gates, ngates, levels, nlevels, inWires, inSizes, nin, outWires, outSizes, nout);
-        Piecewise pw;
-        pw.thresholds = {Coef{false, 0, -0.5}, Coef{false, 0, 0.5}};
-        pw.coefs = {{}, {Coef{false, 0, 0.5}, Coef{true, 1, 0}}, {Coef{true, 1, 0}}};
-        auto enc = makeEncryptors(0);
-        auto ev = makeEvaluators(1);
-        Mat X(n, d), Y(n, 1), w0(d, 1);
-        u64 x = 234345;
-        auto rnd = [&] {
-            x ^= x << 13;
-            x ^= x >> 7;
-            x ^= x << 17;
-            return x;
-        };
-        for (auto& v : X.v) v = (i64)(rnd() % (2ull << D)) - (1ll << D);
-        for (auto& v : Y.v) v = (rnd() & 1) ? (1ll << D) : 0;
+        std::array<Party, 3> enc, ev;
+        mlParties(enc, ev);
+        Mat X, Y, w0(d, 1);
+        logisticModelGen(logisticModel(d), n, D, X, Y);
         Shared sX = shareInt(enc, 0, X), sY = shareInt(enc, 0, Y), sW = shareInt(enc, 0, w0);
-        std::vector<u64> perm(n);
-        for (u64 i = 0; i < n; ++i) perm[i] = i;
-        for (u64 i = n; i > 1; --i) std::swap(perm[i - 1], perm[rnd() % i]);
-        auto iteration = [&](u64 t) {
-            const u64 start = (t * B) % (n - B + 1);
-            Shared XX, YY, XXt;
-            for (int p = 0; p < 3; ++p) {
-                XX[p] = SMat(B, d);
-                YY[p] = SMat(B, 1);
-                XXt[p] = SMat(d, B);
-                for (int s = 0; s < 2; ++s)
-                    for (u64 i = 0; i < B; ++i) {
-                        const u64 r = perm[start + i];
-                        for (u64 j = 0; j < d; ++j) {
-                            XX[p].s[s].v[i * d + j] = sX[p].s[s].v[r * d + j];
-                            XXt[p].s[s].v[j * B + i] = sX[p].s[s].v[r * d + j];
-                        }
-                        YY[p].s[s].v[i] = sY[p].s[s].v[r];
-                    }
-            }
-            Shared xw = mulTrunc(ev, MUL_GEMM, XX, sW, D);
-            Shared f = piecewiseEval(ev, pw, c, xw, D);
-            for (int p = 0; p < 3; ++p)
-                for (int s = 0; s < 2; ++s)
-                    for (u64 i = 0; i < B; ++i) f[p].s[s].v[i] = (i64)((u64)f[p].s[s].v[i] - (u64)YY[p].s[s].v[i]);
-            Shared upd = mulTrunc(ev, MUL_GEMM, XXt, f, D + aB);
-            for (int p = 0; p < 3; ++p)
-                for (int s = 0; s < 2; ++s)
-                    for (u64 j = 0; j < d; ++j) sW[p].s[s].v[j] = (i64)((u64)sW[p].s[s].v[j] - (u64)upd[p].s[s].v[j]);
-        };
-        iteration(0);
+        BatchSampler sampler(n);
+        std::vector<u64> batch(B);
+        sampler.next(batch);
+        sgdLogisticIteration(ev, c, sX, sY, sW, batch, D, aB);
         auto t0 = std::chrono::steady_clock::now();
-        for (int t = 1; t <= iters; ++t) iteration((u64)t);
+        for (int t = 0; t < iters; ++t) {
+            sampler.next(batch);
+            sgdLogisticIteration(ev, c, sX, sY, sW, batch, D, aB);
+        }
         auto t1 = std::chrono::steady_clock::now();
         return std::chrono::duration<double>(t1 - t0).count();
     } catch (const std::exception& e) {
         g_err = e.what();
         return -1;
     }
+}
+
+// The C4 dataset (LogisticModelGen, fixed point D): X [n][dim], Y [n],
+// model [dim] (any output may be NULL).
+int orc_lr_dataset(uint64_t n, uint64_t dim, uint64_t D, int64_t* X, int64_t* Y, double* model) {
+    return guard([&] {
+        auto m = logisticModel(dim);
+        if (model) memcpy(model, m.data(), 8 * dim);
+        if (!X && !Y) return;
+        Mat x, y;
+        logisticModelGen(m, n, D, x, y);
+        if (X) memcpy(X, x.v.data(), 8 * x.size());
+        if (Y) memcpy(Y, y.v.data(), 8 * n);
+    });
+}
+
+// getSubset's first `iters` mini-batches of B indices over n rows: out [iters][B]
+int orc_lr_batches(uint64_t n, uint64_t B, uint64_t iters, uint64_t* out) {
+    return guard([&] {
+        BatchSampler s(n);
+        std::vector<u64> b(B);
+        for (u64 t = 0; t < iters; ++t) {
+            s.next(b);
+            memcpy(out + t * B, b.data(), 8 * B);
+        }
+    });
+}
+
+// `iters` SGD_Logistic iterations, 3 parties with aby3ML's seeds: party 0
+// shares X [n][d], Y [n], w = 0 [d] (localFixedMatrix, in that order), then
+// iteration t uses batch [t][B]. out_w_shares [3][2][d], out_w_plain [d].
+int orc_sim_lr(uint32_t wires, const uint32_t* gates, uint64_t ngates, const uint32_t* levels, uint64_t nlevels,
+               const uint32_t* inWires, const uint32_t* inSizes, uint64_t nin, const uint32_t* outWires,
+               const uint32_t* outSizes, uint64_t nout, uint64_t n, uint64_t d, uint64_t B, uint64_t D, uint64_t aB,
+               uint64_t iters, const int64_t* X, const int64_t* Y, const uint64_t* batches, int64_t* out_w_shares,
+               int64_t* out_w_plain) {
+    return guard([&] {
+        Circuit c = toCircuit(wires, gates, ngates, levels, nlevels, inWires, inSizes, nin, outWires, outSizes, nout);
+        std::array<Party, 3> enc, ev;
+        mlParties(enc, ev);
+        Shared sX = shareInt(enc, 0, toMat(X, n, d)), sY = shareInt(enc, 0, toMat(Y, n, 1));
+        Shared sW = shareInt(enc, 0, Mat(d, 1));
+        for (u64 t = 0; t < iters; ++t) {
+            std::vector<u64> batch(batches + t * B, batches + (t + 1) * B);
+            for (u64 r : batch)
+                if (r >= n) throw std::runtime_error("batch index out of range");
+            sgdLogisticIteration(ev, c, sX, sY, sW, batch, D, aB);
+        }
+        if (!consistent(sW)) throw std::runtime_error("inconsistent shares");
+        if (out_w_shares) putShared(sW, out_w_shares);
+        Mat w = revealInt(sW);
+        if (out_w_plain) memcpy(out_w_plain, w.v.data(), 8 * d);
+    });
 }
 
 }  // extern "C"

@@ -278,3 +278,44 @@ std::vector<Shared> hdMultiMerge(std::array<Party, 3>& ev, const Circuit& cmpSwa
                                  std::vector<std::vector<Shared>> data);
 
 }  // namespace orc
+
+namespace orc {
+
+// --------------------------------------------------------------------------
+// aby3-ML logistic regression (C4).
+// --------------------------------------------------------------------------
+// main-logistic.cpp:82-92: model(i) = PRNG(toBlock(1)).get<int>() % 10 for
+// i < min(dim, 10); the reference leaves the other entries uninitialized
+// (Eigen), they are 0 here.
+std::vector<double> logisticModel(u64 dim);
+// LogisticModelGen::sample (LinearModelGen.cpp:49-93): libstdc++
+// default_random_engine(234345), normal_distribution(1, 1) (setModel's
+// defaults, LinearModelGen.h:36), row-major X draws then one noise draw per
+// row; Y = [X model + noise > 0]; both converted to fixed point D as
+// fp<i64, D>::operator=(double) (Sh3FixedPoint.h:94-97: i64(v * 2^D)).
+void logisticModelGen(const std::vector<double>& model, u64 n, u64 D, Mat& X, Mat& Y);
+// getSubset (Regression.h:24-40) over the pool 0..n-1, reshuffled by
+// std::random_shuffle (libstdc++: for i in 1..n-1, j = r(i + 1), swap) with
+// the cryptoTools PRNG(toBlock(234543234)) as the RNG functor r(m) =
+// get<u64>() % m (the functor's integer type is not pinned: parity is
+// defined on the committed batch list, tests/golden/lr.json).
+struct BatchSampler {
+    std::vector<u64> pool;
+    u64 iter;
+    Stream prng;
+    explicit BatchSampler(u64 n);
+    void next(std::vector<u64>& dest);
+};
+// aby3ML::init (aby3ML.cpp:4-17): party i's seed toBlock(i); PRNG(seed)'s
+// first block seeds its Sh3Encryptor, the second its Sh3Evaluator, each
+// exchanged with the neighbours (Sh3ShareGen.h:25-31: nextSeed = own seed,
+// prevSeed = the previous party's).
+void mlParties(std::array<Party, 3>& enc, std::array<Party, 3>& ev);
+// One SGD_Logistic iteration (Regression.h:249-293): XX, YY = extractBatch;
+// xw = mul(XX, w) (trunc D); f = logisticFunc(xw) (Sh3Piecewise, aby3ML.h:
+// 121-139, helper circuit supplied); w -= mulTruncate(XX^T, f - YY, aB)
+// (trunc D + aB).
+void sgdLogisticIteration(std::array<Party, 3>& ev, const Circuit& pwHelper, const Shared& X, const Shared& Y,
+                          Shared& w, const std::vector<u64>& batch, u64 D, u64 aB);
+
+}  // namespace orc

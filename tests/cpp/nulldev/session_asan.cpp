@@ -47,6 +47,11 @@ int main() {
         const uint64_t n = mode == 3 ? 4 : 6, dim = mode >= 2 ? 2 : 0;
         if (aby3h_sim_merge(0, mode, lens, n, dim, keys.data(), sorted.data(), msh.data())) return fail("sim_merge");
     }
+    std::vector<int64_t> lx(500 * 8, 1 << 16), ly(500, 0), wsh(6 * 8), wpl(8);
+    std::vector<uint64_t> lb(2 * 64);
+    if (aby3h_lr_batches(500, 64, 2, lb.data())) return fail("lr_batches");
+    if (aby3h_sim_lr(0, 500, 8, 64, 16, 11, 2, lx.data(), ly.data(), lb.data(), wsh.data(), wpl.data()))
+        return fail("sim_lr");
     std::printf("session_asan: ok\n");
     return 0;
 }

@@ -159,10 +159,28 @@ def merge(st):
     return out
 
 
+def lr():
+    # C4 driver (main-logistic.cpp:82-140, Regression.h:24-58, 249-293): the
+    # model, the first mini-batches getSubset draws over the 10^6-row dataset,
+    # the dataset's first rows, and every party's w shares after 3 iterations
+    # on the first 4096 rows (aby3ML seeds, the oracle's batches over 4096 rows)
+    X, Y, model = orc.lr_dataset(4096, 128, 16)
+    assert list(model[10:]) == [0.0] * 118 and all(abs(v) <= 9 for v in model[:10])
+    b_full = orc.lr_batches(10**6, 256, 2)
+    assert len(set(L(b_full))) == 512  # without replacement
+    b = orc.lr_batches(4096, 256, 3)
+    sh, w = orc.sim_lr(nt.circuit("int_Sh3Piecewise_helper", 64, 2), X, Y, b)
+    # the revealed model moves along the planted one (first updates)
+    assert np.sign(w[0]) == np.sign(model[0]) and np.sign(w[1]) == np.sign(model[1])
+    return {"lr_4096x128_B256": dict(n=4096, d=128, B=256, D=16, aB=11, iters=3, model=[float(v) for v in model],
+                                     batches_1e6=L(b_full), batches=L(b), x_rows01=L(X[:2]), y_head=L(Y[:64]),
+                                     x_sum=int(X.sum()), y_sum=int(Y.sum()), w_shares=L(sh), w=L(w))}
+
+
 def main():
     st = Stream()
     files = dict(arith=arith(st), binary=binary(st), fetch_msb=fetch_msb(st), piecewise=piecewise(st),
-                 merge=merge(st))
+                 merge=merge(st), lr=lr())
     for name, data in files.items():
         path = os.path.join(HERE, f"{name}.json")
         with open(path, "w") as f:

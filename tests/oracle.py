@@ -186,3 +186,37 @@ def sim_merge(cir, lists, mode: int = 0, dim: int = 0, with_shares: bool = False
     _check(dll().orc_sim_merge(*args, c_int(mode), _p(lens), c_uint64(len(lists)), c_uint64(dim), _p(keys), _p(out),
                                _p(sh)))
     return (out, sh.reshape(3, 2, n)) if with_shares else out
+
+
+def lr_dataset(n: int, dim: int = 128, D: int = 16):
+    """The oracle's LogisticModelGen restatement: (X [n][dim], Y [n], model [dim])."""
+    X = np.zeros((n, dim), dtype=np.int64)
+    Y = np.zeros(n, dtype=np.int64)
+    m = np.zeros(dim, dtype=np.float64)
+    _check(dll().orc_lr_dataset(c_uint64(n), c_uint64(dim), c_uint64(D), _p(X), _p(Y), _p(m)))
+    return X, Y, m
+
+
+def lr_batches(n: int, B: int = 256, iters: int = 1):
+    """The oracle's getSubset restatement: the first `iters` mini-batches [iters][B]."""
+    out = np.zeros((iters, B), dtype=np.uint64)
+    _check(dll().orc_lr_batches(c_uint64(n), c_uint64(B), c_uint64(iters), _p(out)))
+    return out
+
+
+def sim_lr(cir, X, Y, batches, D: int = 16, aB: int = 11):
+    """SGD_Logistic iterations on the oracle (aby3ML seeds, party 0 shares X, Y,
+    w = 0); cir: the int_Sh3Piecewise_helper(64, 2) circuit. Returns
+    (w shares [3][2][d], revealed w)."""
+    args, keep = _cir_args(cir)
+    X = np.ascontiguousarray(X, dtype=np.int64)
+    Y = np.ascontiguousarray(Y, dtype=np.int64).reshape(-1)
+    batches = np.ascontiguousarray(batches, dtype=np.uint64)
+    n, d = X.shape
+    iters, B = batches.shape
+    sh = np.zeros(6 * d, dtype=np.int64)
+    w = np.zeros(d, dtype=np.int64)
+    u = c_uint64
+    _check(dll().orc_sim_lr(*args, u(n), u(d), u(B), u(D), u(aB), u(iters), _p(X), _p(Y), _p(batches), _p(sh),
+                            _p(w)))
+    return sh.reshape(3, 2, d), w

@@ -86,7 +86,9 @@ __global__ void __launch_bounds__(kBlock, 4) k_bitinj_send(const u32* __restrict
         } else {  // prev words pwb (odd) and pwb + 1 straddle two blocks
             u64 alo, ahi, blo, bhi;
             aes_ctr_block(lds, lane32, kn, c, nv[0], nv[1]);
-            aes_ctr_block2(lds, lane32, kp, pwb >> 1, kp, (pwb >> 1) + 1, alo, ahi, blo, bhi);
+            // the second word's block from its own index: pwb wraps to ~0 when
+            // nw0 is odd and pw0 == 0 (bit -1 of the first counter is not emitted)
+            aes_ctr_block2(lds, lane32, kp, pwb >> 1, kp, (pwb + 1) >> 1, alo, ahi, blo, bhi);
             pv[0] = ahi;
             pv[1] = blo;
         }

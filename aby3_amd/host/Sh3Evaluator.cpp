@@ -44,23 +44,40 @@ Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, const si64Matrix& A, const si64Matri
     return asyncMul(dep, A, B, C, mMulMode);
 }
 
+// C's storage overlaps an operand's (C = A * B with C == A, say): the
+// reference evaluates the product into an Eigen temporary before assigning,
+// so the product goes to a private matrix that replaces C once complete.
+static bool aliases(const SharedMat& C, const SharedMat& X) {
+    if (&C == &X) return true;
+    if (C.empty() || X.empty()) return false;
+    const char *c = (const char*)C.data(), *x = (const char*)X.data();
+    return c < x + 2 * X.size() * sizeof(i64) && x < c + 2 * C.size() * sizeof(i64);
+}
+
 Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, const si64Matrix& A, const si64Matrix& B, si64Matrix& C, MulMode mode) {
     return dep
         .then([this, &A, &B, &C, mode](CommPkg& comm, Sh3Task& self) {
             Gpu& g = self.getRuntime().gpu();
             u64 M, K, N;
             shape(mode, A, B, M, K, N);
-            C.resize(M, N);
+            std::shared_ptr<si64Matrix> tmp;
+            if (aliases(C, A) || aliases(C, B)) tmp = std::make_shared<si64Matrix>();
+            si64Matrix& out = tmp ? *tmp : C;
+            out.resize(M, N);
             const u64 n = M * N;
             size_t wsBytes = 0;
             void* ws = workspace(mode, M, K, N, wsBytes, g);
             // C0 = share product + getShare() per element (Sh3Evaluator.cpp:101-105)
             aby3g_zero_share zs = mShareGen.zeroShare(mShareGen.takeDraws(n));
-            GPU_CALL(aby3g_mul_local((int)mode, A.data(), B.data(), C.share(0), M, K, N,
+            GPU_CALL(aby3g_mul_local((int)mode, A.data(), B.data(), out.share(0), M, K, N,
                                      DEBUG_disable_randomization ? nullptr : &zs, ws, wsBytes, g.stream()));
-            comm.mNext.asyncSendDevice(C.share(0), n * sizeof(i64), g);
-            auto fu = comm.mPrev.asyncRecvDevice(C.share(1), n * sizeof(i64), g);
-            self.then([fu](CommPkg&, Sh3Task&) { fu.get(); });
+            comm.mNext.asyncSendDevice(out.share(0), n * sizeof(i64), g);
+            auto fu = comm.mPrev.asyncRecvDevice(out.share(1), n * sizeof(i64), g);
+            si64Matrix* caller = &C;
+            self.then([fu, tmp, caller](CommPkg&, Sh3Task&) {
+                fu.get();
+                if (tmp) *caller = std::move(*tmp);
+            });
         })
         .getClosure();
 }
@@ -94,11 +111,14 @@ Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, const si64Matrix& A, const si64Matri
 Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, const si64Matrix& A, const si64Matrix& B, si64Matrix& C, u64 shift,
                                MulMode mode) {
     return dep
-        .then([this, &A, &B, &C, shift, mode](CommPkg& comm, Sh3Task& self) {
+        .then([this, &A, &B, &Cref = C, shift, mode](CommPkg& comm, Sh3Task& self) {
             Gpu& g = self.getRuntime().gpu();
             u64 M, K, N;
             shape(mode, A, B, M, K, N);
             const u64 n = M * N, bytes = n * sizeof(i64);
+            std::shared_ptr<si64Matrix> tmp;
+            if (aliases(Cref, A) || aliases(Cref, B)) tmp = std::make_shared<si64Matrix>();
+            si64Matrix& C = tmp ? *tmp : Cref;
             C.resize(M, N);
             // z = product - r is revealed to P0 and P1 zero-copy: the buffer
             // itself is the message (Channel::asyncSendShared)
@@ -148,15 +168,20 @@ Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, const si64Matrix& A, const si64Matri
                 auto fu0 = comm.mNext.asyncRecvShared(bytes, g);
                 auto fu1 = comm.mPrev.asyncRecvShared(bytes, g);
                 // round 2 (:703-719): C[p] += (z0 + z1 + z2) >> d
-                self.then([z, fu0, fu1, &C, shift, p, n](CommPkg&, Sh3Task& self2) {
+                si64Matrix* dst = &C;     // the product (C itself or the private matrix)
+                si64Matrix* caller = &Cref;  // the caller's C (outlives the task)
+                self.then([z, fu0, fu1, dst, caller, tmp, shift, p, n](CommPkg&, Sh3Task& self2) {
                     Gpu& g2 = self2.getRuntime().gpu();
                     auto zn = fu0.getShared();
                     auto zp = fu1.getShared();
                     GPU_CALL(aby3g_trunc_finalize((int)p, zn->as<i64>(), zp->as<i64>(), z->as<i64>(), (unsigned)shift,
-                                                  C.data(), n, g2.stream()));
+                                                  dst->data(), n, g2.stream()));
                     zn->fence(g2.stream());
                     zp->fence(g2.stream());
+                    if (tmp) *caller = std::move(*tmp);
                 });
+            } else if (tmp) {
+                Cref = std::move(*tmp);
             }
         })
         .getClosure();

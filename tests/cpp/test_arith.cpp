@@ -8,7 +8,8 @@
 using namespace aby3;
 using namespace harness;
 
-static void mulTest(MulMode mode, u64 M, u64 K, u64 N, bool trunc, u64 d, u64 seed) {
+// alias: 0 C separate, 1 C is A, 2 C is B (the product overwrites an operand)
+static void mulTest(MulMode mode, u64 M, u64 K, u64 N, bool trunc, u64 d, u64 seed, int alias = 0) {
     const u64 bRows = mode == MulMode::Gemm ? K : M;
     const u64 bCols = mode == MulMode::Gemm ? N : K;
     i64Matrix a = randMat(M, K, seed), b = randMat(bRows, bCols, seed + 1);
@@ -27,13 +28,14 @@ static void mulTest(MulMode mode, u64 M, u64 K, u64 N, bool trunc, u64 d, u64 se
             p.enc.remoteIntMatrix(p.rt, A).get();
             p.enc.remoteIntMatrix(p.rt, B).get();
         }
+        si64Matrix& out = alias == 1 ? A : alias == 2 ? B : C;
         if (trunc)
-            p.eval.asyncMul(p.rt, A, B, C, d, mode).get();
+            p.eval.asyncMul(p.rt, A, B, out, d, mode).get();
         else
-            p.eval.asyncMul(p.rt, A, B, C, mode).get();
-        got.put(p.idx, C);
+            p.eval.asyncMul(p.rt, A, B, out, mode).get();
+        got.put(p.idx, out);
         i64Matrix r;
-        p.enc.revealAll(p.rt, C, r).get();
+        p.enc.revealAll(p.rt, out, r).get();
         if (p.idx == 0) revealed = r.mData;
     });
     auto enc = orc::makeEncryptors(0);
@@ -138,6 +140,12 @@ int main() {
     test("asyncMul_trunc_gemm_4x4_D8 (matrixFixed_test)", [] { mulTest(MulMode::Gemm, 4, 4, 4, true, 8, 6); });
     test("asyncMul_trunc_gemm_128x256x1_D27 (LR update)", [] { mulTest(MulMode::Gemm, 128, 256, 1, true, 27, 7); });
     test("asyncMul_trunc_gemm_256x256x256_D16", [] { mulTest(MulMode::Gemm, 256, 256, 256, true, 16, 8); });
+    // C aliasing an operand (C = A * B with C == A or B): the reference forms the
+    // product in an Eigen temporary before assigning
+    test("asyncMul_gemm_alias_C_is_A_64", [] { mulTest(MulMode::Gemm, 64, 64, 64, false, 0, 12, 1); });
+    test("asyncMul_trunc_gemm_alias_C_is_A_512_D16", [] { mulTest(MulMode::Gemm, 512, 512, 512, true, 16, 13, 1); });
+    test("asyncMul_trunc_gemm_alias_C_is_B_300x300x40", [] { mulTest(MulMode::Gemm, 300, 300, 40, true, 16, 14, 2); });
+    test("asyncMul_trunc_hadamard_alias_C_is_B_100x7_D8", [] { mulTest(MulMode::Hadamard, 100, 7, 7, true, 8, 15, 2); });
     test("asyncMul_si64_x_sb (sh3_asyncArithBinMul_test)", [] { bitMulTest(false, 100, 9); });
     test("asyncMul_i64_x_sb (sh3_asyncPubArithBinMul_test)", [] { bitMulTest(true, 100, 10); });
     test("asyncMul_si64_x_sb_1000", [] { bitMulTest(false, 1000, 11); });

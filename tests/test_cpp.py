@@ -25,11 +25,6 @@ def test_circuit_library_plaintext():
     _run("test_circuits", 120)
 
 
-def test_bitsliced_aes_matches_oracle():
-    # the device's bitsliced AES-CTR (aby3_amd/csrc/aes_bs.h) compiled for the host
-    _run("test_aes_bs", 120)
-
-
 @pytest.mark.gpu
 def test_arith_protocols_gpu():
     _run("test_arith", 600)

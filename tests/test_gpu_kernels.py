@@ -55,7 +55,6 @@ def k16(seed):
     return bytes(np.random.default_rng(seed).integers(0, 256, size=16, dtype=np.uint8))
 
 
-# sizes >= 2^16 blocks take the bitsliced kernels, smaller ones the T-table ones
 @pytest.mark.parametrize("base,n", [(0, 1), (5, 1000), (2**40 + 3, 4097), (2047, 70001), (2**64 - 100000, 99999)])
 def test_aes_ctr(gpu, base, n):
     key = k16(1)
@@ -304,6 +303,42 @@ def test_transposes_mapped_rejects_out_of_range(gpu):
     rm = nt.RowMap(0, 50, 1, 100, 0, None)  # rows 50 .. 149 of a 100-row matrix
     with pytest.raises(nt.NativeError, match="past the matrix"):
         gpu.bits_to_wires_map(P(x), 100, 1, 64, ctypes.byref(rm), 100, P(mem), 64 * 32, 32, None)
+
+
+@pytest.mark.parametrize("next_off,prev_off,rows,bits,two", [
+    (8, 0, 70, 3, 0),      # next word offset odd, prev at 0: the straddling path's first counter
+    (16, 8, 33, 64, 1),    # offsets of different parity, one OT
+    (24, 40, 50, 7, 0),    # same parity (both odd words)
+])
+def test_bitinj_send_vs_oracle(gpu, next_off, prev_off, rows, bits, two):
+    """bitInjection sender (Sh3Converter.cpp:319-361) through the C-ABI:
+    dest words from the next / prev streams at the given offsets, OT messages
+    m[c] = -d0 - d1 + (c ^ b) padded with AES(key, ctr + k)."""
+    cols = (bits + 63) // 64
+    x = rnd(rows + bits, 2 * rows * cols).reshape(2, rows, cols)
+    if bits % 64:
+        x[:, :, -1] &= np.int64((1 << (bits % 64)) - 1)
+    n = rows * bits
+    sn, sp, ka, kb = k16(1), k16(2), k16(3), k16(4)
+    nxt = nt.StreamPos(nt.key16(sn), next_off)
+    prv = nt.StreamPos(nt.key16(sp), prev_off)
+    dest, ma = empty(2 * n), empty(2 * n)
+    mb = None if two else empty(2 * n)
+    gpu.bitinj_send(P(dev(x)), rows, cols, bits, ctypes.byref(nxt), ctypes.byref(prv), nt.key16(ka), 5,
+                    nt.key16(kb), 9, P(dest), P(ma), P(mb) if mb is not None else None, None)
+    d0 = orc.prng_i64(sn, next_off, n).view(np.uint64)
+    d1 = orc.prng_i64(sp, prev_off, n).view(np.uint64)
+    xv = (x[0] ^ x[1]).view(np.uint64)
+    k = np.arange(n)
+    b = (xv[k // bits, (k % bits) // 64] >> (k % bits % 64).astype(np.uint64)) & np.uint64(1)
+    base = (np.uint64(0) - d0 - d1)
+    m = np.stack([base + b, base + (b ^ np.uint64(1))], axis=1).reshape(-1)
+    got = host(dest).view(np.uint64).reshape(2, n)
+    assert np.array_equal(got[0], d0) and np.array_equal(got[1], d1)
+    pa = orc.aes_ctr(ka, 5, n)
+    assert np.array_equal(host(ma).view(np.uint64), pa ^ m)
+    if mb is not None:
+        assert np.array_equal(host(mb).view(np.uint64), orc.aes_ctr(kb, 9, n) ^ m)
 
 
 def _gate_ref(t, x0, x1, y0, y1, z):

@@ -299,6 +299,55 @@ int aby3g_stream_wait_value(aby3g_stream stream, uint64_t* word, uint64_t value)
         [&] { ABY3G_CHECK_HIP(hipStreamWaitValue64(S(stream), word, value, hipStreamWaitValueGte, ~0ull)); });
 }
 
+static_assert(sizeof(aby3g_ipc_handle) == sizeof(hipIpcMemHandle_t), "IPC handle size");
+int aby3g_ipc_get_handle(void* ptr, aby3g_ipc_handle* handle) {
+    return guarded([&] {
+        ABY3G_REQUIRE(ptr != nullptr && handle != nullptr, "null argument");
+        hipIpcMemHandle_t h;
+        ABY3G_CHECK_HIP(hipIpcGetMemHandle(&h, ptr));
+        std::memcpy(handle->bytes, &h, sizeof(h));
+    });
+}
+int aby3g_ipc_open(const aby3g_ipc_handle* handle, void** ptr) {
+    return guarded([&] {
+        ABY3G_REQUIRE(ptr != nullptr && handle != nullptr, "null argument");
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, handle->bytes, sizeof(h));
+        ABY3G_CHECK_HIP(hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess));
+    });
+}
+int aby3g_ipc_close(void* ptr) {
+    return guarded([&] { ABY3G_CHECK_HIP(hipIpcCloseMemHandle(ptr)); });
+}
+int aby3g_host_register(void* host, size_t bytes, void** dev) {
+    return guarded([&] {
+        ABY3G_REQUIRE(host != nullptr && dev != nullptr && ((uintptr_t)host & 4095) == 0, "host memory must be page aligned");
+        ABY3G_CHECK_HIP(hipHostRegister(host, bytes, hipHostRegisterMapped));
+        ABY3G_CHECK_HIP(hipHostGetDevicePointer(dev, host, 0));
+    });
+}
+int aby3g_host_unregister(void* host) {
+    return guarded([&] { ABY3G_CHECK_HIP(hipHostUnregister(host)); });
+}
+int aby3g_enable_peer_access(int device, int peer) {
+    return guarded([&] {
+        if (device == peer) return;
+        int can = 0;
+        ABY3G_CHECK_HIP(hipDeviceCanAccessPeer(&can, device, peer));
+        ABY3G_REQUIRE(can, "devices cannot access each other's memory (no peer path)");
+        int cur = 0;
+        ABY3G_CHECK_HIP(hipGetDevice(&cur));
+        ABY3G_CHECK_HIP(hipSetDevice(device));
+        hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+        (void)hipSetDevice(cur);
+        if (e == hipErrorPeerAccessAlreadyEnabled) {
+            (void)hipGetLastError();
+            return;
+        }
+        ABY3G_CHECK_HIP(e);
+    });
+}
+
 // the T-table image the AES round function reads, built once on the host
 static const std::vector<u32>& host_aes_tables() {
     static const std::vector<u32> rep = [] {

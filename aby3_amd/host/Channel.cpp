@@ -1,4 +1,5 @@
 #include "Channel.h"
+#include "Link.h"
 #include <chrono>
 #include <cstdlib>
 #include <atomic>
@@ -27,6 +28,33 @@ struct Msg {
     // to *sigWord when the payload is ready (cheaper than an event hand-off)
     u64* sigWord = nullptr;
     u64 sigValue = 0;
+    // from another process (LinkEnd): the payload sits in the sender's
+    // staging slot `lslot` (generation lgen, IPC handle lh) once the link's
+    // ready word reaches lseq
+    bool link = false;
+    u32 lslot = 0;
+    u64 lgen = 0, lseq = 0;
+    int ldevice = -1;
+    aby3g_ipc_handle lh{};
+};
+
+// a message descriptor on a link's ring (host payloads follow it)
+struct WireMsg {
+    u64 bytes;
+    u32 kind;  // 0 host payload, 1 device payload
+    u32 slot;
+    u64 gen, seq;
+    i64 device;  // the sender's device
+    aby3g_ipc_handle handle;
+};
+constexpr u32 kNoSlot = ~0u;
+
+// a sender's staging slot of a link (device memory exported through IPC)
+struct LinkSlot {
+    void* ptr = nullptr;
+    size_t cap = 0;
+    u64 gen = 0, lastSeq = 0;
+    aby3g_ipc_handle h{};
 };
 }  // namespace
 
@@ -47,6 +75,14 @@ struct Pipe {
     u64* word = nullptr;  // allocated by the sender on first use
     u64 devSeq = 0;       // device payloads signalled so far (sender thread only)
 
+    // cross-process direction: this process holds one end of it
+    std::unique_ptr<LinkEnd> link;
+    int linkDevice = -1;                      // this end's device
+    std::vector<LinkSlot> lslots;             // sender: staging slots
+    std::vector<void*> retired;               // sender: outgrown slots (freed at teardown)
+    std::map<std::pair<u32, u64>, void*> mapped;  // receiver: opened slots by (slot, gen)
+    u64 linkRead = 0;                         // receiver: messages taken off the ring
+
     // readiness of a device payload enqueued so far on `gpu`'s stream
     void signalReady(Msg& m, Gpu& gpu, Event* fallback) {
         if (signalDevice >= 0 && signalDevice == gpu.device()) {
@@ -60,6 +96,13 @@ struct Pipe {
     }
 
     ~Pipe() {
+        if (link) {
+            aby3g_set_device(linkDevice);
+            aby3g_device_sync();
+            for (auto& m : mapped) aby3g_ipc_close(m.second);
+            for (auto& s : lslots) aby3g_free(s.ptr);
+            for (void* p : retired) aby3g_free(p);
+        }
         for (auto& s : slots)
             if (s->ptr) {
                 aby3g_set_device(s->device);
@@ -76,6 +119,10 @@ struct Pipe {
     std::atomic<u64> published{0};  // messages pushed so far (sendSeq, readable without the lock)
 
     void push(Msg&& m) {
+        if (link) {
+            linkPush(m);
+            return;
+        }
         std::lock_guard<std::mutex> lk(mu);
         sent += m.bytes;
         msgs.emplace(sendSeq++, std::move(m));
@@ -91,6 +138,14 @@ struct Pipe {
             std::chrono::steady_clock::time_point t0;
             ~WaitClock() { t_recvWaitUs += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count(); }
         } clock{t0};
+        if (link) {
+            std::lock_guard<std::mutex> lk(mu);
+            while (!msgs.count(ticket)) linkTake();
+            Msg m = std::move(msgs[ticket]);
+            msgs.erase(ticket);
+            received += m.bytes;
+            return m;
+        }
         while (published.load(std::memory_order_acquire) <= ticket &&
                std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(kSpinUs)) {
             for (int i = 0; i < 64; ++i) __builtin_ia32_pause();
@@ -121,6 +176,108 @@ struct Pipe {
     void releaseSlot(Slot* s) {
         std::lock_guard<std::mutex> lk(mu);
         s->busy = false;
+    }
+
+    // ---- cross-process ends ----
+    // sender: host payloads go onto the ring; device payloads are copied into
+    // a staging slot whose previous message the receiver has already taken
+    // (its copy-out enqueued), the stream waiting for that copy-out to finish.
+    void linkPush(const Msg& m) {
+        std::lock_guard<std::mutex> lk(mu);
+        WireMsg w{};
+        w.bytes = m.bytes;
+        w.kind = 0;
+        w.slot = kNoSlot;
+        w.device = linkDevice;
+        sent += m.bytes;
+        link->write(&w, sizeof w);
+        if (m.bytes) link->write(m.host.data(), m.bytes);
+    }
+    void linkSendDevice(const void* src, size_t bytes, Gpu& gpu) {
+        std::lock_guard<std::mutex> lk(mu);
+        WireMsg w{};
+        w.bytes = bytes;
+        w.kind = 1;
+        w.slot = kNoSlot;
+        w.device = gpu.device();
+        if (bytes) {
+            int k = -1;
+            for (size_t i = 0; i < lslots.size() && k < 0; ++i)
+                if (lslots[i].cap >= bytes && link->posted((u32)i).load(std::memory_order_acquire) >= lslots[i].lastSeq)
+                    k = (int)i;
+            for (size_t i = 0; i < lslots.size() && k < 0; ++i)
+                if (link->posted((u32)i).load(std::memory_order_acquire) >= lslots[i].lastSeq) {
+                    // free but too small: replace it (the receiver may still be
+                    // reading the old buffer on its stream: retire, don't free)
+                    k = (int)i;
+                    retired.push_back(lslots[i].ptr);
+                    lslots[i].ptr = nullptr;
+                }
+            if (k < 0) {
+                if (lslots.size() >= LinkEnd::kMaxSlots) throw std::runtime_error("link: too many messages in flight");
+                lslots.emplace_back();
+                k = (int)lslots.size() - 1;
+            }
+            LinkSlot& s = lslots[(size_t)k];
+            if (!s.ptr) {
+                s.cap = std::max<size_t>(bytes, 64 << 10);
+                GPU_CALL(aby3g_malloc(&s.ptr, s.cap));
+                GPU_CALL(aby3g_ipc_get_handle(s.ptr, &s.h));
+                ++s.gen;
+            } else if (s.lastSeq) {
+                // the receiver's copy-out of the slot's previous message
+                GPU_CALL(aby3g_stream_wait_value(gpu.stream(), link->consumedDev((u32)k), s.lastSeq));
+            }
+            GPU_CALL(aby3g_memcpy(s.ptr, src, bytes, 2, gpu.stream()));
+            s.lastSeq = ++devSeq;
+            GPU_CALL(aby3g_stream_write_value(gpu.stream(), link->readyDev(), s.lastSeq));
+            w.slot = (u32)k;
+            w.gen = s.gen;
+            w.seq = s.lastSeq;
+            w.handle = s.h;
+        }
+        sent += bytes;
+        link->write(&w, sizeof w);
+    }
+    // receiver: the next message off the ring, filed under its ticket
+    void linkTake() {
+        WireMsg w;
+        link->read(&w, sizeof w);
+        Msg m;
+        m.bytes = w.bytes;
+        if (w.kind == 0) {
+            m.host.resize(w.bytes);
+            if (w.bytes) link->read(m.host.data(), w.bytes);
+        } else {
+            m.device = true;
+            m.link = true;
+            m.lslot = w.slot;
+            m.lgen = w.gen;
+            m.lseq = w.seq;
+            m.ldevice = (int)w.device;
+            m.lh = w.handle;
+        }
+        msgs.emplace(linkRead++, std::move(m));
+    }
+    // receiver: enqueue the copy of a linked device payload into dst
+    void linkCopyOut(const Msg& m, void* dst, Gpu& g) {
+        if (!m.bytes) return;
+        void* src;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            auto key = std::make_pair(m.lslot, m.lgen);
+            auto it = mapped.find(key);
+            if (it == mapped.end()) {
+                void* p = nullptr;
+                GPU_CALL(aby3g_ipc_open(&m.lh, &p));
+                it = mapped.emplace(key, p).first;
+            }
+            src = it->second;
+        }
+        GPU_CALL(aby3g_stream_wait_value(g.stream(), link->readyDev(), m.lseq));
+        GPU_CALL(aby3g_memcpy(dst, src, m.bytes, m.ldevice == g.device() ? 2 : 3, g.stream()));
+        GPU_CALL(aby3g_stream_write_value(g.stream(), link->consumedDev(m.lslot), m.lseq));
+        link->posted(m.lslot).store(m.lseq, std::memory_order_release);
     }
 };
 
@@ -155,9 +312,14 @@ void RecvFuture::get() const {
         if (st.bytes) std::memcpy(st.dst, m.host.data(), st.bytes);
     } else {
         if (!m.device) throw std::runtime_error("channel: host payload received into a device buffer");
-        Slot* s = m.slot;
         Gpu& g = *st.gpu;
         GPU_CALL(aby3g_set_device(g.device()));
+        if (m.link) {
+            st.pipe->linkCopyOut(m, st.dst, g);
+            st.done = true;
+            return;
+        }
+        Slot* s = m.slot;
         if (st.bytes) {
             if (m.sigWord)
                 GPU_CALL(aby3g_stream_wait_value(g.stream(), m.sigWord, m.sigValue));
@@ -180,6 +342,18 @@ std::shared_ptr<DeviceBuffer> RecvFuture::getShared() const {
     std::lock_guard<std::mutex> lk(st.mu);
     if (st.done) return st.out;
     Msg m = st.pipe->pop(st.ticket);
+    if (m.link) {
+        // from another process: the payload is copied out of the sender's
+        // staging slot into a buffer of this party
+        if (m.bytes != st.bytes)
+            throw std::runtime_error("channel: message size mismatch (expected " + std::to_string(st.bytes) +
+                                     ", got " + std::to_string(m.bytes) + ")");
+        GPU_CALL(aby3g_set_device(st.gpu->device()));
+        st.out = std::make_shared<DeviceBuffer>(*st.gpu, std::max<size_t>(m.bytes, 8));
+        st.pipe->linkCopyOut(m, st.out->data(), *st.gpu);
+        st.done = true;
+        return st.out;
+    }
     if (!m.shared) throw std::runtime_error("channel: expected a zero-copy device payload");
     if (m.bytes != st.bytes)
         throw std::runtime_error("channel: message size mismatch (expected " + std::to_string(st.bytes) + ", got " +
@@ -198,6 +372,11 @@ void Channel::asyncSendShared(std::shared_ptr<DeviceBuffer> buf, size_t bytes, G
     if (!mOut) throw std::runtime_error("channel not connected");
     if (!buf || buf->bytes() < bytes) throw std::runtime_error("asyncSendShared: buffer smaller than the message");
     GPU_CALL(aby3g_set_device(gpu.device()));
+    if (mOut->link) {
+        // another process cannot read this buffer in place: stage a copy
+        mOut->linkSendDevice(buf->data(), bytes, gpu);
+        return;
+    }
     Msg m;
     m.device = true;
     m.bytes = bytes;
@@ -239,6 +418,10 @@ RecvFuture Channel::asyncRecv(void* dst, size_t bytes) {
 void Channel::asyncSendDevice(const void* src, size_t bytes, Gpu& gpu) {
     if (!mOut) throw std::runtime_error("channel not connected");
     GPU_CALL(aby3g_set_device(gpu.device()));
+    if (mOut->link) {
+        mOut->linkSendDevice(src, bytes, gpu);
+        return;
+    }
     Slot* s = mOut->acquire(bytes, gpu.device());
     if (s->consumedRecorded) GPU_CALL(aby3g_stream_wait_event(gpu.stream(), s->consumed->get()));
     if (bytes) GPU_CALL(aby3g_memcpy(s->ptr, src, bytes, 2, gpu.stream()));  // staging slot on the sender's device
@@ -281,6 +464,12 @@ static bool signalWordsAllowed() {
 }
 
 std::vector<CommPkg> makeLocalRing(const int* devices) {
+    // parties on different devices read each other's buffers in place
+    // (zero-copy messages): that needs peer access both ways
+    if (devices)
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                if (devices[i] != devices[j]) GPU_CALL(aby3g_enable_peer_access(devices[i], devices[j]));
     if (!signalWordsAllowed()) devices = nullptr;
     // pipe[i][j]: messages from party i to party j
     std::shared_ptr<Pipe> p[3][3];
@@ -296,6 +485,30 @@ std::vector<CommPkg> makeLocalRing(const int* devices) {
         c[i].mNext = Channel(p[i][nx], p[nx][i]);
         c[i].mPrev = Channel(p[i][pv], p[pv][i]);
     }
+    return c;
+}
+
+CommPkg makeProcessRing(int party, const std::string& link, int device) {
+    if (party < 0 || party > 2) throw std::runtime_error("makeProcessRing: party must be 0, 1 or 2");
+    if (link.empty() || link.find('/') != std::string::npos)
+        throw std::runtime_error("makeProcessRing: link name must be non-empty without '/'");
+    auto seg = [&](int from, int to) { return "/aby3." + link + "." + std::to_string(from) + std::to_string(to); };
+    auto end = [&](int from, int to) {
+        auto p = std::make_shared<Pipe>();
+        p->link = std::make_unique<LinkEnd>(seg(from, to), from == party, device);
+        p->linkDevice = device;
+        return p;
+    };
+    const int nx = (party + 1) % 3, pv = (party + 2) % 3;
+    // attach order is the same in every process (lower party pair first),
+    // so the handshakes never wait on each other in a cycle
+    std::shared_ptr<Pipe> pipes[3][3];
+    for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b)
+            if (a != b && (a == party || b == party)) pipes[a][b] = end(a, b);
+    CommPkg c;
+    c.mNext = Channel(pipes[party][nx], pipes[nx][party]);
+    c.mPrev = Channel(pipes[party][pv], pipes[pv][party]);
     return c;
 }
 

@@ -19,6 +19,7 @@
 #include <deque>
 #include <memory>
 #include <mutex>
+#include <string>
 #include <vector>
 
 namespace aby3 {
@@ -92,5 +93,13 @@ double recvWaitUs();
 // devices[i]), device payloads between parties on one device are signalled
 // through stream-ordered words instead of events.
 std::vector<CommPkg> makeLocalRing(const int* devices = nullptr);
+
+// One party per process (the reference's deployment): the CommPkg of `party`
+// in this process, its four directions carried by shared-memory links named
+// after `link` (the same string in the three processes, unique per session;
+// Link.h). Blocks until the two other parties have attached. Device payloads
+// are staged in IPC-exported slots and copied out by the receiver; a
+// zero-copy send (asyncSendShared) becomes such a staged copy.
+CommPkg makeProcessRing(int party, const std::string& link, int device);
 
 }  // namespace aby3

@@ -399,6 +399,7 @@ struct SortJob : Job {
 struct Session {
     std::unique_ptr<Job> job;
     std::thread th[3];
+    std::vector<int> locals;  // the parties run by this process (all three, or one)
     std::mutex mu;
     std::condition_variable cv, done;
     // command: 0 idle, 1 run, 2 stop, 3 probe read, 4 probe reset, 5 check
@@ -531,9 +532,27 @@ struct Session {
         finished = 0;
         ++gen;
         cv.notify_all();
-        done.wait(lk, [&] { return finished == 3; });
+        done.wait(lk, [&] { return finished == (int)locals.size(); });
     }
 };
+
+std::unique_ptr<Job> makeJob(int job, const uint64_t* params, int nparams) {
+    auto P = [&](int i, u64 def) { return i < nparams ? params[i] : def; };
+    switch (job) {
+        case ABY3H_JOB_MUL_TRUNC:
+            return std::make_unique<MulJob>(P(0, 1024), P(1, 1024), P(2, 1024), P(3, 16),
+                                            P(4, 1) ? MulMode::Gemm : MulMode::Hadamard, true);
+        case ABY3H_JOB_MUL:
+            return std::make_unique<MulJob>(P(0, 128), P(1, 128), P(2, 128), 0, P(3, 0) ? MulMode::Gemm : MulMode::Hadamard,
+                                            false);
+        case ABY3H_JOB_MSB: return std::make_unique<MsbJob>(P(0, 1 << 20));
+        case ABY3H_JOB_LR: return std::make_unique<LrJob>(P(0, 1000000), P(1, 128), P(2, 256), P(3, 16), P(4, 11));
+        case ABY3H_JOB_SORT: return std::make_unique<SortJob>(P(0, 1 << 20));
+        case ABY3H_JOB_A2B: return std::make_unique<A2bJob>(P(0, 1 << 20));
+        case ABY3H_JOB_BITINJ: return std::make_unique<BitInjJob>(P(0, 1 << 16), P(1, 64));
+        default: throw std::runtime_error("unknown job");
+    }
+}
 
 }  // namespace aby3
 
@@ -549,27 +568,10 @@ const char* aby3h_last_error(void) { return t_err.c_str(); }
 
 aby3h_session* aby3h_session_create(int job, const uint64_t* params, int nparams, const int* devices, int probe) {
     try {
-        auto P = [&](int i, u64 def) { return i < nparams ? params[i] : def; };
         auto* h = new aby3h_session;
         Session& s = h->s;
-        switch (job) {
-            case ABY3H_JOB_MUL_TRUNC:
-                s.job = std::make_unique<MulJob>(P(0, 1024), P(1, 1024), P(2, 1024), P(3, 16),
-                                                 P(4, 1) ? MulMode::Gemm : MulMode::Hadamard, true);
-                break;
-            case ABY3H_JOB_MUL:
-                s.job = std::make_unique<MulJob>(P(0, 128), P(1, 128), P(2, 128), 0,
-                                                 P(3, 0) ? MulMode::Gemm : MulMode::Hadamard, false);
-                break;
-            case ABY3H_JOB_MSB: s.job = std::make_unique<MsbJob>(P(0, 1 << 20)); break;
-            case ABY3H_JOB_LR:
-                s.job = std::make_unique<LrJob>(P(0, 1000000), P(1, 128), P(2, 256), P(3, 16), P(4, 11));
-                break;
-            case ABY3H_JOB_SORT: s.job = std::make_unique<SortJob>(P(0, 1 << 20)); break;
-            case ABY3H_JOB_A2B: s.job = std::make_unique<A2bJob>(P(0, 1 << 20)); break;
-            case ABY3H_JOB_BITINJ: s.job = std::make_unique<BitInjJob>(P(0, 1 << 16), P(1, 64)); break;
-            default: throw std::runtime_error("unknown job");
-        }
+        s.job = makeJob(job, params, nparams);
+        s.locals = {0, 1, 2};
         {
             int dv[3] = {0, 0, 0};
             if (devices)
@@ -587,6 +589,40 @@ aby3h_session* aby3h_session_create(int job, const uint64_t* params, int nparams
         {
             std::unique_lock<std::mutex> lk(s.mu);
             s.done.wait(lk, [&] { return s.finished == 3; });
+        }
+        if (!s.err.empty()) {
+            std::string e = s.err;
+            aby3h_session_destroy(h);
+            throw std::runtime_error(e);
+        }
+        return h;
+    } catch (const std::exception& e) {
+        t_err = e.what();
+        return nullptr;
+    }
+}
+
+aby3h_session* aby3h_party_create(int job, const uint64_t* params, int nparams, int party, int device,
+                                  const char* link, int colocated, int probe) {
+    try {
+        if (party < 0 || party > 2) throw std::runtime_error("party must be 0, 1 or 2");
+        if (!link) throw std::runtime_error("null link name");
+        auto* h = new aby3h_session;
+        Session& s = h->s;
+        s.job = makeJob(job, params, nparams);
+        s.locals = {party};
+        s.comms.resize(3);
+        s.comms[(size_t)party] = makeProcessRing(party, link, device);
+        s.colocated = colocated != 0;
+        s.turnNext = party;  // stream-creation turns: only this party's here
+        {
+            std::unique_lock<std::mutex> lk(s.mu);
+            s.finished = 0;
+        }
+        s.th[party] = std::thread([&s, party, device, probe] { s.worker(party, device, probe); });
+        {
+            std::unique_lock<std::mutex> lk(s.mu);
+            s.done.wait(lk, [&] { return s.finished == 1; });
         }
         if (!s.err.empty()) {
             std::string e = s.err;
@@ -632,11 +668,12 @@ int aby3h_session_probe_reset(aby3h_session* h) {
 int aby3h_session_info(aby3h_session* h, double* out, int n) {
     double tmp[ABY3H_INFO_COUNT] = {0};
     h->s.job->info(tmp);
+    const int q = h->s.locals[0];  // party 0, or this process's party
     tmp[ABY3H_INFO_HOST_ENQUEUE_US] = *std::max_element(h->s.hostEnqueueUs, h->s.hostEnqueueUs + 3);
-    tmp[ABY3H_INFO_HOST_DRAIN_US] = h->s.hostDrainUs[0];
-    tmp[ABY3H_INFO_HOST_RECV_WAIT_US] = h->s.hostRecvWaitUs[0];
-    tmp[ABY3H_INFO_HOST_API_US] = h->s.hostApiUs[0];
-    tmp[ABY3H_INFO_HOST_API_CALLS] = h->s.hostApiCalls[0];
+    tmp[ABY3H_INFO_HOST_DRAIN_US] = h->s.hostDrainUs[q];
+    tmp[ABY3H_INFO_HOST_RECV_WAIT_US] = h->s.hostRecvWaitUs[q];
+    tmp[ABY3H_INFO_HOST_API_US] = h->s.hostApiUs[q];
+    tmp[ABY3H_INFO_HOST_API_CALLS] = h->s.hostApiCalls[q];
     for (int i = 0; i < n && i < ABY3H_INFO_COUNT; ++i) out[i] = tmp[i];
     return 0;
 }

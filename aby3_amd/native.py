@@ -93,6 +93,12 @@ _SIGS = {
     "aby3g_signal_alloc": (c_int, [POINTER(c_void_p)]),
     "aby3g_stream_write_value": (c_int, [c_void_p, c_void_p, c_uint64]),
     "aby3g_stream_wait_value": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "aby3g_ipc_get_handle": (c_int, [c_void_p, c_void_p]),
+    "aby3g_ipc_open": (c_int, [c_void_p, POINTER(c_void_p)]),
+    "aby3g_ipc_close": (c_int, [c_void_p]),
+    "aby3g_host_register": (c_int, [c_void_p, c_size_t, POINTER(c_void_p)]),
+    "aby3g_host_unregister": (c_int, [c_void_p]),
+    "aby3g_enable_peer_access": (c_int, [c_int, c_int]),
     "aby3g_probe_enable": (c_int, [c_int]),
     "aby3g_probe_enable_mask": (c_int, [ctypes.c_uint32]),
     "aby3g_probe_read": (c_int, [c_int, POINTER(c_double), POINTER(c_uint64)]),
@@ -196,6 +202,7 @@ INFO = dict(mults_per_step=0, gemm_int8_ops=1, and_words=2, gate_words=3, gate_b
 _HOST_SIGS = {
     "aby3h_last_error": (c_char_p, []),
     "aby3h_session_create": (c_void_p, [c_int, POINTER(c_uint64), c_int, POINTER(c_int), c_int]),
+    "aby3h_party_create": (c_void_p, [c_int, POINTER(c_uint64), c_int, c_int, c_int, c_char_p, c_int, c_int]),
     "aby3h_session_run": (c_int, [c_void_p, c_uint64]),
     "aby3h_session_probe": (c_int, [c_void_p, c_int, POINTER(c_double), POINTER(c_uint64)]),
     "aby3h_session_probe_reset": (c_int, [c_void_p]),
@@ -251,6 +258,21 @@ class Session:
         if not self._h:
             raise NativeError("aby3h_session_create: " + h.aby3h_last_error().decode())
         self.host = h
+
+    @classmethod
+    def party(cls, job: int, params, party: int, link: str, device: int = 0, colocated: bool = True,
+              probe=False):
+        """One party of a session in this process (aby3h_party_create): the
+        three processes pass the same job, params and link name."""
+        self = cls.__new__(cls)
+        h = host()
+        p = (c_uint64 * len(params))(*params)
+        mask = 0xFF if probe is True else int(probe)
+        self._h = h.aby3h_party_create(job, p, len(params), party, device, link.encode(), int(colocated), mask)
+        if not self._h:
+            raise NativeError("aby3h_party_create: " + h.aby3h_last_error().decode())
+        self.host = h
+        return self
 
     def run(self, steps: int):
         if self.host.aby3h_session_run(self._h, steps) != 0:

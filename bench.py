@@ -114,6 +114,11 @@ def load_pmc(kind: str, cfg: dict, field: str = "hbm_bytes_per_launch"):
     return best
 
 
+def local_fraction(info, step_s):
+    """1 - (party 0's host wait for peer messages) / wall clock, per step."""
+    return max(0.0, 1.0 - info["host_recv_wait_us"] * 1e-6 / step_s) if step_s > 0 else None
+
+
 def timed(sess, steps, pg):
     barrier(pg)
     t0 = time.perf_counter()
@@ -121,6 +126,42 @@ def timed(sess, steps, pg):
     t1 = time.perf_counter()
     barrier(pg)
     return allmax(pg, t1 - t0)
+
+
+def cpu_mul_s(mode, reps):
+    """Seconds per C1 multiplication of the oracle (cpu_baseline leg only)."""
+    import ctypes
+
+    orc = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "liborc.so"))
+    orc.orc_bench_mul.restype = ctypes.c_double
+    secs = orc.orc_bench_mul(mode, 128, 128, 128, reps)
+    if secs < 0:
+        raise SystemExit("bench: oracle C1 baseline failed")
+    return secs / reps
+
+
+def party_processes(args, steps=30):
+    """C2 in the north_star's process layout: three processes, one party
+    each (aby3h_party_create), on this node's GPU 0 (the driver's boxes have
+    one GPU, so the three share it), messages over the shared-memory links
+    and IPC staging slots. Returns the slowest party's ms per step."""
+    import subprocess
+
+    link = f"bench{os.getpid()}"
+    params = f"{args.m},{args.k},{args.n},{args.decimal},1"
+    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "party_worker.py"), str(0), str(p),
+                               str(steps), link, "0", params], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                              text=True, env=dict(os.environ, ABY3_LINK_TIMEOUT_S="120"))
+             for p in range(3)]
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=300)
+        if p.returncode != 0:
+            raise SystemExit("bench: party process failed: " + e[-2000:])
+        outs.append(json.loads(o.strip().splitlines()[-1]))
+    if not all(o["ok"] for o in outs):
+        raise SystemExit("bench: party-process product differs from the plaintext")
+    return max(o["ms_per_step"] for o in outs), outs
 
 
 def cpu_msb(nt, rows, reps):
@@ -228,12 +269,14 @@ def extras(args, nt, dev, world, pg):
     with nt.Session(nt.JOB_LR, [args.lr_rows, 128, 256, 16, 11], devices=(dev,) * 3, probe=False) as s:
         s.run(5)
         dt = timed(s, 50, pg)
+        linfo = s.info()
         if not s.check():
             raise SystemExit("bench: LR model differs from the plaintext fixed-point restatement")
         res["lr_iteration"] = {
             "workload": f"SGD_Logistic iteration, {args.lr_rows}x128, batch 256, D16, lr 2^-11 (sigmoid piecewise)",
             "ms_per_iteration": dt / 50 * 1e3,
             "iterations_per_s": world * 50 / dt,
+            "local_compute_fraction": local_fraction(linfo, dt / 50),
         }
         if world == 1 and not args.no_cpu_baseline:
             progress("C4 CPU baseline")
@@ -268,6 +311,26 @@ def extras(args, nt, dev, world, pg):
                 "est_full_sort_s": info["and_words"] / rate,
             }
             res["merge_sort"]["speedup_vs_cpu_baseline"] = res["merge_sort"]["and_word_gates_per_s"] / rate
+    # C1: asyncMul 128x128, both modes, no truncation
+    res["c1_mul"] = {}
+    for mode, name in ((0, "hadamard"), (1, "gemm")):
+        with nt.Session(nt.JOB_MUL, [128, 128, 128, mode], devices=(dev,) * 3, probe=False) as s:
+            s.run(20)
+            if not s.check():
+                raise SystemExit("bench: C1 product differs from the plaintext")
+            reps = 500
+            dt = timed(s, reps, pg)
+            mults = 128 * 128 * (128 if mode else 1)
+            e = {"workload": f"asyncMul 128x128 si64 ({name}{', 128x128x128' if mode else ''}), 3 parties",
+                 "ms_per_mul": dt / reps * 1e3, "mults_per_s": world * reps * mults / dt}
+            if world == 1 and not args.no_cpu_baseline:
+                cpu_s = cpu_mul_s(mode, 2000 if mode == 0 else 300)
+                e["cpu_baseline"] = {
+                    "value": mults / cpu_s, "unit": "mults/s", "cores": 3, "kind": "port",
+                    "sample": f"{2000 if mode == 0 else 300} x asyncMul 128x128 ({name}): the oracle's local share "
+                              "product + zero-share per party (3 party threads), ring reshare as a copy"}
+                e["speedup_vs_cpu_baseline"] = e["mults_per_s"] / e["cpu_baseline"]["value"]
+            res["c1_mul"][name] = e
     # share conversions, each checked on its revealed output
     with nt.Session(nt.JOB_A2B, [1 << 20], devices=(dev,) * 3, probe=False) as s:
         s.run(2)
@@ -389,7 +452,7 @@ def main():
             "kernel": "k_share_gemm16s (int8 MFMA 16x16x64, 36 digit pairs as 20 two-pair MFMAs per block and stage)",
             "achieved": achieved_tops,
             "peak": PEAK_INT8_TOPS,
-            "unit": "TFLOP/s",
+            "unit": "TOP/s",
             "frac": achieved_tops / PEAK_INT8_TOPS,
             "traffic": traffic,
             "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_*.json)",
@@ -400,6 +463,10 @@ def main():
             "ops_per_launch": info["gemm_int8_ops"],
         },
         "kernel_ms_per_step": breakdown,
+        # host time party 0 spends blocked on its peers' messages, as a share
+        # of the step (the parties' threads enqueue asynchronously; the GPU
+        # streams wait on each other without a host round trip)
+        "local_compute_fraction": local_fraction(info, dt / args.steps),
     }
 
     if not args.no_binary:
@@ -427,6 +494,7 @@ def main():
             "unit": "AND word-gates/s (1 AND-type gate on one 64-row word)",
             "ms_per_step": bdt / args.binary_steps * 1e3,
             "and_words_per_step": binfo["and_words"],
+            "local_compute_fraction": local_fraction(binfo, bdt / args.binary_steps),
             "roofline": {
                 "bound": "hbm",
                 "kernel": "k_bin_level (one launch per level: unpack of the received AND shares + the level's gate batches)",
@@ -456,6 +524,16 @@ def main():
     if not args.no_extras:
         progress("C4 / C5 extras")
         out["extras"] = extras(args, nt, dev, world, pg)
+        if world == 1:
+            progress("C2 as three party processes")
+            ms, outs = party_processes(args)
+            out["extras"]["party_processes"] = {
+                "workload": f"the C2 multiplication with each party in its own process (aby3h_party_create), "
+                            "all three on GPU 0, messages over shared-memory links + IPC device staging slots",
+                "ms_per_step": ms,
+                "mults_per_s": M * N * K / (ms * 1e-3),
+                "recv_wait_us_per_step": [o["recv_wait_us"] for o in sorted(outs, key=lambda o: o["party"])],
+            }
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         import ctypes

@@ -70,6 +70,20 @@ const char* aby3h_last_error(void);
 /* probe: 0 off, else a bitmask of aby3gpu.h probe families (1 << family) whose
  * launches are bracketed by timing events */
 aby3h_session* aby3h_session_create(int job, const uint64_t* params, int nparams, const int* devices, int probe);
+/* One party of a session in this process: the reference's deployment of
+ * three processes, one per party (Eval/dis_exec.sh:10-12), here one GPU per
+ * party. The three processes call this with the same job,
+ * params and `link` (a session name unique on the machine, no '/'), each with
+ * its own party 0..2 and device; the call returns once the session is set up
+ * in all three. The parties' messages travel over shared-memory links (host
+ * control words) and IPC-exported device staging slots (payloads; peer reads
+ * over xGMI between GPUs). colocated != 0: other parties share this party's
+ * GPU (one stream per party). Every aby3h_session_* call below must then be
+ * made by all three processes in the same order; info and probe report this
+ * process's party, check reports party 0's verdict in party 0's process (the
+ * others return 0 when their part succeeded). */
+aby3h_session* aby3h_party_create(int job, const uint64_t* params, int nparams, int party, int device,
+                                  const char* link, int colocated, int probe);
 int aby3h_session_run(aby3h_session* s, uint64_t steps);
 /* kernel time (ms) and launches of a probe family (aby3gpu.h), summed over parties */
 int aby3h_session_probe(aby3h_session* s, int family, double* ms, uint64_t* launches);

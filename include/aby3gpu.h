@@ -81,6 +81,27 @@ int aby3g_signal_alloc(uint64_t** word); /* zeroed, on the current device */
 int aby3g_stream_write_value(aby3g_stream stream, uint64_t* word, uint64_t value);
 int aby3g_stream_wait_value(aby3g_stream stream, uint64_t* word, uint64_t value);
 
+/* Cross-process transport: one party per process (the
+ * reference's parties are processes joined by cryptoTools Channels over TCP,
+ * Sh3Types.h:32-34, Eval/dis_exec.sh:10-12). A channel's staging slots are
+ * device buffers exported through IPC handles (hipIpcGetMemHandle); its
+ * stream-ordered signal words live in host memory shared by the processes
+ * (POSIX shm) and registered with each party's device; parties on different
+ * devices of one process reach each other's buffers through peer access. */
+typedef struct {
+    unsigned char bytes[64];
+} aby3g_ipc_handle;
+int aby3g_ipc_get_handle(void* ptr, aby3g_ipc_handle* handle); /* ptr: a base pointer from aby3g_malloc */
+int aby3g_ipc_open(const aby3g_ipc_handle* handle, void** ptr); /* mapped for the current device */
+int aby3g_ipc_close(void* ptr);
+/* page-aligned host memory -> an address the current device's streams can
+ * write / wait on (aby3g_stream_write_value / aby3g_stream_wait_value) */
+int aby3g_host_register(void* host, size_t bytes, void** dev);
+int aby3g_host_unregister(void* host);
+/* lets `device` read and write `peer`'s memory (0 also when already enabled;
+ * an error when the two devices cannot reach each other) */
+int aby3g_enable_peer_access(int device, int peer);
+
 /* Kernel timing probe: when enabled, every kernel launched by this library on
  * the calling thread is bracketed by events; aby3g_probe_read() returns the
  * accumulated device time (ms) and launch count per kernel family:

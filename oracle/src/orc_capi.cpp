@@ -394,6 +394,52 @@ double orc_bench_mul_trunc(int mode, uint64_t M, uint64_t K, uint64_t N, uint64_
 }
 
 
+// CPU baseline of C1: asyncMul without truncation
+// (Sh3Evaluator.cpp:92-116), one thread per party: each party's local share
+// product as Eigen evaluates it (three i64 products, or the fork's
+// element-wise loop) plus its zero-share, then the ring reshare (a copy of
+// C0 to the next party). Seconds for `reps` multiplications.
+double orc_bench_mul(int mode, uint64_t M, uint64_t K, uint64_t N, int reps) {
+    try {
+        auto ev = makeEvaluators(1);
+        std::array<SMat, 3> A, B;
+        u64 x = 43;
+        auto rnd = [&](SMat& m, u64 r, u64 c) {
+            m = SMat(r, c);
+            for (int s = 0; s < 2; ++s)
+                for (auto& v : m.s[s].v) {
+                    x ^= x << 13;
+                    x ^= x >> 7;
+                    x ^= x << 17;
+                    v = (i64)x;
+                }
+        };
+        for (int p = 0; p < 3; ++p) {
+            rnd(A[p], M, K);
+            rnd(B[p], mode == MUL_GEMM ? K : M, mode == MUL_GEMM ? N : K);
+        }
+        auto t0 = std::chrono::steady_clock::now();
+        for (int r = 0; r < reps; ++r) {
+            std::array<SMat, 3> C;
+            std::vector<std::thread> th;
+            for (int p = 0; p < 3; ++p)
+                th.emplace_back([&, p] {
+                    Mat c0;
+                    localProduct((MulMode)mode, A[p], B[p], c0);
+                    for (u64 k = 0; k < c0.size(); ++k) c0.v[k] = (i64)((u64)c0.v[k] + (u64)ev[p].gen.getShare());
+                    C[p].s[0] = std::move(c0);
+                });
+            for (auto& t : th) t.join();
+            for (int p = 0; p < 3; ++p) C[(p + 1) % 3].s[1] = C[p].s[0];
+        }
+        auto t1 = std::chrono::steady_clock::now();
+        return std::chrono::duration<double>(t1 - t0).count();
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
 // CPU baseline of cipher_gt / fetch_msb (bench.py binary cpu_baseline for C3,
 // BuildingBlocks.cpp:464-532): diff = B - A, the two-input binary resharing,
 // and the 64-bit MSB circuit evaluated by the three parties (bit-sliced u64

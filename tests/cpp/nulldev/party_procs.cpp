@@ -1,0 +1,66 @@
+// One party per process on the null device: the driver forks three
+// processes, each runs aby3h_party_create for its party (shared-memory links,
+// "IPC" slots in a shared arena) and steps / checks / destroys every job.
+// Built with -fsanitize=address by tests/test_host_asan.py. Compute results
+// are meaningless here; the test covers the cross-process transport's
+// message order, sizes, slot reuse and teardown.
+#include <aby3.h>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <sys/wait.h>
+#include <unistd.h>
+#include <vector>
+
+extern "C" int nulldev_shared_arena(size_t bytes);
+
+static int party_main(int party, const std::string& tag) {
+    struct J {
+        int job;
+        std::vector<uint64_t> p;
+        int steps;
+    } jobs[] = {
+        {ABY3H_JOB_MUL_TRUNC, {64, 48, 80, 16, 1}, 3}, {ABY3H_JOB_MUL_TRUNC, {64, 64, 64, 8, 0}, 3},
+        {ABY3H_JOB_MUL, {32, 16, 8, 1}, 3},            {ABY3H_JOB_MSB, {3000}, 2},
+        {ABY3H_JOB_LR, {2048, 16, 64, 16, 11}, 3},     {ABY3H_JOB_SORT, {512}, 1},
+        {ABY3H_JOB_A2B, {1000}, 2},                    {ABY3H_JOB_BITINJ, {300, 20}, 2},
+    };
+    int k = 0;
+    for (auto& j : jobs) {
+        const std::string link = tag + "." + std::to_string(k++);
+        aby3h_session* s = aby3h_party_create(j.job, j.p.data(), (int)j.p.size(), party, 0, link.c_str(), 1, 0);
+        if (!s) {
+            std::printf("FAIL party %d create job %d: %s\n", party, j.job, aby3h_last_error());
+            return 1;
+        }
+        if (aby3h_session_run(s, j.steps) || aby3h_session_check(s) == 2) {
+            std::printf("FAIL party %d job %d: %s\n", party, j.job, aby3h_last_error());
+            return 1;
+        }
+        double info[ABY3H_INFO_COUNT];
+        aby3h_session_info(s, info, ABY3H_INFO_COUNT);
+        aby3h_session_destroy(s);
+    }
+    return 0;
+}
+
+int main() {
+    if (nulldev_shared_arena((size_t)1 << 30)) return 2;
+    const std::string tag = "t" + std::to_string(getpid());
+    pid_t kids[3];
+    for (int p = 0; p < 3; ++p) {
+        kids[p] = fork();
+        if (kids[p] == 0) _exit(party_main(p, tag));
+    }
+    int bad = 0;
+    for (int p = 0; p < 3; ++p) {
+        int st = 0;
+        waitpid(kids[p], &st, 0);
+        if (!WIFEXITED(st) || WEXITSTATUS(st) != 0) {
+            std::printf("party %d exited with status %d\n", p, st);
+            bad = 1;
+        }
+    }
+    if (!bad) std::printf("party_procs: ok\n");
+    return bad;
+}

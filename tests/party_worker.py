@@ -1,0 +1,32 @@
+"""One party of a three-process session (aby3h_party_create), started by
+tests/test_gpu_parties.py and bench.py's party deployment checks: runs
+`steps` steps of a job, checks the revealed result, prints one JSON line."""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from aby3_amd import native  # noqa: E402
+
+
+def main():
+    job, party, steps = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
+    link, device = sys.argv[4], int(sys.argv[5])
+    params = [int(x) for x in sys.argv[6].split(",")] if len(sys.argv) > 6 and sys.argv[6] else []
+    s = native.Session.party(job, params, party, link, device=device, colocated=True)
+    try:
+        s.run(1)  # warm-up
+        t0 = time.perf_counter()
+        s.run(steps)
+        dt = time.perf_counter() - t0
+        ok = s.check()
+        info = s.info()
+    finally:
+        s.close()
+    print(json.dumps({"party": party, "ok": ok, "ms_per_step": 1e3 * dt / steps,
+                      "recv_wait_us": info["host_recv_wait_us"]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,57 @@
+"""The north_star deployment's transport: three processes, one ABY3 party
+each (aby3h_party_create), joined by shared-memory links and IPC-exported
+device staging slots (aby3_amd/host/Link.h, Channel.cpp). On the one-GPU box
+the three processes share cuda:0, so the payload copies run over IPC
+mappings of one device; between GPUs the same code path reads the peer's
+slot over xGMI. Each job's revealed result is checked by party 0 against
+plaintext exactly as the in-process sessions of test_gpu_protocols.py."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from aby3_amd import native as nt
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def run_parties(job, params, steps, tag, timeout=150):
+    link = f"gt{os.getpid()}.{tag}"
+    env = dict(os.environ, ABY3_LINK_TIMEOUT_S="100")
+    args = [str(job), None, str(steps), link, "0", ",".join(str(p) for p in params)]
+    procs = []
+    for party in range(3):
+        a = list(args)
+        a[1] = str(party)
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "party_worker.py"), *a],
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
+    outs = []
+    try:
+        for p in procs:
+            o, e = p.communicate(timeout=timeout)
+            assert p.returncode == 0, f"party exited {p.returncode}: {e[-3000:]}"
+            outs.append(json.loads(o.strip().splitlines()[-1]))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return outs
+
+
+@pytest.mark.parametrize("job,params,steps", [
+    (nt.JOB_MUL_TRUNC, [1024, 1024, 1024, 16, 1], 3),   # C2 shapes
+    (nt.JOB_MUL_TRUNC, [257, 200, 250, 8, 1], 2),       # ragged GEMM, D8
+    (nt.JOB_MUL, [128, 128, 128, 0], 3),                # C1 Hadamard
+    (nt.JOB_MSB, [1 << 16], 2),                         # C3 circuit levels
+    (nt.JOB_LR, [20000, 128, 256, 16, 11], 5),          # C4 (dataset trimmed)
+    (nt.JOB_SORT, [4096], 1),                           # C5 network, every key checked
+    (nt.JOB_A2B, [5000], 2),                            # toBinaryMatrix
+    (nt.JOB_BITINJ, [777, 13], 2),                      # bitInjection (OT messages)
+])
+def test_three_party_processes(gpu, job, params, steps):
+    outs = run_parties(job, params, steps, f"{job}_{params[0]}")
+    assert sorted(o["party"] for o in outs) == [0, 1, 2]
+    assert all(o["ok"] for o in outs), outs

@@ -15,14 +15,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ND = os.path.join(ROOT, "tests", "cpp", "nulldev")
 
 
-def _build(tmp, sanitizer):
+def _build(tmp, sanitizer, driver="session_asan.cpp"):
     nulldev = os.path.join(tmp, "nulldev.cpp")
     subprocess.run([sys.executable, os.path.join(ND, "gen_nulldev.py"), nulldev], check=True)
-    exe = os.path.join(tmp, f"session_{sanitizer}")
+    exe = os.path.join(tmp, f"{driver[:-4]}_{sanitizer}")
     cmd = ["g++", "-std=c++17", "-O1", "-g", f"-fsanitize={sanitizer}", "-fno-omit-frame-pointer",
            "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "aby3_amd", "host"),
            *sorted(glob.glob(os.path.join(ROOT, "aby3_amd", "host", "*.cpp"))), nulldev,
-           os.path.join(ND, "session_asan.cpp"), "-o", exe, "-pthread"]
+           os.path.join(ND, driver), "-o", exe, "-pthread", "-lrt"]
     subprocess.run(cmd, check=True, timeout=600)
     return exe
 
@@ -35,3 +35,13 @@ def test_host_runtime_sanitized(tmp_path, sanitizer):
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
     assert "session_asan: ok" in r.stdout
     assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-4000:]
+
+
+def test_party_processes_sanitized(tmp_path):
+    """Three processes, one party each (aby3h_party_create): every job over
+    the shared-memory links and IPC staging slots, under AddressSanitizer."""
+    exe = _build(str(tmp_path), "address", "party_procs.cpp")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1", ABY3_LINK_TIMEOUT_S="60")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    assert "party_procs: ok" in r.stdout

@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--cpu-reps", type=int, default=10)
     ap.add_argument("--no-extras", action="store_true", help="skip the LR-iteration and merge-layer lines")
     ap.add_argument("--lr-rows", type=int, default=1000000)
+    ap.add_argument("--deployment", choices=("replicas", "parties"), default="replicas",
+                    help="replicas: every rank runs a whole 3-party job on its GPU; parties: every 3 ranks form "
+                         "one job, one party per rank and GPU (the north_star layout; world size a multiple of 3)")
     return ap.parse_args()
 
 
@@ -372,10 +375,66 @@ def extras(args, nt, dev, world, pg):
     return res
 
 
+def main_parties(args, world, rank, local, pg, nt):
+    """--deployment parties: ranks 3g, 3g+1, 3g+2 are parties 0, 1, 2 of job g,
+    each on its own GPU (local rank modulo the visible devices), messages
+    over shared-memory links and IPC device slots (peer reads over xGMI)."""
+    import ctypes
+
+    if world % 3:
+        raise SystemExit("bench: --deployment parties needs a world size that is a multiple of 3")
+    n = ctypes.c_int(0)
+    nt.lib().device_count(ctypes.byref(n))
+    dev = local % max(n.value, 1)
+    party, group = rank % 3, rank // 3
+    colocated = n.value < 3
+    M, K, N, D = args.m, args.k, args.n, args.decimal
+    link = f"bench{os.environ.get('MASTER_PORT', '0')}.{group}"
+    s = nt.Session.party(nt.JOB_MUL_TRUNC, [M, K, N, D, 1], party, link, device=dev, colocated=colocated)
+    s.run(2)
+    ok = s.check()
+    if allmax(pg, 0.0 if ok else 1.0) > 0:
+        raise SystemExit("bench: revealed product does not match the plaintext")
+    s.run(args.warmup)
+    dt = timed(s, args.steps, pg)
+    info = s.info()
+    s.close()
+    groups = world // 3
+    out = {
+        "metric": "secret-shared 64-bit mults/sec (matmul + binary-AND) per party, 3 parties on 3 MI355X",
+        "value": groups * args.steps * info["mults_per_step"] / dt,
+        "unit": "mults/s",
+        "n_gpus": world if not colocated else n.value,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic: fixed-point operands round(U[-8,8) * 2^16), shared by party 0",
+        "config": {
+            "workload": f"sf64Matrix asyncMul + truncation {M}x{K} . {K}x{N} (D{D}), upstream GEMM semantics, "
+                        "one party per process" + (" (processes sharing a GPU)" if colocated else " and GPU"),
+            "parties_per_gpu": 3 if colocated else 1,
+            "global_batch": groups,
+            "parallelism": f"parties3x{groups}",
+        },
+        "local_compute_fraction": local_fraction(info, dt / args.steps),
+    }
+    if rank == 0:
+        print(json.dumps(out))
+    if pg is not None:
+        pg.destroy_process_group()
+
+
 def main():
     args = parse()
     world, rank, local, pg = dist_setup()
     from aby3_amd import native as nt
+
+    if args.deployment == "parties":
+        return main_parties(args, world, rank, local, pg, nt)
 
     dev = local
     M, K, N, D = args.m, args.k, args.n, args.decimal

@@ -44,8 +44,12 @@ static int party_main(int party, const std::string& tag) {
     return 0;
 }
 
-int main() {
+int main(int argc, char** argv) {
     if (nulldev_shared_arena((size_t)1 << 30)) return 2;
+    // `party_procs <party> <tag>`: one party only, started by a launcher
+    // (tests/test_dist.py: three gloo ranks, one party each, sharing the
+    // named arena ND_ARENA)
+    if (argc == 3) return party_main(atoi(argv[1]), argv[2]);
     const std::string tag = "t" + std::to_string(getpid());
     pid_t kids[3];
     for (int p = 0; p < 3; ++p) {

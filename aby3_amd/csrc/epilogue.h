@@ -154,12 +154,13 @@ __global__ void __launch_bounds__(kEpiBlock, 4) k_finish_zero_share(const u32* _
 // threads never exchange words and the grid-stride loop balances to a block.
 // Even waves run the next stream (R, RT0, z), odd waves the prev stream
 // (RT1): the key is wave-uniform, one schedule in SGPRs.
+// The body of k_finish_trunc for workgroup `bid` of `nblocks` (any
+// blockDim that is a multiple of 128; lds: kAesLdsWords words).
 template <class Src>
-__global__ void __launch_bounds__(kEpiBlock) k_finish_trunc(const u32* __restrict__ T0g, Src src, AesKeyPair kk,
-                                                            u64 nw0, u64 pw0, u64 n, u32 d, i64* __restrict__ R,
-                                                            i64* __restrict__ RT0, i64* __restrict__ RT1,
-                                                            i64* __restrict__ z) {
-    __shared__ u32 lds[kAesLdsWords];  // static: lookups fold the table base into ds_read's offset
+__device__ __forceinline__ void trunc_pair_block(u32* lds, const u32* __restrict__ T0g, Src src, const AesKeyPair& kk,
+                                                 u64 nw0, u64 pw0, u64 n, u32 d, i64* __restrict__ R,
+                                                 i64* __restrict__ RT0, i64* __restrict__ RT1, i64* __restrict__ z,
+                                                 u32 bid, u32 nblocks) {
     aes_fill_lds(lds, T0g);
     const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), h = wave & 1, lane = threadIdx.x & 63;
     u32 off = h * (u32)sizeof(AesKey);
@@ -167,10 +168,9 @@ __global__ void __launch_bounds__(kEpiBlock) k_finish_trunc(const u32* __restric
     const AesKey& k = *reinterpret_cast<const AesKey*>(reinterpret_cast<const char*>(&kk) + off);
     const u64 w0 = h ? pw0 : nw0;
     const u64 c_first = w0 >> 1, c_last = (w0 + n - 1) >> 1;
-    const u64 per = (u64)gridDim.x * (blockDim.x >> 1);  // threads per stream
+    const u64 per = (u64)nblocks * (blockDim.x >> 1);  // threads per stream
     // two counters per step (c, c + per), as k_aes_ctr
-    for (u64 c = c_first + ((u64)blockIdx.x * (blockDim.x >> 7) + (wave >> 1)) * 64 + lane; c <= c_last;
-         c += 2 * per) {
+    for (u64 c = c_first + ((u64)bid * (blockDim.x >> 7) + (wave >> 1)) * 64 + lane; c <= c_last; c += 2 * per) {
         u64 w[4];
         {
             // interleaved: the two blocks' table reads overlap (latency-bound at small n)
@@ -196,6 +196,22 @@ __global__ void __launch_bounds__(kEpiBlock) k_finish_trunc(const u32* __restric
             }
         }
     }
+}
+
+// R = t0 >> 2, RT = (t0 >> (d+2), t1 >> (d+2)); z = src(i) - R when z != null.
+// t0 = word (nw0 + i) of the next stream, t1 = word (pw0 + i) of the prev
+// stream. No windows: a thread encrypts one counter c of ONE stream and emits
+// the elements of its two words 2c, 2c+1 (whatever the stream's parity), so
+// threads never exchange words and the grid-stride loop balances to a block.
+// Even waves run the next stream (R, RT0, z), odd waves the prev stream
+// (RT1): the key is wave-uniform, one schedule in SGPRs.
+template <class Src>
+__global__ void __launch_bounds__(kEpiBlock) k_finish_trunc(const u32* __restrict__ T0g, Src src, AesKeyPair kk,
+                                                            u64 nw0, u64 pw0, u64 n, u32 d, i64* __restrict__ R,
+                                                            i64* __restrict__ RT0, i64* __restrict__ RT1,
+                                                            i64* __restrict__ z) {
+    __shared__ u32 lds[kAesLdsWords];  // static: lookups fold the table base into ds_read's offset
+    trunc_pair_block(lds, T0g, src, kk, nw0, pw0, n, d, R, RT0, RT1, z, blockIdx.x, gridDim.x);
 }
 
 template <class Src>

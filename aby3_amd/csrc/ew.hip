@@ -59,6 +59,22 @@ __global__ void k_gather_rows(const i64* __restrict__ src, u64 rows, u64 cols, c
     }
 }
 
+// out[i][w] = a[g][w] ^ b[g][w] ^ c[g][w] ^ mask[w], g = idx ? idx[i] : i
+// (every operand optional)
+__global__ void k_xor_gather_units(u64 units, u64 unit, const u32* __restrict__ idx, const u64* __restrict__ a,
+                                   const u64* __restrict__ b, const u64* __restrict__ c, const u64* __restrict__ mask,
+                                   u64* __restrict__ out) {
+    GRID_STRIDE(t, units * unit) {
+        const u64 i = t / unit, w = t % unit;
+        const u64 g = (idx ? (u64)idx[i] : i) * unit + w;
+        u64 v = mask ? mask[w] : 0;
+        if (a) v ^= a[g];
+        if (b) v ^= b[g];
+        if (c) v ^= c[g];
+        out[t] = v;
+    }
+}
+
 // 64 x 64 tile transpose through LDS (padded rows: conflict-free)
 __global__ void __launch_bounds__(256) k_transpose(const i64* __restrict__ src, u64 rows, u64 cols,
                                                    i64* __restrict__ dst) {
@@ -128,6 +144,18 @@ int aby3g_i64_gather_rows(const int64_t* src, uint64_t rows, uint64_t cols, cons
         if (!n || !cols) return;
         launch(PROBE_OTHER, k_gather_rows, dim3(ew_grid(2 * n * cols)), dim3(kB), 0, S(stream), src, rows, cols, idx,
                n, dst);
+    });
+}
+
+int aby3g_u64_xor_gather_units(uint64_t units, uint64_t unit, const uint32_t* idx, const uint64_t* a,
+                               const uint64_t* b, const uint64_t* c, const uint64_t* mask, uint64_t* out,
+                               aby3g_stream stream) {
+    return guarded([&] {
+        ABY3G_REQUIRE(out != nullptr, "null output");
+        ABY3G_REQUIRE(!idx || (out != a && out != b && out != c), "a gathering step cannot run in place");
+        if (!units || !unit) return;
+        launch(PROBE_OTHER, k_xor_gather_units, dim3(ew_grid(units * unit)), dim3(kB), 0, S(stream), units, unit, idx,
+               a, b, c, mask, out);
     });
 }
 

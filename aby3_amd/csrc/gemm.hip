@@ -47,7 +47,16 @@ inline char gemm_variant() {
     return v;
 }
 constexpr u32 TBM = 128;  // output tile height (8 waves of 32 x 32)
-inline u32 gemm_target_wgs() { return 256u; }
+// Share GEMMs of this many parties run side by side on the calling thread's
+// device (aby3g_set_gemm_sharing): split-K fills 1/k of the CUs per GEMM.
+thread_local u32 t_gemm_sharing = 1;
+inline u32 gemm_target_wgs() {
+    static const int env = [] {
+        const char* e = getenv("ABY3G_GEMM_WGS");  // override, for A/B runs
+        return e ? atoi(e) : 0;
+    }();
+    return env > 0 ? (u32)env : 256u / t_gemm_sharing;
+}
 
 inline u64 roundup(u64 x, u64 m) { return (x + m - 1) / m * m; }
 
@@ -163,14 +172,16 @@ __device__ __forceinline__ void digit_words(const u64 (&v)[4], u32 (&w)[8]) {
     }
 }
 
-__global__ void __launch_bounds__(256) k_digits(const i64* __restrict__ A0, const i64* __restrict__ A1,
-                                                const i64* __restrict__ B0, const i64* __restrict__ B1, u64 M,
-                                                u64 K, u64 N, u64 S2, u64 aGroups, u64 stages, u8* __restrict__ Ad,
-                                                u8* __restrict__ Bd) {
-    __shared__ __attribute__((aligned(16))) u8 img[2 * kDigitCols * kDigitPitch];  // record images
-    const u32 t = threadIdx.x;
-    const bool isA = blockIdx.x < aGroups;
-    const u64 g = isA ? blockIdx.x : blockIdx.x - aGroups;
+// One digit group: an A-group (32 rows x 32 k of A0, A1) or a B-group (32 k x
+// 64 columns of B0, B1) -> its records. t in [0, 256); img: 2 * 64 record
+// images. Every thread of the workgroup reaches the one barrier inside, also
+// when `valid` is false.
+__device__ __forceinline__ void digit_group(bool valid, u64 gid, u32 t, u8* img, const i64* __restrict__ A0,
+                                            const i64* __restrict__ A1, const i64* __restrict__ B0,
+                                            const i64* __restrict__ B1, u64 M, u64 K, u64 N, u64 S2, u64 aGroups,
+                                            u64 stages, u8* __restrict__ Ad, u8* __restrict__ Bd) {
+    const bool isA = gid < aGroups;
+    const u64 g = isA ? gid : gid - aGroups;
     const u64 st = g % S2, k0 = st * 32;
     u32 nrec;
     u8* out;
@@ -184,7 +195,7 @@ __global__ void __launch_bounds__(256) k_digits(const i64* __restrict__ A0, cons
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const u64 k = k0 + 4 * kq + j;
-            const bool in = m < M && k < K;
+            const bool in = valid && m < M && k < K;
             v0[j] = in ? (u64)A0[m * K + k] : 0;
             v1[j] = in ? (u64)A1[m * K + k] : 0;
         }
@@ -212,7 +223,7 @@ __global__ void __launch_bounds__(256) k_digits(const i64* __restrict__ A0, cons
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const u64 k = k0 + 4 * kq + j;
-                const bool in = n < N && k < K;
+                const bool in = valid && n < N && k < K;
                 const u64 b0 = in ? (u64)B0[k * N + n] : 0, b1 = in ? (u64)B1[k * N + n] : 0;
                 vs[j] = b0 + b1;
                 vb[j] = b0;
@@ -232,14 +243,23 @@ __global__ void __launch_bounds__(256) k_digits(const i64* __restrict__ A0, cons
         out = Bd;
     }
     __syncthreads();
+    if (!valid) return;
     // 16 chunks of 16 B per record; record (r, half) -> stage st + half * S2 of row / column r0 + r
-    for (u32 c = t; c < nrec * 16; c += blockDim.x) {
+    for (u32 c = t; c < nrec * 16; c += 256) {
         const u32 rec = c >> 4, ch = c & 15;
         const u32 rr = isA ? rec >> 1 : rec & (kDigitCols - 1), half = isA ? rec & 1 : rec / kDigitCols;
         const u64 r = r0 + rr, stg = st + half * S2;
         const v4i x = *reinterpret_cast<const v4i*>(img + rec * kDigitPitch + ch * 16);
         *reinterpret_cast<v4i*>(out + (r * stages + stg) * kRec + ch * 16) = x;
     }
+}
+
+__global__ void __launch_bounds__(256) k_digits(const i64* __restrict__ A0, const i64* __restrict__ A1,
+                                                const i64* __restrict__ B0, const i64* __restrict__ B1, u64 M,
+                                                u64 K, u64 N, u64 S2, u64 aGroups, u64 stages, u8* __restrict__ Ad,
+                                                u8* __restrict__ Bd) {
+    __shared__ __attribute__((aligned(16))) u8 img[2 * kDigitCols * kDigitPitch];  // record images
+    digit_group(true, blockIdx.x, threadIdx.x, img, A0, A1, B0, B1, M, K, N, S2, aGroups, stages, Ad, Bd);
 }
 
 // XCD-aware tile order. Workgroup ids are dealt round-robin to the 8 XCDs
@@ -624,20 +644,35 @@ Workspace carve(const GemmPlan& p, void* ws) {
     return w;
 }
 
-// Runs the digit split and the MFMA GEMM. One split: the GEMM writes the
-// product (minus `sub`, when given) straight to `out`; several: `splits`
-// partial slabs in w.P (the caller reduces them).
-void run_gemm(const GemmPlan& p, const i64* A, const i64* B, const Workspace& w, hipStream_t s, i64* out = nullptr,
-              const i64* sub = nullptr, hipEvent_t subReady = nullptr) {
-    const i64* A0 = A;
-    const i64* A1 = A + p.M * p.K;
-    const i64* B0 = B;
-    const i64* B1 = B + p.K * p.N;
+struct DigitArgs {
+    const i64 *A0, *A1, *B0, *B1;
+    u64 M, K, N, S2, aGroups, groups, stages;
+    u8 *Ad, *Bd;
+};
+DigitArgs digit_args(const GemmPlan& p, const i64* A, const i64* B, const Workspace& w) {
+    DigitArgs da;
+    da.A0 = A;
+    da.A1 = A + p.M * p.K;
+    da.B0 = B;
+    da.B1 = B + p.K * p.N;
+    da.M = p.M;
+    da.K = p.K;
+    da.N = p.N;
+    da.stages = p.Kc / BK;
+    da.S2 = p.Kp / 32;
+    da.aGroups = (p.Mp / kDigitRows) * da.S2;
+    da.groups = da.aGroups + (p.Np / kDigitCols) * da.S2;
+    da.Ad = w.Ad;
+    da.Bd = w.Bd;
+    return da;
+}
+
+// The MFMA GEMM over digit records already in the workspace. One split: the
+// GEMM writes the product (minus `sub`, when given) straight to `out`;
+// several: `splits` partial slabs in w.P (the caller reduces them).
+void run_share_gemm(const GemmPlan& p, const Workspace& w, hipStream_t s, i64* out = nullptr,
+                    const i64* sub = nullptr, hipEvent_t subReady = nullptr) {
     const u64 stages = p.Kc / BK;
-    const u64 S2 = p.Kp / 32;
-    const u64 aGroups = (p.Mp / kDigitRows) * S2, bGroups = (p.Np / kDigitCols) * S2;
-    launch(PROBE_DIGITS, k_digits, dim3((u32)(aGroups + bGroups)), dim3(256), 0, s, A0, A1, B0, B1, p.M, p.K, p.N, S2,
-           aGroups, stages, w.Ad, w.Bd);
     const u32 TM = (u32)(p.Mp / p.tbm), TN = (u32)(p.Np / BN);
     const bool direct = p.splits == 1 && out != nullptr;
     if (direct && sub && subReady) ABY3G_CHECK_HIP(hipStreamWaitEvent(s, subReady, 0));
@@ -654,6 +689,15 @@ void run_gemm(const GemmPlan& p, const i64* A, const i64* B, const Workspace& w,
                sps, TM, TN, p.splits, dst, sb);
 }
 
+// Runs the digit split and the MFMA GEMM.
+void run_gemm(const GemmPlan& p, const i64* A, const i64* B, const Workspace& w, hipStream_t s, i64* out = nullptr,
+              const i64* sub = nullptr, hipEvent_t subReady = nullptr) {
+    const DigitArgs da = digit_args(p, A, B, w);
+    launch(PROBE_DIGITS, k_digits, dim3((u32)da.groups), dim3(256), 0, s, da.A0, da.A1, da.B0, da.B1, p.M, p.K, p.N,
+           da.S2, da.aGroups, da.stages, w.Ad, w.Bd);
+    run_share_gemm(p, w, s, out, sub, subReady);
+}
+
 void check_ws(const GemmPlan& p, void* ws, size_t bytes) {
     ABY3G_REQUIRE(ws != nullptr && bytes >= p.total, "workspace too small (see aby3g_mul_workspace_bytes)");
 }
@@ -665,6 +709,13 @@ void check_ws(const GemmPlan& p, void* ws, size_t bytes) {
 using namespace aby3g;
 
 extern "C" {
+
+int aby3g_set_gemm_sharing(int parties) {
+    return guarded([&] {
+        ABY3G_REQUIRE(parties >= 1 && parties <= 256, "parties out of range");
+        t_gemm_sharing = (u32)parties;
+    });
+}
 
 int aby3g_mfma_turn(int on) {
     return guarded([&] { MfmaTurn::mode().store(on ? 1 : 0); });

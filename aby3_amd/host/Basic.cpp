@@ -216,4 +216,42 @@ void bool2arith(int pIdx, const sbMatrix& boolInput, si64Matrix& res, Sh3Encrypt
     res = std::move(out);
 }
 
+// ---- large messages (Basic.cpp:3-62) --------------------------------------
+namespace {
+Channel& neighbour(Sh3Runtime& rt, bool next) { return next ? rt.mComm.mNext : rt.mComm.mPrev; }
+void checkChunk(u64 chunk) {
+    if (!chunk) throw std::runtime_error("large_data: chunk size must be positive");
+}
+}  // namespace
+
+int large_data_sending(int, const i64Matrix& sharedA, Sh3Runtime& runtime, bool toNext, u64 chunk) {
+    checkChunk(chunk);
+    const u64 len = sharedA.mData.size();
+    Channel& ch = neighbour(runtime, toNext);
+    for (u64 o = 0; o < len; o += chunk) ch.asyncSendCopy(sharedA.mData.data() + o, 8 * std::min(chunk, len - o));
+    return 0;
+}
+
+int large_data_receiving(int, i64Matrix& res, Sh3Runtime& runtime, bool fromPrev, u64 chunk) {
+    checkChunk(chunk);
+    const u64 len = res.mData.size();
+    Channel& ch = neighbour(runtime, !fromPrev);
+    for (u64 o = 0; o < len; o += chunk) ch.recv(res.mData.data() + o, 8 * std::min(chunk, len - o));
+    return 0;
+}
+
+int large_data_sending(int, const i64* sharedA, u64 len, Sh3Runtime& runtime, bool toNext, u64 chunk) {
+    checkChunk(chunk);
+    Channel& ch = neighbour(runtime, toNext);
+    for (u64 o = 0; o < len; o += chunk) ch.asyncSendDevice(sharedA + o, 8 * std::min(chunk, len - o), runtime.gpu());
+    return 0;
+}
+
+int large_data_receiving(int, i64* res, u64 len, Sh3Runtime& runtime, bool fromPrev, u64 chunk) {
+    checkChunk(chunk);
+    Channel& ch = neighbour(runtime, !fromPrev);
+    for (u64 o = 0; o < len; o += chunk) ch.asyncRecvDevice(res + o, 8 * std::min(chunk, len - o), runtime.gpu()).get();
+    return 0;
+}
+
 }  // namespace aby3

@@ -61,6 +61,23 @@ void bool_cipher_min(int pIdx, const sbMatrix& A, const sbMatrix& B, sbMatrix& r
 void bool2arith(int pIdx, const sbMatrix& boolInput, si64Matrix& res, Sh3Encryptor& enc, Sh3Evaluator& eval,
                 Sh3Runtime& runtime);
 
+// ---- large messages (aby3-Basic/Basic.cpp:3-62): a column of `len` i64
+// sent to / received from a neighbour as messages of at most `chunk`
+// elements (MAX_SENDING_SIZE in the reference). The receiver must use the
+// same length and chunk size. toNext / fromPrev pick mNext / mPrev, as there.
+constexpr u64 MAX_SENDING_SIZE = 1ull << 25;
+// host columns (the reference's form): blocking, like its asyncSendFuture(..).get()
+int large_data_sending(int pIdx, const i64Matrix& sharedA, Sh3Runtime& runtime, bool toNext,
+                       u64 chunk = MAX_SENDING_SIZE);
+int large_data_receiving(int pIdx, i64Matrix& res, Sh3Runtime& runtime, bool fromPrev, u64 chunk = MAX_SENDING_SIZE);
+// device columns of this party: the chunks are enqueued on the party's
+// stream (sends) / delivered on it (receives: usable by later work on the
+// stream when the call returns)
+int large_data_sending(int pIdx, const i64* sharedA, u64 len, Sh3Runtime& runtime, bool toNext,
+                       u64 chunk = MAX_SENDING_SIZE);
+int large_data_receiving(int pIdx, i64* res, u64 len, Sh3Runtime& runtime, bool fromPrev,
+                         u64 chunk = MAX_SENDING_SIZE);
+
 // ---- sort: Sort.h (odd_even_merge, odd_even_multi_merge, high_dimensional_*)
 
 // Evaluate one library circuit on sbMatrix inputs (shared helper).

@@ -1,6 +1,9 @@
 #include "Circuit.h"
 #include <atomic>
 #include <algorithm>
+#include <fstream>
+#include <istream>
+#include <ostream>
 
 namespace aby3 {
 
@@ -342,7 +345,125 @@ BetaCircuit* CircuitLibrary::cmp_swap(u64 size) {
     });
 }
 
+namespace {
+// cryptoTools GateType codes (truth tables, bit a + 2b)
+constexpr u8 kTruthTable[8] = {6, 9, 8, 14, 1, 4, 10, 5};  // indexed by GateType
+GateType fromTruthTable(u8 t) {
+    for (u32 i = 0; i < 8; ++i)
+        if (kTruthTable[i] == t) return (GateType)i;
+    throw std::runtime_error("BetaCircuit::readBin: unsupported gate type " + std::to_string(t));
+}
+template <class T>
+void put(std::ostream& o, T v) {
+    o.write(reinterpret_cast<const char*>(&v), sizeof v);
+}
+template <class T>
+T get(std::istream& in) {
+    T v{};
+    in.read(reinterpret_cast<char*>(&v), sizeof v);
+    if (!in) throw std::runtime_error("BetaCircuit::readBin: truncated circuit file");
+    return v;
+}
+}  // namespace
+
+void BetaCircuit::writeBin(std::ostream& out) const {
+    u64 nonXor = 0;
+    for (const auto& g : mGates) nonXor += isAndType(g.type);
+    put<u64>(out, mWireCount);
+    put<u64>(out, nonXor);
+    for (const auto* bundles : {&mInputs, &mOutputs}) {
+        put<u64>(out, bundles->size());
+        for (const auto& b : *bundles) {
+            put<u64>(out, b.size());
+            out.write(reinterpret_cast<const char*>(b.data()), (std::streamsize)(4 * b.size()));
+        }
+    }
+    put<u64>(out, mGates.size());
+    for (const auto& g : mGates) {
+        put<u32>(out, g.in0);
+        put<u32>(out, g.in1);
+        put<u32>(out, g.out);
+        const u8 rec[4] = {kTruthTable[(u32)g.type], 0, 0, 0};
+        out.write(reinterpret_cast<const char*>(rec), 4);
+    }
+    if (!out) throw std::runtime_error("BetaCircuit::writeBin: write failed");
+}
+
+void BetaCircuit::readBin(std::istream& in) {
+    BetaCircuit c;
+    const u64 wires = get<u64>(in), nonXor = get<u64>(in);
+    if (wires > (1ull << 31)) throw std::runtime_error("BetaCircuit::readBin: wire count out of range");
+    c.mWireCount = (u32)wires;
+    std::vector<u8> defined(wires, 0);
+    for (auto* bundles : {&c.mInputs, &c.mOutputs}) {
+        const u64 nb = get<u64>(in);
+        if (nb > wires + 1) throw std::runtime_error("BetaCircuit::readBin: bundle count out of range");
+        bundles->resize(nb);
+        for (auto& b : *bundles) {
+            const u64 n = get<u64>(in);
+            if (n > wires) throw std::runtime_error("BetaCircuit::readBin: bundle size out of range");
+            b.resize(n);
+            for (auto& w : b) {
+                w = get<u32>(in);
+                if (w >= wires) throw std::runtime_error("BetaCircuit::readBin: wire index out of range");
+            }
+        }
+    }
+    for (const auto& b : c.mInputs)
+        for (u32 w : b) defined[w] = 1;
+    const u64 ng = get<u64>(in);
+    if (ng > wires) throw std::runtime_error("BetaCircuit::readBin: gate count out of range");
+    c.mGates.resize(ng);
+    u64 ands = 0;
+    for (auto& g : c.mGates) {
+        g.in0 = get<u32>(in);
+        g.in1 = get<u32>(in);
+        g.out = get<u32>(in);
+        const u32 rec = get<u32>(in);
+        g.type = fromTruthTable((u8)(rec & 0xff));
+        const bool unary = g.type == GateType::a || g.type == GateType::Inv;
+        if (g.in0 >= wires || g.in1 >= wires || g.out >= wires)
+            throw std::runtime_error("BetaCircuit::readBin: gate wire out of range");
+        if (!defined[g.in0] || (!unary && !defined[g.in1]))
+            throw std::runtime_error("BetaCircuit::readBin: gate input used before it is defined");
+        if (defined[g.out]) throw std::runtime_error("BetaCircuit::readBin: wire defined twice");
+        defined[g.out] = 1;
+        ands += isAndType(g.type);
+    }
+    if (ands != nonXor) throw std::runtime_error("BetaCircuit::readBin: non-XOR gate count mismatch");
+    for (const auto& b : c.mOutputs)
+        for (u32 w : b)
+            if (!defined[w]) throw std::runtime_error("BetaCircuit::readBin: output wire never defined");
+    mWireCount = c.mWireCount;
+    mGates = std::move(c.mGates);
+    mInputs = std::move(c.mInputs);
+    mOutputs = std::move(c.mOutputs);
+    mLevelGates.clear();
+    mLevelCounts.clear();
+    mLevelAndCounts.clear();
+    mLevelBatches.clear();
+    mBatchGates.clear();
+    mBatchZRow.clear();
+    mBatchSendRow.clear();
+    mAndCount = 0;
+    mSerial = g_circuitSerial++;  // a new circuit for the device caches
+}
+
 BetaCircuit* CircuitLibrary::byName(const std::string& n, u64 size, u64 param) {
+    // "bin:<path>": a circuit file (BetaCircuit::readBin), levelized on load
+    if (n.compare(0, 4, "bin:") == 0) {
+        auto key = std::make_pair(n, (u64)0);
+        auto& slot = mCirMap[key];
+        if (!slot) {
+            std::ifstream f(n.substr(4), std::ios::binary);
+            if (!f) throw std::runtime_error("cannot open circuit file " + n.substr(4));
+            auto c = std::make_unique<BetaCircuit>();
+            c->readBin(f);
+            c->levelByAndDepth();
+            slot = std::move(c);
+        }
+        return slot.get();
+    }
     if (n == "int_comp_helper") return int_comp_helper(size);
     if (n == "int_int_lt") return int_int_lt(size);
     if (n == "int_eq") return int_eq(size);

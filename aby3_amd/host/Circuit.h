@@ -12,6 +12,7 @@
 //  and share-level against the oracle on the same gate list.
 #pragma once
 #include "Defines.h"
+#include <iosfwd>
 #include <map>
 #include <memory>
 #include <vector>
@@ -64,6 +65,22 @@ public:
 
     // plaintext evaluation on 64-bit words (tests; row r of a word = bit r)
     std::vector<std::vector<u64>> evalPlain(const std::vector<std::vector<u64>>& inputs) const;
+
+    // Binary circuit files (cryptoTools BetaCircuit::writeBin / readBin, used
+    // by aby3-DB/DBServer.cpp:48-54 and aby3-DB_tests/lowMC.cpp:296-324 to
+    // store and reload externally built circuits). cryptoTools is not vendored
+    // in the reference, so the layout is this restatement of its published
+    // form, all fields little-endian:
+    //   u64 wireCount, u64 nonXorGateCount,
+    //   u64 #inputs,  per bundle: u64 size, u32 wire[size],
+    //   u64 #outputs, per bundle: u64 size, u32 wire[size],
+    //   u64 #gates,   per gate: u32 in0, u32 in1, u32 out, u8 type, u8 pad[3]
+    // with `type` cryptoTools' GateType code (the gate's truth table, bit
+    // a + 2b = output: Xor 6, Nxor 9, And 8, Or 14, Nor 1, na_And 4, a 10,
+    // na 5). readBin checks every index and the topological order and
+    // returns the circuit unlevelized (levelByAndDepth() before evaluation).
+    void writeBin(std::ostream& out) const;
+    void readBin(std::istream& in);
 
 private:
     u64 mSerial;

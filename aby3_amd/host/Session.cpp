@@ -7,6 +7,7 @@
 #include <cmath>
 #include <condition_variable>
 #include <cstdio>
+#include <fstream>
 #include <functional>
 #include <numeric>
 #include <thread>
@@ -449,6 +450,8 @@ struct Session {
                 // hardware queues every party's stream has a queue of its own
                 // (measured: 3 streams beat 6 sharing 4 queues on every job)
                 if (colocated) p.rt.gpu().aliasAux();
+                // their share GEMMs run side by side: each fills its share of the CUs
+                if (colocated) GPU_CALL(aby3g_set_gemm_sharing(3));
                 p.rt.gpu().aux();
             });
             if (job->mlSeeds()) {
@@ -701,6 +704,20 @@ void aby3h_session_destroy(aby3h_session* h) {
     for (auto& t : s.th)
         if (t.joinable()) t.join();
     delete h;
+}
+
+int aby3h_circuit_write(const char* name, uint64_t size, uint64_t param, const char* path) {
+    try {
+        CircuitLibrary lib;
+        BetaCircuit* c = lib.byName(name, size, param);
+        std::ofstream f(path, std::ios::binary | std::ios::trunc);
+        if (!f) throw std::runtime_error(std::string("cannot write ") + path);
+        c->writeBin(f);
+        return 0;
+    } catch (const std::exception& e) {
+        t_err = e.what();
+        return 1;
+    }
 }
 
 int aby3h_circuit(const char* name, uint64_t size, uint64_t param, uint64_t counts[6], uint32_t* gates,

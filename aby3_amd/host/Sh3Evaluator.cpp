@@ -137,27 +137,13 @@ Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, const si64Matrix& A, const si64Matri
                 std::memcpy(ts.prev_seed, mShareGen.mPrevSeed.data(), 16);
                 ts.next_off = mShareGen.takeNext(8 * n);
                 ts.prev_off = mShareGen.takePrev(8 * n);
-                // One launch pass for the product's epilogue, the truncation pair
-                // and z when the product is small / element-wise, or when this
-                // party has no second stream (co-located parties: the share GEMM
-                // holds every CU's registers while it runs, so nothing would
-                // overlap it and the fused form saves the split-K slab pass).
-                if (aby3g_mul_prefers_fused((int)mode, M, K, N) || g.auxAliased()) {
-                    GPU_CALL(aby3g_mul_trunc_local((int)mode, A.data(), B.data(), M, K, N, (unsigned)shift, &ts,
-                                                   z->as<i64>(), C.data(), ws, wsBytes, g.stream()));
-                } else {
-                    // the truncation pair (AES-CTR of both streams) on the auxiliary
-                    // stream, beside the share GEMM on the main stream. r and C's RT
-                    // are written on aux; the main stream waits for them (rReady)
-                    // before the pass that reads r, so freeing r into the main
-                    // stream's pool and later uses of C are ordered.
-                    DeviceBuffer r(g, bytes);
-                    g.forkAux();
-                    GPU_CALL(aby3g_trunc_tuple(&ts, n, (unsigned)shift, r.as<i64>(), C.data(), g.aux()));
-                    aby3g_event rReady = g.aux() == g.stream() ? nullptr : g.recordAux();
-                    GPU_CALL(aby3g_mul_sub_local((int)mode, A.data(), B.data(), r.as<i64>(), rReady, z->as<i64>(), M,
-                                                 K, N, ws, wsBytes, g.stream()));
-                }
+                // The truncation pair's AES-CTR runs inside the product's own
+                // passes: in the element-wise / small-GEMM epilogue, or, for a
+                // share GEMM, in the launch that splits the operands into digits
+                // (HBM-bound; the AES workgroups share its CUs), with z =
+                // product - r in the GEMM's epilogue or slab-reducing pass.
+                GPU_CALL(aby3g_mul_trunc_local((int)mode, A.data(), B.data(), M, K, N, (unsigned)shift, &ts,
+                                               z->as<i64>(), C.data(), ws, wsBytes, g.stream()));
             }
             // reveal z to parties 0 and 1 (:681-684)
             const u64 p = self.getRuntime().mPartyIdx;

@@ -79,6 +79,11 @@ public:
 };
 
 // sbMatrix (Sh3Types.h:335-387): rows x ceil(bitCount/64) words per share.
+// si64 (Sh3Types.h:113-170): one replicated 64-bit share pair, host values.
+struct si64 {
+    i64 mData[2] = {0, 0};
+};
+
 class sbMatrix : public SharedMat {
 public:
     sbMatrix() = default;

@@ -10,6 +10,7 @@
 #include <thread>
 #include "Basic.h"
 #include "Sh3Piecewise.h"
+#include "Shuffle.h"
 #include "aby3ML.h"
 
 namespace aby3 {
@@ -227,6 +228,56 @@ int aby3h_sim_cipher_gt(int device, const int64_t* a, const int64_t* b, uint64_t
             i64Matrix r;
             p.enc.revealAll(p.rt, g, r).get();
             if (p.idx == 0 && out_plain) std::memcpy(out_plain, r.mData.data(), 8 * n);
+        });
+    });
+}
+
+int aby3h_sim_shuffle(int device, int mode, const int64_t* x, uint64_t len, uint64_t unit, int64_t* out_shares,
+                      int64_t* out_pi_shares, int64_t* out_plain) {
+    return guarded([&] {
+        if (mode < 0 || mode > 3) throw std::runtime_error("unknown shuffle mode");
+        if (mode == 1 && unit != 1) throw std::runtime_error("the sbMatrix form takes one word per row");
+        if (!len || !unit) throw std::runtime_error("empty input");
+        const u64 L = len * unit;
+        run3(device, [&](SimParty& p) {
+            // party 0 shares x [len][unit] as one binary matrix (row-major
+            // draws: the same as sharing the units one after the other)
+            sbMatrix X(len, 64 * unit), R(len, 64 * unit), Pi(len, 64);
+            shareBinIn(p, hostMat(x, len, unit), X);
+            Gpu& g = p.rt.gpu();
+            if (mode == 1) {
+                efficient_shuffle(X, p.idx, R, p.enc, p.eval, p.rt);
+            } else if (mode == 3) {
+                efficient_shuffle_units(reinterpret_cast<const u64*>(X.data()), len, unit, p.idx,
+                                        reinterpret_cast<u64*>(R.data()), p.enc, p.rt);
+            } else {
+                // the reference's vector<sbMatrix> form: one unit per matrix
+                std::vector<sbMatrix> T(len), Tres;
+                for (u64 i = 0; i < len; ++i) {
+                    T[i].resize(unit, 64);
+                    for (int sh = 0; sh < 2; ++sh) d2d(T[i].share(sh), X.share(sh) + i * unit, 8 * unit, g);
+                }
+                std::vector<si64> pi;
+                if (mode == 0)
+                    efficient_shuffle(T, p.idx, Tres, p.enc, p.eval, p.rt);
+                else
+                    efficient_shuffle_with_random_permutation(T, p.idx, Tres, pi, p.enc, p.eval, p.rt);
+                for (u64 i = 0; i < len; ++i)
+                    for (int sh = 0; sh < 2; ++sh) d2d(R.share(sh) + i * unit, Tres[i].share(sh), 8 * unit, g);
+                if (mode == 2) {
+                    std::vector<i64> h(2 * len);
+                    for (u64 i = 0; i < len; ++i) {
+                        h[i] = pi[i].mData[0];
+                        h[len + i] = pi[i].mData[1];
+                    }
+                    toDevice(Pi.data(), h.data(), 16 * len, g);
+                }
+            }
+            putShares(p.idx, R, out_shares);
+            if (mode == 2) putShares(p.idx, Pi, out_pi_shares);
+            i64Matrix r;
+            p.enc.revealAll(p.rt, R, r).get();
+            if (p.idx == 0 && out_plain) std::memcpy(out_plain, r.mData.data(), 8 * L);
         });
     });
 }

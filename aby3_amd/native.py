@@ -99,6 +99,9 @@ _SIGS = {
     "aby3g_host_register": (c_int, [c_void_p, c_size_t, POINTER(c_void_p)]),
     "aby3g_host_unregister": (c_int, [c_void_p]),
     "aby3g_enable_peer_access": (c_int, [c_int, c_int]),
+    "aby3g_set_gemm_sharing": (c_int, [c_int]),
+    "aby3g_u64_xor_gather_units": (c_int, [c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                           c_void_p, c_void_p]),
     "aby3g_probe_enable": (c_int, [c_int]),
     "aby3g_probe_enable_mask": (c_int, [ctypes.c_uint32]),
     "aby3g_probe_read": (c_int, [c_int, POINTER(c_double), POINTER(c_uint64)]),
@@ -211,6 +214,7 @@ _HOST_SIGS = {
     "aby3h_session_destroy": (None, [c_void_p]),
     "aby3h_circuit": (c_int, [c_char_p, c_uint64, c_uint64, POINTER(c_uint64), c_void_p, c_void_p, c_void_p,
                               c_void_p, c_void_p, c_void_p]),
+    "aby3h_circuit_write": (c_int, [c_char_p, c_uint64, c_uint64, c_char_p]),
     "aby3h_sim_last_error": (c_char_p, []),
     "aby3h_sim_mul": (c_int, [c_int, c_int, c_int, c_uint64, c_void_p, c_void_p, c_uint64, c_uint64, c_uint64,
                               c_void_p, c_void_p]),
@@ -222,6 +226,7 @@ _HOST_SIGS = {
                              c_void_p, c_void_p, c_void_p]),
     "aby3h_lr_dataset": (c_int, [c_uint64, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p]),
     "aby3h_lr_batches": (c_int, [c_uint64, c_uint64, c_uint64, c_void_p]),
+    "aby3h_sim_shuffle": (c_int, [c_int, c_int, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p]),
     "aby3h_sim_merge": (c_int, [c_int, c_int, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p]),
 }
 
@@ -308,6 +313,14 @@ class Session:
 
     def __exit__(self, *a):
         self.close()
+
+
+def circuit_write(name: str, path: str, size: int = 64, param: int = 0):
+    """Store a library circuit in the BetaCircuit binary format; "bin:" + path
+    then names it for circuit() / sim.circuit()."""
+    h = host()
+    if h.aby3h_circuit_write(name.encode(), size, param, path.encode()) != 0:
+        raise NativeError(h.aby3h_last_error().decode())
 
 
 def circuit(name: str, size: int = 64, param: int = 0) -> dict:
@@ -407,6 +420,19 @@ class sim:
         sh, plain = np.zeros(6 * n, np.int64), np.zeros(n, np.int64)
         cls._call("aby3h_sim_piecewise", device, kind, cls._p(x), n, D, cls._p(sh), cls._p(plain))
         return sh.reshape(3, 2, -1), plain
+
+    @classmethod
+    def shuffle(cls, x, mode=0, device=0):
+        """x [len][unit] int64; returns (shares [3][2][len*unit], revealed
+        [len][unit], permutation shares [3][2][len] or None)."""
+        np = cls._np()
+        x = np.ascontiguousarray(np.asarray(x, np.int64).reshape(len(x), -1))
+        n, unit = x.shape
+        sh, plain = np.zeros(6 * n * unit, np.int64), np.zeros(n * unit, np.int64)
+        pi = np.zeros(6 * n, np.int64) if mode == 2 else None
+        cls._call("aby3h_sim_shuffle", device, mode, cls._p(x), n, unit, cls._p(sh),
+                  cls._p(pi) if pi is not None else None, cls._p(plain))
+        return sh.reshape(3, 2, -1), plain.reshape(n, unit), (pi.reshape(3, 2, -1) if pi is not None else None)
 
     @classmethod
     def cipher_gt(cls, a, b, device=0):

@@ -104,6 +104,12 @@ int aby3h_circuit(const char* name, uint64_t size, uint64_t param, uint64_t coun
                   uint32_t* level_counts, uint32_t* in_sizes, uint32_t* in_wires, uint32_t* out_sizes,
                   uint32_t* out_wires);
 
+/* Writes a library circuit to `path` in the BetaCircuit binary format
+ * (BetaCircuit::writeBin, aby3_amd/host/Circuit.h). Any circuit name above
+ * also accepts "bin:<path>": the circuit stored in that file (readBin,
+ * levelized on load), so externally built circuits run on the engine. */
+int aby3h_circuit_write(const char* name, uint64_t size, uint64_t param, const char* path);
+
 /* ---- one protocol call by three in-process parties ---------------------
  * The topology and seeds of the reference's unit tests
  * (Sh3EvaluatorTests.cpp:23-131): encryptor seeds toBlock(0, i) /
@@ -143,6 +149,15 @@ int aby3h_sim_cipher_gt(int device, const int64_t* a, const int64_t* b, uint64_t
  * [party][share][total] of the same (either may be NULL). */
 int aby3h_sim_merge(int device, int mode, const uint64_t* lens, uint64_t nlists, uint64_t dim, const int64_t* keys,
                     int64_t* out_sorted, int64_t* out_shares);
+/* The 3-party shuffle (aby3-Basic/Shuffle.cpp, aby3_amd/host/Shuffle.h) of
+ * x [len][unit] (binary-shared by party 0 as one matrix): mode 0
+ * efficient_shuffle(vector<sbMatrix>, one unit per matrix), 1
+ * efficient_shuffle(sbMatrix) (unit 1), 2 efficient_shuffle_with_random_
+ * permutation (out_pi_shares [party][share][len]: the applied permutation),
+ * 3 the packed form efficient_shuffle_units (same result as mode 0).
+ * out_shares [party][share][len*unit], out_plain the revealed units. */
+int aby3h_sim_shuffle(int device, int mode, const int64_t* x, uint64_t len, uint64_t unit, int64_t* out_shares,
+                      int64_t* out_pi_shares, int64_t* out_plain);
 /* `iters` SGD_Logistic iterations (aby3-ML/Regression.h:249-293) by three
  * parties seeded as aby3ML::init (aby3ML.cpp:4-17): party 0 shares X [n][d],
  * Y [n] (fixed point D) and w = 0 [d], iteration t uses the B row indices

@@ -180,6 +180,11 @@ typedef struct {
  * overlapping GEMMs finish sooner together, but a launch's span then includes
  * the CUs spent on the others' -- bench.py's roofline pass takes turns. */
 int aby3g_mfma_turn(int on);
+/* The calling thread's share GEMMs run beside those of `parties` parties in
+ * all (co-located parties, one stream each): split-K then fills 1/parties of
+ * the CUs per GEMM (the others' GEMMs take the rest) instead of the whole
+ * device. Default 1. Plans (and aby3g_mul_workspace_bytes) depend on it. */
+int aby3g_set_gemm_sharing(int parties);
 
 /* 1 when the whole round-1 local part runs best as one fused launch
  * (aby3g_mul_trunc_local / aby3g_mul_local with zs): Hadamard, and GEMMs of
@@ -424,6 +429,15 @@ int aby3g_i64_transpose(const int64_t* src, uint64_t rows, uint64_t cols, int64_
 /* dst[i] = src[idx[i]] (gather) and dst[idx[i]] = src[i] (scatter), u64. */
 int aby3g_u64_gather(uint64_t n, const uint32_t* idx, const uint64_t* src, uint64_t* dst, aby3g_stream stream);
 int aby3g_u64_scatter(uint64_t n, const uint32_t* idx, const uint64_t* src, uint64_t* dst, aby3g_stream stream);
+/* One step of the 3-party shuffle (aby3-Basic/Shuffle.cpp): `units` units of
+ * `unit` u64 words, out[i] = a[g] ^ b[g] ^ c[g] ^ mask with g = idx[i] (idx
+ * NULL: g = i; any of a, b, c, mask NULL: omitted; mask is one unit, the
+ * same for every unit, as get_random_mask draws it for a vector of units).
+ * A permutation that scatters (tmp[p[i]] = data[i], Basics.h:324-332) is
+ * applied as the gather of its inverse. */
+int aby3g_u64_xor_gather_units(uint64_t units, uint64_t unit, const uint32_t* idx, const uint64_t* a,
+                               const uint64_t* b, const uint64_t* c, const uint64_t* mask, uint64_t* out,
+                               aby3g_stream stream);
 
 #ifdef __cplusplus
 }

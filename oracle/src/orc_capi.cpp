@@ -394,6 +394,44 @@ double orc_bench_mul_trunc(int mode, uint64_t M, uint64_t K, uint64_t N, uint64_
 }
 
 
+// The shuffles of aby3-Basic/Shuffle.cpp by three parties with the
+// encryptor seeds toBlock(0, i): x [len][unit] shared by party 0 as one
+// binary matrix. mode 0 efficient_shuffle(vector<sbMatrix>), 1
+// efficient_shuffle(sbMatrix) (unit 1), 2 efficient_shuffle_with_random_
+// permutation. out_shares [3][2][len*unit], out_pi_shares [3][2][len] (mode 2),
+// out_plain [len*unit]; any may be NULL.
+int orc_sim_shuffle(int mode, const int64_t* x, uint64_t len, uint64_t unit, int64_t* out_shares,
+                    int64_t* out_pi_shares, int64_t* out_plain) {
+    return guard([&] {
+        if (mode < 0 || mode > 2) throw std::runtime_error("unknown shuffle mode");
+        if (mode == 1 && unit != 1) throw std::runtime_error("the sbMatrix form takes one word per row");
+        auto enc = makeEncryptors(0);
+        Shared T = shareBin(enc, 0, toMat(x, len, unit));
+        Shared pi, out;
+        if (mode == 0)
+            out = shuffleUnits(enc, T);
+        else if (mode == 1)
+            out = shuffleRows(enc, T);
+        else
+            out = shuffleWithPermutation(enc, T, pi);
+        if (!consistent(out) || (mode == 2 && !consistent(pi))) throw std::runtime_error("inconsistent shares");
+        if (out_shares) putShared(out, out_shares);
+        if (out_pi_shares && mode == 2) putShared(pi, out_pi_shares);
+        if (out_plain) {
+            Mat r = revealBin(out);
+            memcpy(out_plain, r.v.data(), 8 * r.size());
+        }
+    });
+}
+
+// get_permutation(len, seed) (BoolBasic.cpp:925-934)
+int orc_shuffle_permutation(uint64_t len, const uint8_t seed[16], uint64_t* out) {
+    return guard([&] {
+        auto p = shufflePermutation(len, seed);
+        memcpy(out, p.data(), 8 * len);
+    });
+}
+
 // CPU baseline of C1: asyncMul without truncation
 // (Sh3Evaluator.cpp:92-116), one thread per party: each party's local share
 // product as Eigen evaluates it (three i64 products, or the fork's

@@ -318,4 +318,14 @@ void mlParties(std::array<Party, 3>& enc, std::array<Party, 3>& ev);
 void sgdLogisticIteration(std::array<Party, 3>& ev, const Circuit& pwHelper, const Shared& X, const Shared& Y,
                           Shared& w, const std::vector<u64>& batch, u64 D, u64 aB);
 
+// --------------------------------------------------------------------------
+// 3-party shuffle (aby3-Basic/Shuffle.cpp, orc_shuffle.cpp). T: units as the
+// rows of an SMat [len][unit] (the encryptor's prev / next seeds drive the
+// permutations and masks).
+// --------------------------------------------------------------------------
+std::vector<u64> shufflePermutation(u64 len, const u8 seed[16]);  // get_permutation
+Shared shuffleUnits(std::array<Party, 3>& enc, const Shared& T);    // efficient_shuffle(vector)
+Shared shuffleRows(std::array<Party, 3>& enc, const Shared& T);     // efficient_shuffle(sbMatrix)
+Shared shuffleWithPermutation(std::array<Party, 3>& enc, const Shared& T, Shared& Pi);
+
 }  // namespace orc

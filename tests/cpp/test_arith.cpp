@@ -3,6 +3,7 @@
 // multiplications and reveal -- every party's shares bit-exact against the
 // CPU oracle on the reference tests' seeds (Sh3EvaluatorTests.cpp:594-690,
 // :350-410, :780-1032; Test.cpp:74-191).
+#include "Basic.h"
 #include "harness.h"
 
 using namespace aby3;
@@ -130,7 +131,48 @@ static void arithBasic16() {
     for (int i = 0; i < T; ++i) check(revealed[i] == i * (T - i), "mul 16");
 }
 
+// large_data_sending / large_data_receiving (aby3-Basic/Basic.cpp:3-62):
+// host and device columns in chunks, both directions, ragged last chunk
+static void largeData(u64 len, u64 chunk) {
+    i64Matrix col(len, 1);
+    for (u64 i = 0; i < len; ++i) col(i, 0) = (i64)(i * 0x9E3779B97F4A7C15ull);
+    i64Matrix gotHost, gotDev, gotBack;
+    run3([&](harness::Party& p) {
+        Gpu& g = p.rt.gpu();
+        if (p.idx == 0) {
+            large_data_sending(0, col, p.rt, true, chunk);  // host -> P1
+            DeviceBuffer d(g, 8 * len);
+            toDevice(d.data(), col.mData.data(), 8 * len, g);
+            large_data_sending(0, d.as<i64>(), len, p.rt, true, chunk);  // device -> P1
+            g.sync();
+        } else if (p.idx == 1) {
+            i64Matrix h(len, 1);
+            large_data_receiving(1, h, p.rt, true, chunk);
+            gotHost = h;
+            DeviceBuffer d(g, 8 * len);
+            large_data_receiving(1, d.as<i64>(), len, p.rt, true, chunk);
+            i64Matrix back(len, 1);
+            toHost(back.mData.data(), d.data(), 8 * len, g);
+            gotDev = back;
+            large_data_sending(1, d.as<i64>(), len, p.rt, false, chunk);  // device -> P0, P1's prev
+            g.sync();
+        }
+        if (p.idx == 0) {
+            i64Matrix h(len, 1);
+            DeviceBuffer d(g, 8 * len);
+            large_data_receiving(0, d.as<i64>(), len, p.rt, false, chunk);  // from next (P1)
+            toHost(h.mData.data(), d.data(), 8 * len, g);
+            gotBack = h;
+        }
+    });
+    check(gotHost.mData == col.mData, "host column");
+    check(gotDev.mData == col.mData, "device column");
+    check(gotBack.mData == col.mData, "device column back to prev");
+}
+
 int main() {
+    test("large_data_sending_receiving_10007_in_chunks_of_1000", [] { largeData(10007, 1000); });
+    test("large_data_sending_receiving_4096_one_chunk", [] { largeData(4096, MAX_SENDING_SIZE); });
     test("share_reveal_and_hadamard_16 (Test.cpp arith_basic_test mul)", arithBasic16);
     test("asyncMul_hadamard_128x128", [] { mulTest(MulMode::Hadamard, 128, 128, 128, false, 0, 1); });
     test("asyncMul_gemm_10x10 (Sh3_Evaluator_mul_test)", [] { mulTest(MulMode::Gemm, 10, 10, 10, false, 0, 2); });

@@ -5,6 +5,7 @@
 // Sh3BinaryEvaluatorTests.cpp:333-424 (add / msb), BoolTest.cpp (lt = [A<B]).
 #include "Circuit.h"
 #include <cstdio>
+#include <sstream>
 #include <functional>
 #include <limits>
 #include <random>
@@ -158,6 +159,65 @@ int main() {
                 check(o[2][i] == (u64)(v >= t1), "region 2");
             }
         }
+    });
+    test("BetaCircuit writeBin / readBin round trip (DBServer.cpp:48-54)", [&] {
+        const char* names[] = {"int_comp_helper", "int_int_lt", "int_eq", "int_int_add", "int_int_sub",
+                               "cmp_swap", "bits_nor_helper", "int_Sh3Piecewise_helper"};
+        for (const char* n : names) {
+            BetaCircuit* c = lib.byName(n, 64, 2);
+            std::stringstream f;
+            c->writeBin(f);
+            const std::string bytes = f.str();
+            BetaCircuit d;
+            d.readBin(f);
+            check(d.mWireCount == c->mWireCount && d.mGates.size() == c->mGates.size(), std::string(n) + " shape");
+            for (size_t i = 0; i < c->mGates.size(); ++i) {
+                const auto &g = c->mGates[i], &h = d.mGates[i];
+                check(g.in0 == h.in0 && g.in1 == h.in1 && g.out == h.out && g.type == h.type, std::string(n) + " gate");
+            }
+            check(d.mInputs == c->mInputs && d.mOutputs == c->mOutputs, std::string(n) + " bundles");
+            d.levelByAndDepth();
+            levelInvariants(&d);
+            check(d.mAndCount == c->mAndCount && d.mLevelCounts == c->mLevelCounts, std::string(n) + " levels");
+            check(d.serial() != c->serial(), "a loaded circuit gets its own serial");
+            std::vector<std::vector<u64>> in;
+            for (size_t b = 0; b < c->mInputs.size(); ++b) in.push_back(samples(64, 100 + b));
+            check(d.evalPlain(in) == c->evalPlain(in), std::string(n) + " evaluation");
+            std::stringstream f2;
+            d.writeBin(f2);
+            check(f2.str() == bytes, std::string(n) + " re-written bytes");
+            // u64 wires, u64 nonXor, bundles, u64 gates, 16 B per gate
+            u64 expect = 8 * 5;
+            for (auto* bs : {&c->mInputs, &c->mOutputs})
+                for (auto& b : *bs) expect += 8 + 4 * b.size();
+            check(bytes.size() == expect + 16 * c->mGates.size(), std::string(n) + " layout size");
+        }
+    });
+    test("BetaCircuit readBin rejects malformed files", [&] {
+        std::stringstream f;
+        lib.int_int_add(8)->writeBin(f);
+        const std::string good = f.str();
+        auto rejects = [&](std::string b, const char* what) {
+            std::stringstream in(b);
+            BetaCircuit d;
+            bool threw = false;
+            try {
+                d.readBin(in);
+            } catch (const std::runtime_error&) {
+                threw = true;
+            }
+            check(threw, what);
+        };
+        rejects(good.substr(0, good.size() - 3), "truncated");
+        std::string t = good;
+        t[t.size() - 4] = 7;  // last gate: Nand (unsupported)
+        rejects(t, "gate type");
+        t = good;
+        t[0] = 2;  // wire count 2: indices out of range
+        rejects(t, "wire range");
+        t = good;
+        t[8] ^= 1;  // non-XOR count off by one
+        rejects(t, "and count");
     });
     return failures ? 1 : 0;
 }

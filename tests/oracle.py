@@ -220,3 +220,41 @@ def sim_lr(cir, X, Y, batches, D: int = 16, aB: int = 11):
     _check(dll().orc_sim_lr(*args, u(n), u(d), u(B), u(D), u(aB), u(iters), _p(X), _p(Y), _p(batches), _p(sh),
                             _p(w)))
     return sh.reshape(3, 2, d), w
+
+
+def shuffle_permutation(n: int, seed: bytes) -> np.ndarray:
+    """get_permutation(n, seed) (BoolBasic.cpp:925-934)."""
+    out = np.zeros(n, dtype=np.uint64)
+    _check(dll().orc_shuffle_permutation(c_uint64(n), seed, _p(out)))
+    return out.astype(np.int64)
+
+
+def sim_shuffle(x: np.ndarray, mode: int = 0):
+    """The shuffles of Shuffle.cpp by three parties (encryptor seeds
+    toBlock(0, i)); x [len][unit]. Returns (shares [3][2][len*unit], revealed
+    [len][unit], permutation shares [3][2][len] or None)."""
+    x = np.ascontiguousarray(np.asarray(x, dtype=np.int64).reshape(len(x), -1))
+    n, unit = x.shape
+    sh = np.zeros(6 * n * unit, dtype=np.int64)
+    plain = np.zeros(n * unit, dtype=np.int64)
+    pi = np.zeros(6 * n, dtype=np.int64) if mode == 2 else None
+    _check(dll().orc_sim_shuffle(c_int(mode), _p(x), c_uint64(n), c_uint64(unit), _p(sh),
+                                 _p(pi) if pi is not None else None, _p(plain)))
+    return sh.reshape(3, 2, -1), plain.reshape(n, unit), (pi.reshape(3, 2, -1) if pi is not None else None)
+
+
+def reference_shuffle_order(n: int, c: int = 0):
+    """The expected result of shuffle_test (aby3_tests/Test.cpp:305-340) for
+    encryptor seeds toBlock(c, i): party 0's permutation list {next, prev,
+    party 1's next} combined (BoolBasic.cpp:946-961); returns final_permutation
+    (the scattering plain_permutate puts unit i at final[i])."""
+    perms = [shuffle_permutation(n, to_block(c, 1)), shuffle_permutation(n, to_block(c, 0)),
+             shuffle_permutation(n, to_block(c, 2))]
+    final = np.arange(n, dtype=np.int64)
+    for p in reversed(perms):
+        inv = np.empty(n, dtype=np.int64)
+        inv[p] = np.arange(n)
+        tmp = np.empty(n, dtype=np.int64)
+        tmp[inv] = final
+        final = tmp
+    return final

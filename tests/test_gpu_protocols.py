@@ -79,6 +79,20 @@ def test_circuit_vs_oracle(gpu, name, bits, rows):
         assert np.array_equal(res_g[o], res_o[o])
 
 
+def test_circuit_file_vs_oracle(gpu, tmp_path):
+    """An externally stored circuit (BetaCircuit binary file, "bin:" name)
+    evaluated by the GPU engine, share-exact against the oracle."""
+    path = str(tmp_path / "add64.bin")
+    nt.circuit_write("int_int_add", path, 64)
+    name = "bin:" + path
+    cir = nt.circuit(name)
+    ins = [rand(3001, 30), rand(3001, 31)]
+    shs_g, res_g = nt.sim.circuit(name, 64, 0, 3001, ins)
+    res_o, shs_o = orc.sim_circuit(cir, 3001, ins, with_shares=True)
+    assert np.array_equal(shs_g[0], shs_o[0]) and np.array_equal(res_g[0], res_o[0])
+    assert np.array_equal(res_g[0][:, 0], (ins[0].astype(np.uint64) + ins[1].astype(np.uint64)).astype(np.int64))
+
+
 @pytest.mark.parametrize("kind,n,D", [(0, 256, 16), (0, 1, 16), (1, 500, 8)])
 def test_piecewise_vs_oracle(gpu, kind, n, D):
     x = rand(n, 21, 3 << D)

@@ -517,7 +517,12 @@ def main():
             "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_*.json)",
             "launch_ms": gemm_avg_s * 1e3,
             "launch_ms_measured": "HIP events around every share-GEMM launch of a 30-step pass whose co-located "
-                                  "parties' GEMMs take turns (aby3g_mfma_turn); in the timed region they overlap",
+                                  "parties' GEMMs take turns (aby3g_mfma_turn); in the timed region they overlap. "
+                                  "Co-located parties plan each GEMM for a third of the chip "
+                                  "(aby3g_set_gemm_sharing(3): 128 workgroups of 128x64 tiles, one K split at "
+                                  "1024^3), so a launch alone leaves half the CUs to the other parties' kernels",
+            "job_mfma_rate": info["gemm_int8_ops"] * 3 / (dt / args.steps) / 1e12,
+            "job_mfma_rate_unit": "TOP/s: the three parties' share-GEMM int8 ops per step / the whole step",
             "launch_span_ms_overlapped": ovl_ms / max(ovl_n, 1),
             "ops_per_launch": info["gemm_int8_ops"],
         },

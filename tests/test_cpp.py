@@ -36,6 +36,12 @@ def test_binary_protocols_gpu():
 
 
 @pytest.mark.gpu
+def test_oram_gpu():
+    # sqrt-ORAM and its position map at the reference tests' revealed checks
+    _run("test_oram", 600)
+
+
+@pytest.mark.gpu
 def test_convert_protocols_gpu():
     _run("test_convert", 600)
 

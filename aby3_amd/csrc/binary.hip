@@ -280,6 +280,129 @@ __global__ void __launch_bounds__(256) k_bits_to_wires_tiled(const i64* __restri
     }
 }
 
+// ---- register transposes: one thread per 64-row word ----------------------
+// A thread holds the 64 rows of one word (R[r] = row r) and transposes them
+// in registers (T[b] bit r = bit b of row r): six delta-swap stages over
+// row pairs (r, r + j), 32-bit halves independent for j < 32 (the stage mask
+// never takes a bit across the half boundary). About 25 VALU ops per row and
+// no LDS or cross-lane traffic, so the bit-slicing passes run at the rate of
+// their HBM streams: row loads / stores are 512 contiguous bytes per thread
+// (16 B per lane-instruction), wire-word stores / loads 512 B per wave
+// instruction (64 consecutive words of one wire).
+__device__ __forceinline__ void transpose64_regs(u64 (&R)[64]) {
+#pragma unroll
+    for (int r = 0; r < 32; ++r) {  // j = 32: swap hi(R[r]) with lo(R[r + 32])
+        const u32 a_hi = (u32)(R[r] >> 32), b_lo = (u32)R[r + 32];
+        R[r] = (R[r] & 0xffffffffull) | ((u64)b_lo << 32);
+        R[r + 32] = (R[r + 32] & 0xffffffff00000000ull) | a_hi;
+    }
+    constexpr u32 kM[5] = {0x0000ffffu, 0x00ff00ffu, 0x0f0f0f0fu, 0x33333333u, 0x55555555u};
+#pragma unroll
+    for (int st = 0; st < 5; ++st) {
+        const int j = 16 >> st;
+        const u32 m = kM[st];
+#pragma unroll
+        for (int r = 0; r < 64; ++r) {
+            if (r & j) continue;
+            u32 al = (u32)R[r], ah = (u32)(R[r] >> 32);
+            u32 bl = (u32)R[r + j], bh = (u32)(R[r + j] >> 32);
+            const u32 tl = ((al >> j) ^ bl) & m, th = ((ah >> j) ^ bh) & m;
+            bl ^= tl;
+            bh ^= th;
+            al ^= tl << j;
+            ah ^= th << j;
+            R[r] = ((u64)ah << 32) | al;
+            R[r + j] = ((u64)bh << 32) | bl;
+        }
+    }
+}
+
+// 64 rows of one 64-bit column -> R (rows past `rows` read as zero); a
+// contiguous column (cols64 == 1) loads 16 B per lane-instruction
+template <class F>
+__device__ __forceinline__ void load_rows(u64 (&R)[64], u64 r0, u64 rows, u64 cols64, u64 c, F&& at) {
+    if (cols64 == 1 && r0 + 64 <= rows) {
+#pragma unroll
+        for (int k = 0; k < 64; k += 2) {
+            const u64x2 v = at.pair(r0 + k);
+            R[k] = v.x;
+            R[k + 1] = v.y;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 64; ++k) R[k] = (r0 + k < rows) ? at.one((r0 + k) * cols64 + c) : 0;
+    }
+}
+
+struct RowsOf {
+    const u64* p;
+    __device__ __forceinline__ u64x2 pair(u64 r) const { return *reinterpret_cast<const u64x2*>(p + r); }
+    __device__ __forceinline__ u64 one(u64 i) const { return p[i]; }
+};
+
+// bits -> wires, both shares (blockIdx.y = share), a thread per (word, column)
+__global__ void __launch_bounds__(64) k_b2w_regs(const i64* __restrict__ in, u64 rows, u64 cols64, u32 nbits,
+                                                 u64* __restrict__ wrows, u64 shareStride, u64 words) {
+    in += (u64)blockIdx.y * rows * cols64;
+    wrows += (u64)blockIdx.y * shareStride;
+    const u64 wpc = (words + 63) / 64;  // workgroups per column
+    const u64 c = blockIdx.x / wpc, w = (blockIdx.x % wpc) * 64 + threadIdx.x;
+    if (w >= words) return;
+    u64 R[64];
+    load_rows(R, w * 64, rows, cols64, c, RowsOf{(const u64*)in});
+    transpose64_regs(R);
+#pragma unroll
+    for (int b = 0; b < 64; ++b)
+        if (c * 64 + b < nbits) wrows[(c * 64 + b) * words + w] = R[b];
+}
+
+// wires -> bits, both shares (blockIdx.y = share), a thread per (word, column)
+__global__ void __launch_bounds__(64) k_w2b_regs(const u64* __restrict__ mem, u64 shareStride,
+                                                 const u32* __restrict__ wires, u32 nbits, u64 words,
+                                                 i64* __restrict__ out, u64 rows) {
+    const u64 cols = (nbits + 63) / 64;
+    mem += (u64)blockIdx.y * shareStride;
+    out += (u64)blockIdx.y * rows * cols;
+    const u64 rw = (rows + 63) / 64;
+    const u64 wpc = (rw + 63) / 64;
+    const u64 c = blockIdx.x / wpc, w = (blockIdx.x % wpc) * 64 + threadIdx.x;
+    if (w >= rw) return;
+    u64 R[64];
+#pragma unroll
+    for (int b = 0; b < 64; ++b) R[b] = (c * 64 + b < nbits) ? mem[(u64)wires[c * 64 + b] * words + w] : 0;
+    transpose64_regs(R);
+    const u64 r0 = w * 64;
+    if (cols == 1 && r0 + 64 <= rows) {
+#pragma unroll
+        for (int k = 0; k < 64; k += 2) *reinterpret_cast<u64x2*>(out + r0 + k) = u64x2{R[k], R[k + 1]};
+    } else {
+#pragma unroll
+        for (int k = 0; k < 64; ++k)
+            if (r0 + k < rows) out[(r0 + k) * cols + c] = (i64)R[k];
+    }
+}
+
+// Variant selection for A/B runs: ABY3G_B2W=tiled keeps the LDS-tiled
+// butterfly kernels below for the plain / linear-combination transposes.
+inline bool b2w_regs() {
+    static const bool v = [] {
+        const char* e = getenv("ABY3G_B2W");
+        return !(e && e[0] == 't');
+    }();
+    return v;
+}
+// The mapped (gather / scatter) transposes keep the LDS-tiled kernels: their
+// rows are scattered, and a thread's 64 separate 8-byte row accesses measured
+// slower in the merge sort (C5) than the tiled kernels' wave-wide rows;
+// ABY3G_B2W_MAP=regs selects the register form.
+inline bool b2w_map_regs() {
+    static const bool v = [] {
+        const char* e = getenv("ABY3G_B2W_MAP");
+        return e && e[0] == 'r';
+    }();
+    return v;
+}
+
 // k_bits_to_wires_tiled over computed values: blockIdx.y = source
 struct WireSrcs {
     aby3g_wire_src s[ABY3G_WIRE_SRC_MAX];
@@ -318,6 +441,63 @@ __global__ void __launch_bounds__(256) k_bits_to_wires_lin(WireSrcs ws, u64 rows
         const u64 bit = c * 64 + b;
         if (bit < src.nbits && w0 + wl < words) src.wire_rows[bit * words + w0 + wl] = tile[b * kTilePitch + wl];
     }
+}
+
+// k_bits_to_wires_lin with register transposes. The source descriptor is
+// copied out of the kernarg array first and the copy-out is stored only after
+// every term load: a store through copy_out between loads would force the
+// compiler (which cannot rule out aliasing) to serialise the row loads.
+__global__ void __launch_bounds__(64) k_b2w_lin_regs(WireSrcs ws, u64 rows, u64 words) {
+    const aby3g_wire_src src = ws.s[blockIdx.y];
+    const u64 wpc = (words + 63) / 64;
+    const u64 c = blockIdx.x / wpc, w = (blockIdx.x % wpc) * 64 + threadIdx.x;
+    if (c * 64 >= src.nbits || w >= words) return;
+    const u64 r0 = w * 64;
+    const bool contig = src.cols64 == 1 && r0 + 64 <= rows;
+    u64 R[64];
+#pragma unroll
+    for (int k = 0; k < 64; ++k) R[k] = 0;
+    bool any = false;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const u64* __restrict__ p = (const u64*)src.term[t];
+        if (!p) continue;
+        any = true;
+        const u64 cf = (u64)src.coef[t];
+        if (contig) {
+#pragma unroll
+            for (int k = 0; k < 64; k += 2) {
+                const u64x2 x = *reinterpret_cast<const u64x2*>(p + r0 + k);
+                R[k] += cf * x.x;
+                R[k + 1] += cf * x.y;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 64; ++k)
+                if (r0 + k < rows) R[k] += cf * p[(r0 + k) * src.cols64 + c];
+        }
+    }
+    if (any) {
+        if (src.copy_out) {
+            i64* __restrict__ o = src.copy_out;
+            if (contig) {
+#pragma unroll
+                for (int k = 0; k < 64; k += 2) *reinterpret_cast<u64x2*>(o + r0 + k) = u64x2{R[k], R[k + 1]};
+            } else {
+#pragma unroll
+                for (int k = 0; k < 64; ++k)
+                    if (r0 + k < rows) o[(r0 + k) * src.cols64 + c] = (i64)R[k];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 64; ++k)
+            if (r0 + k < rows) R[k] += (u64)src.constant;  // padded rows stay zero
+    }
+    transpose64_regs(R);
+    u64* __restrict__ out = src.wire_rows;
+#pragma unroll
+    for (int b = 0; b < 64; ++b)
+        if (c * 64 + b < src.nbits) out[(c * 64 + b) * words + w] = R[b];
 }
 
 __global__ void __launch_bounds__(256) k_wires_to_bits_tiled(const u64* __restrict__ mem, u64 shareStride,
@@ -442,6 +622,56 @@ __global__ void __launch_bounds__(256) k_wires_to_bits_map(const u64* __restrict
     }
 }
 
+// the mapped transposes with register transposes (one thread per word)
+__global__ void __launch_bounds__(64) k_b2w_map_regs(const i64* __restrict__ in, u64 inRows, u64 cols64, u32 nbits,
+                                                     aby3g_rowmap map, u64 rows, u64* __restrict__ wrows,
+                                                     u64 shareStride, u64 words) {
+    in += (u64)blockIdx.y * inRows * cols64;
+    wrows += (u64)blockIdx.y * shareStride;
+    const u64 wpc = (words + 63) / 64;
+    const u64 c = blockIdx.x / wpc, w = (blockIdx.x % wpc) * 64 + threadIdx.x;
+    if (w >= words) return;
+    u64 R[64];
+#pragma unroll
+    for (int k = 0; k < 64; ++k) {
+        const u64 r = w * 64 + k;
+        u64 v = 0;
+        if (r < rows) {
+            const u64 src = map_row(map, r);
+            if (src < inRows) v = (u64)in[src * cols64 + c];
+        }
+        R[k] = v;
+    }
+    transpose64_regs(R);
+#pragma unroll
+    for (int b = 0; b < 64; ++b)
+        if (c * 64 + b < nbits) wrows[(c * 64 + b) * words + w] = R[b];
+}
+
+__global__ void __launch_bounds__(64) k_w2b_map_regs(const u64* __restrict__ mem, u64 shareStride,
+                                                     const u32* __restrict__ wires, u32 nbits, u64 words,
+                                                     i64* __restrict__ out, u64 outRows, aby3g_rowmap map, u64 rows) {
+    const u64 cols = (nbits + 63) / 64;
+    mem += (u64)blockIdx.y * shareStride;
+    out += (u64)blockIdx.y * outRows * cols;
+    const u64 rw = (rows + 63) / 64;
+    const u64 wpc = (rw + 63) / 64;
+    const u64 c = blockIdx.x / wpc, w = (blockIdx.x % wpc) * 64 + threadIdx.x;
+    if (w >= rw) return;
+    u64 R[64];
+#pragma unroll
+    for (int b = 0; b < 64; ++b) R[b] = (c * 64 + b < nbits) ? mem[(u64)wires[c * 64 + b] * words + w] : 0;
+    transpose64_regs(R);
+#pragma unroll
+    for (int k = 0; k < 64; ++k) {
+        const u64 row = w * 64 + k;
+        if (row < rows) {
+            const u64 dst = map_row(map, row);
+            if (dst < outRows) out[dst * cols + c] = (i64)R[k];
+        }
+    }
+}
+
 // Largest row an affine map reaches over p < rows (strides are unsigned, so
 // the maximum is at the last element of the last or the next-to-last rep).
 static u64 affine_max_row(const aby3g_rowmap& m, u64 rows) {
@@ -535,6 +765,12 @@ int aby3g_bits_to_wires2(const int64_t* in, uint64_t rows, uint64_t cols64, uint
         ABY3G_REQUIRE(nbits <= cols64 * 64, "nbits exceeds input columns");
         ABY3G_REQUIRE(words * 64 >= rows, "words too small for rows");
         if (!nbits || !words) return;
+        if (b2w_regs()) {
+            const u64 wgs = ((words + 63) / 64) * ((nbits + 63) / 64);
+            launch(PROBE_OTHER, k_b2w_regs, dim3((u32)wgs, 2), dim3(64), 0, S(stream), in, rows, cols64, nbits,
+                   wire_rows, share_stride, words);
+            return;
+        }
         const u64 tiles = ((words + kTileWords - 1) / kTileWords) * ((nbits + 63) / 64);
         launch(PROBE_OTHER, k_bits_to_wires_tiled, dim3((u32)tiles, 2), dim3(256), 0, S(stream), in, rows, cols64,
                nbits, wire_rows, share_stride, words);
@@ -556,6 +792,12 @@ int aby3g_bits_to_wires_lin(const aby3g_wire_src* srcs, uint32_t nsrc, uint64_t 
             cols = std::max<u64>(cols, (srcs[k].nbits + 63) / 64);
         }
         if (!cols) return;
+        if (b2w_regs()) {
+            const u64 wgs = ((words + 63) / 64) * cols;
+            launch(PROBE_OTHER, k_b2w_lin_regs, dim3((u32)wgs, nsrc), dim3(64), 0, S(stream), ws, (u64)rows,
+                   (u64)words);
+            return;
+        }
         const u64 tiles = ((words + kTileWords - 1) / kTileWords) * cols;
         launch(PROBE_OTHER, k_bits_to_wires_lin, dim3((u32)tiles, nsrc), dim3(256), 0, S(stream), ws, (u64)rows,
                (u64)words);
@@ -572,6 +814,12 @@ int aby3g_wires_to_bits2(const uint64_t* mem, uint64_t share_stride, const uint3
     return guarded([&] {
         ABY3G_REQUIRE(words * 64 >= rows, "words too small for rows");
         if (!nbits || !rows) return;
+        if (b2w_regs()) {
+            const u64 wgs = (((rows + 63) / 64 + 63) / 64) * ((nbits + 63) / 64);
+            launch(PROBE_OTHER, k_w2b_regs, dim3((u32)wgs, 2), dim3(64), 0, S(stream), mem, (u64)share_stride, wires,
+                   nbits, (u64)words, out, (u64)rows);
+            return;
+        }
         const u64 tiles = (((rows + 63) / 64 + kTileWords - 1) / kTileWords) * ((nbits + 63) / 64);
         launch(PROBE_OTHER, k_wires_to_bits_tiled, dim3((u32)tiles, 2), dim3(256), 0, S(stream), mem, share_stride,
                wires, nbits, words, out, rows);
@@ -586,6 +834,12 @@ int aby3g_bits_to_wires_map(const int64_t* in, uint64_t in_rows, uint64_t cols64
         ABY3G_REQUIRE(words * 64 >= rows, "words too small for rows");
         check_map(map, rows, in_rows);
         if (!nbits || !words) return;
+        if (b2w_map_regs()) {
+            const u64 wgs = ((words + 63) / 64) * ((nbits + 63) / 64);
+            launch(PROBE_OTHER, k_b2w_map_regs, dim3((u32)wgs, 2), dim3(64), 0, S(stream), in, (u64)in_rows,
+                   (u64)cols64, nbits, *map, (u64)rows, wire_rows, (u64)share_stride, (u64)words);
+            return;
+        }
         const u64 tiles = ((words + kTileWords - 1) / kTileWords) * ((nbits + 63) / 64);
         launch(PROBE_OTHER, k_bits_to_wires_map, dim3((u32)tiles, 2), dim3(256), 0, S(stream), in, (u64)in_rows,
                (u64)cols64, nbits, *map, (u64)rows, wire_rows, (u64)share_stride, (u64)words);
@@ -599,6 +853,12 @@ int aby3g_wires_to_bits_map(const uint64_t* mem, uint64_t share_stride, const ui
         ABY3G_REQUIRE(words * 64 >= rows, "words too small for rows");
         check_map(map, rows, out_rows);
         if (!nbits || !rows) return;
+        if (b2w_map_regs()) {
+            const u64 wgs = (((rows + 63) / 64 + 63) / 64) * ((nbits + 63) / 64);
+            launch(PROBE_OTHER, k_w2b_map_regs, dim3((u32)wgs, 2), dim3(64), 0, S(stream), mem, (u64)share_stride,
+                   wires, nbits, (u64)words, out, (u64)out_rows, *map, (u64)rows);
+            return;
+        }
         const u64 tiles = (((rows + 63) / 64 + kTileWords - 1) / kTileWords) * ((nbits + 63) / 64);
         launch(PROBE_OTHER, k_wires_to_bits_map, dim3((u32)tiles, 2), dim3(256), 0, S(stream), mem,
                (u64)share_stride, wires, nbits, (u64)words, out, (u64)out_rows, *map, (u64)rows);

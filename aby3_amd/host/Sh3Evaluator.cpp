@@ -137,11 +137,12 @@ Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, const si64Matrix& A, const si64Matri
                 std::memcpy(ts.prev_seed, mShareGen.mPrevSeed.data(), 16);
                 ts.next_off = mShareGen.takeNext(8 * n);
                 ts.prev_off = mShareGen.takePrev(8 * n);
-                // The truncation pair's AES-CTR runs inside the product's own
-                // passes: in the element-wise / small-GEMM epilogue, or, for a
-                // share GEMM, in the launch that splits the operands into digits
-                // (HBM-bound; the AES workgroups share its CUs), with z =
-                // product - r in the GEMM's epilogue or slab-reducing pass.
+                // The truncation pair's AES-CTR runs in the product's epilogue
+                // pass (k_finish_trunc): the element-wise / small-GEMM epilogue,
+                // or, after a share GEMM, the pass that reads its product (or
+                // reduces its split-K slabs) and writes z = product - R, RT.
+                // (Drawing the pair first on the auxiliary stream, with the
+                // GEMM's epilogue subtracting R, measured slower for C2.)
                 GPU_CALL(aby3g_mul_trunc_local((int)mode, A.data(), B.data(), M, K, N, (unsigned)shift, &ts,
                                                z->as<i64>(), C.data(), ws, wsBytes, g.stream()));
             }

@@ -61,6 +61,13 @@ class RowMap(ctypes.Structure):
                 ("rep_stride", c_uint64), ("idx", c_void_p)]
 
 
+class WireSrc(ctypes.Structure):
+    """aby3g_wire_src: one source of aby3g_bits_to_wires_lin."""
+    _fields_ = [("term", ctypes.POINTER(ctypes.c_int64) * 4), ("coef", ctypes.c_int64 * 4),
+                ("constant", ctypes.c_int64), ("cols64", c_uint64), ("nbits", c_uint32),
+                ("wire_rows", ctypes.POINTER(c_uint64)), ("copy_out", ctypes.POINTER(ctypes.c_int64))]
+
+
 def key16(b: bytes):
     assert len(b) == 16
     return (ctypes.c_uint8 * 16)(*b)

@@ -208,10 +208,11 @@ def _bits_ref(x, nbits, words):
     rows = x.shape[0]
     out = np.zeros((nbits, words), dtype=np.uint64)
     xu = x.view(np.uint64)
+    sh = np.arange(64, dtype=np.uint64)
     for b in range(nbits):
-        col = (xu[:, b // 64] >> np.uint64(b % 64)) & np.uint64(1)
-        for r in np.nonzero(col)[0]:
-            out[b, r // 64] |= np.uint64(1) << np.uint64(r % 64)
+        col = np.zeros(words * 64, dtype=np.uint64)
+        col[:rows] = (xu[:, b // 64] >> np.uint64(b % 64)) & np.uint64(1)
+        out[b] = np.bitwise_or.reduce(col.reshape(words, 64) << sh, axis=1)
     return out
 
 
@@ -234,7 +235,7 @@ def test_transposes(gpu, rows, nbits):
     assert np.array_equal(host(out).reshape(rows, cols), x)
 
 
-@pytest.mark.parametrize("rows,nbits", [(1, 1), (3000, 70)])
+@pytest.mark.parametrize("rows,nbits", [(1, 1), (3000, 70), (4096, 64), (70001, 64), (5000, 130)])
 def test_transposes_both_shares(gpu, rows, nbits):
     """bits_to_wires2 / wires_to_bits2 (both shares, engine memory layout)."""
     import torch
@@ -255,6 +256,38 @@ def test_transposes_both_shares(gpu, rows, nbits):
     out = empty(2 * rows * cols)
     gpu.wires_to_bits2(P(mem), wires * words, P(ids), nbits, words, P(out), rows, None)
     assert np.array_equal(host(out).reshape(2, rows, cols), x)
+
+
+@pytest.mark.parametrize("rows", [1, 4096, 70001])
+def test_bits_to_wires_lin(gpu, rows):
+    """bits_to_wires_lin: per source the wire rows of sum_t coef_t term_t + c
+    (zero wires for a source without terms) and the copy-out, against numpy."""
+    import torch
+
+    words = 32 * ((rows + 2047) // 2048)
+    t = [rnd(rows + k, rows) for k in range(3)]
+    dt = [dev(x) for x in t]
+    mem = dev(rnd(9, 3 * 64 * words))  # garbage: every source row must be written
+    cp = empty(rows)
+    Src = nt.WireSrc * 3
+    s = Src()
+    at = lambda k: ctypes.cast(mem.data_ptr() + 8 * k * 64 * words, ctypes.POINTER(ctypes.c_uint64))
+    i64p = lambda x: ctypes.cast(x.data_ptr(), ctypes.POINTER(ctypes.c_int64))
+    for k in range(3):
+        s[k].cols64, s[k].nbits, s[k].wire_rows = 1, 64, at(k)
+    s[0].term[0], s[0].term[1], s[0].coef[0], s[0].coef[1] = i64p(dt[0]), i64p(dt[1]), 3, -1
+    s[0].constant, s[0].copy_out = 1234567, i64p(cp)
+    s[2].term[2], s[2].coef[2], s[2].constant = i64p(dt[2]), 1, -5
+    gpu.bits_to_wires_lin(s, 3, rows, words, None)
+    m = host(mem).view(np.uint64).reshape(3, 64, words)
+    with np.errstate(over="ignore"):
+        v0 = (3 * t[0].view(np.uint64) - t[1].view(np.uint64))
+        e0 = (v0 + np.uint64(1234567)).view(np.int64).reshape(rows, 1)
+        e2 = (t[2].view(np.uint64) - np.uint64(5)).view(np.int64).reshape(rows, 1)
+    assert np.array_equal(host(cp).view(np.uint64), v0)
+    assert np.array_equal(m[0], _bits_ref(e0, 64, words))
+    assert not m[1].any()
+    assert np.array_equal(m[2], _bits_ref(e2, 64, words))
 
 
 def _map_rows(first, start, step, per_rep, rep_stride, n):

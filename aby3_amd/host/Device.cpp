@@ -81,6 +81,7 @@ Gpu::~Gpu() {
     aby3g_set_device(mDevice);
     aby3g_stream_sync(mStream);
     if (mAux) aby3g_stream_sync(mAux);
+    if (mDraw) aby3g_stream_sync(mDraw->s);  // draws into this party's buffers
     mAttach.clear();
     trim();
     {
@@ -93,6 +94,16 @@ Gpu::~Gpu() {
     if (mAux && !mAuxAliased) aby3g_stream_destroy(mAux);
     aby3g_stream_destroy(mStream);
     if (t_current == this) t_current = nullptr;
+}
+
+Gpu::SharedStream::SharedStream(int dev) : device(dev) {
+    GPU_CALL(aby3g_set_device(dev));
+    GPU_CALL(aby3g_stream_create(&s));
+}
+Gpu::SharedStream::~SharedStream() {
+    aby3g_set_device(device);
+    aby3g_stream_sync(s);
+    aby3g_stream_destroy(s);
 }
 
 void Gpu::bind() {

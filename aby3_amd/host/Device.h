@@ -61,6 +61,20 @@ public:
     void aliasAux();
     bool auxAliased() const { return mAuxAliased; }
 
+    // A stream shared by the co-located parties of one device, for work with
+    // no inputs of the party's stream that should overlap it (the binary
+    // engine's AND-mask draws): with three parties on a device it is the
+    // fourth stream, so every stream keeps a hardware queue of its own.
+    // Destroyed with the last Gpu holding it; null: such work goes to aux().
+    struct SharedStream {
+        aby3g_stream s = nullptr;
+        int device = 0;
+        explicit SharedStream(int device);
+        ~SharedStream();
+    };
+    void setDrawStream(std::shared_ptr<SharedStream> s) { mDraw = std::move(s); }
+    aby3g_stream drawStream() const { return mDraw ? mDraw->s : nullptr; }
+
     struct FreeBlock {
         void* ptr;
         std::vector<std::unique_ptr<Event>> fences;  // other streams' last uses
@@ -97,6 +111,7 @@ private:
     std::shared_ptr<Pool> mPool;
     std::mutex mAttachMu;
     std::map<u64, std::shared_ptr<void>> mAttach;
+    std::shared_ptr<SharedStream> mDraw;
 };
 
 // Owning device allocation from a party's pool (move-only). A buffer handed

@@ -416,6 +416,9 @@ struct Session {
     double hostEnqueueUs[3] = {0, 0, 0}, hostDrainUs[3] = {0, 0, 0}, hostRecvWaitUs[3] = {0, 0, 0};
     double hostApiUs[3] = {0, 0, 0}, hostApiCalls[3] = {0, 0, 0};
     bool colocated = false;  // two or more parties on one device
+    // co-located parties' shared draw stream per device (Gpu::SharedStream),
+    // created once every local party has made its own stream
+    std::map<int, std::shared_ptr<Gpu::SharedStream>> drawStreams;
 
     // Stream creation order. HIP maps streams onto GPU_MAX_HW_QUEUES hardware
     // queues in creation order, so with the three parties on one device the
@@ -439,6 +442,14 @@ struct Session {
         turnCv.notify_all();
     }
 
+    static bool drawStreamsOn() {
+        static const bool on = [] {
+            const char* e = getenv("ABY3G_DRAW_STREAM");  // 0: draws stay on the party's stream (A/B runs)
+            return !(e && e[0] == '0');
+        }();
+        return on;
+    }
+
     void worker(int i, int device, int probe) {
         PartyCtx p;
         u64 seen = 0;
@@ -454,6 +465,20 @@ struct Session {
                 if (colocated) GPU_CALL(aby3g_set_gemm_sharing(3));
                 p.rt.gpu().aux();
             });
+            // (only for parties sharing this process: one party per process
+            // with a second stream each put six queues on the device, measured
+            // 5x slower on C3)
+            if (colocated && locals.size() > 1 && drawStreamsOn()) {
+                std::shared_ptr<Gpu::SharedStream> ds;
+                {
+                    std::unique_lock<std::mutex> lk(turnMu);
+                    turnCv.wait(lk, [&] { return turnNext > locals.back(); });
+                    auto& slot = drawStreams[device];
+                    if (!slot) slot = std::make_shared<Gpu::SharedStream>(device);
+                    ds = slot;
+                }
+                p.rt.gpu().setDrawStream(ds);
+            }
             if (job->mlSeeds()) {
                 const MlSeeds ms = mlSeeds(i);
                 p.enc.init(i, ms.encPrev, ms.encNext);

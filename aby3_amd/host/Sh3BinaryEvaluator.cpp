@@ -76,15 +76,65 @@ void Sh3BinaryEvaluator::setCir(BetaCircuit* cir, u64 width, block prevSeed, blo
     const u64 memBytes = 2 * (u64)cir->mWireCount * mWords * 8;
     if (mMem.bytes() < memBytes || mMem.gpu() != &g) mMem.reset(g, memBytes ? memBytes : 8);
     // all AND masks of the circuit: z[k][w] = binary draw k*words + w, drawn on
-    // the auxiliary stream while the inputs are transposed on the main one
+    // another stream while the inputs are transposed on the main one
+    if (mZPending) waitZ();  // setCir again before evaluating: the old draw lands first
+    releaseZ();
     const u64 zWords = (u64)cir->mAndCount * mWords;
     if (zWords) {
-        if (mZ.bytes() < zWords * 8 || mZ.gpu() != &g) mZ.reset(g, zWords * 8);
-        g.forkAux();
+        mZStream = g.drawStream() ? g.drawStream() : g.aux();
+        const bool other = mZStream != g.stream();
+        mRing = std::static_pointer_cast<ZRing>(
+            g.attachment(0x2a02, [] { return std::static_pointer_cast<void>(std::make_shared<ZRing>()); }));
+        ZRing& r = *mRing;
+        int b = -1;
+        for (int k = 0; k < 2 && b < 0; ++k)
+            if (!r.busy[(r.next + k) % 2]) b = (r.next + k) % 2;
+        bool fresh = true;
+        if (b >= 0) {
+            r.next = (b + 1) % 2;
+            r.busy[b] = true;
+            mZSlot = b;
+            if (r.buf[b].bytes() < zWords * 8 || r.buf[b].gpu() != &g) {
+                r.buf[b].reset(g, zWords * 8);
+                r.recorded[b] = false;
+            }
+            fresh = !r.recorded[b];
+            if (!fresh && other) GPU_CALL(aby3g_stream_wait_event(mZStream, r.done[b]->get()));
+            mZPtr = r.buf[b].as<u64>();
+        } else {
+            // both ring buffers held by evaluations not yet evaluated
+            if (mZ.bytes() < zWords * 8 || mZ.gpu() != &g) mZ.reset(g, zWords * 8);
+            mZPtr = mZ.as<u64>();
+        }
+        if (fresh && other) {
+            // memory from the main stream's pool: the draws wait for the main stream
+            if (!mZFresh) mZFresh = std::make_unique<Event>();
+            mZFresh->record(g.stream());
+            GPU_CALL(aby3g_stream_wait_event(mZStream, mZFresh->get()));
+        }
         GPU_CALL(aby3g_share_draws(ABY3G_DRAW_BIN, mKeyPrev.data(), mKeyNext.data(), 0, zWords, nullptr,
-                                   mZ.as<i64>(), nullptr, g.aux()));
+                                   (i64*)mZPtr, nullptr, mZStream));
+        if (other) {
+            if (!mZEv) mZEv = std::make_unique<Event>();
+            mZEv->record(mZStream);
+        }
         mZPending = true;
     }
+}
+
+void Sh3BinaryEvaluator::waitZ() {
+    if (mZPending && mZEv && mZStream != mGpu->stream()) GPU_CALL(aby3g_stream_wait_event(mGpu->stream(), mZEv->get()));
+    mZPending = false;
+}
+
+void Sh3BinaryEvaluator::releaseZ() {
+    if (mZSlot < 0 || !mRing) return;
+    ZRing& r = *mRing;
+    if (!r.done[mZSlot]) r.done[mZSlot] = std::make_unique<Event>();
+    r.done[mZSlot]->record(mGpu->stream());
+    r.recorded[mZSlot] = true;
+    r.busy[mZSlot] = false;
+    mZSlot = -1;
 }
 
 void Sh3BinaryEvaluator::setInput(u64 i, const sbMatrix& in) {
@@ -266,17 +316,16 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
     const u32 nAnd = gatesHere ? mCir->mLevelAndCounts[mLevel] : 0;
     std::shared_ptr<DeviceBuffer> send;
     if (nAnd) send = std::make_shared<DeviceBuffer>(g, nAnd * rowBytes);
-    if (nb && mZPending) {
-        g.joinAux();
-        mZPending = false;
-    }
+    if (nb && mZPending) waitZ();
     if (nb || nUnpack) {
         const aby3g_gate* gl = nb ? mCur->gates + mCur->levelFirstGate[mLevel] : nullptr;
         const u32* be = nb ? mCur->batchEnds + mCur->levelBatchOffset[mLevel] : nullptr;
         GPU_CALL(aby3g_bin_level(gl, be, nb, recv ? recv->as<u64>() : nullptr, nUnpack ? mCur->outWires[mLevel - 1] : nullptr,
-                                 nUnpack, mMem.as<u64>(), W, mWords, mZ.as<u64>(), send ? send->as<u64>() : nullptr,
+                                 nUnpack, mMem.as<u64>(), W, mWords, mZPtr, send ? send->as<u64>() : nullptr,
                                  g.stream()));
     }
+    // the last level with gates has read its masks: the ring slot is free behind it
+    if (gatesHere && mLevel + 1 == mCir->mLevelCounts.size()) releaseZ();
     if (recv) recv->fence(g.stream());
     if (nAnd) {
         comm.mNext.asyncSendShared(send, nAnd * rowBytes, g);

@@ -23,11 +23,12 @@ public:
     Sh3BinaryEvaluator(const Sh3BinaryEvaluator&) = delete;
     Sh3BinaryEvaluator& operator=(const Sh3BinaryEvaluator&) = delete;
     ~Sh3BinaryEvaluator() {
-        // mZ returns to the main stream's pool behind its draw
-        if (mZPending && mGpu) try {
-                mGpu->joinAux();
-            } catch (...) {
-            }
+        // the masks' buffer is reused behind its draw
+        try {
+            if (mZPending && mGpu) waitZ();
+            releaseZ();
+        } catch (...) {
+        }
     }
     // consumes 16 bytes of the prev and next streams for the AND keys
     // (Sh3BinaryEvaluator.h:96-102)
@@ -66,6 +67,7 @@ public:
     u64 mRows = 0, mWords = 0, mLevel = 0;
     block mKeyPrev, mKeyNext;
     DeviceBuffer mMem, mZ;
+    u64* mZPtr = nullptr;   // the AND masks: a slot of the Gpu's z ring, or mZ
     RecvFuture mRecvFutr;   // previous level's AND shares (zero-copy: the sender's buffer)
     bool mZPending = false;  // z masks still being drawn on the auxiliary stream
 
@@ -86,6 +88,25 @@ private:
     std::shared_ptr<DevCircuit> mCur;
     Gpu* mGpu = nullptr;
     void upload(Gpu& g);
+    // The AND masks are drawn on the Gpu's draw stream when it has one (the
+    // co-located parties' shared fourth stream), else on aux(). Consecutive
+    // evaluations alternate between two mask buffers kept on the Gpu, so the
+    // draws of the next evaluation wait only for the last evaluation that
+    // used the same buffer (its done event), not for everything enqueued so
+    // far: their AES runs beside the previous evaluation's latency-bound
+    // levels instead of in front of the next one's.
+    struct ZRing {
+        DeviceBuffer buf[2];
+        std::unique_ptr<Event> done[2];
+        bool busy[2] = {false, false}, recorded[2] = {false, false};
+        int next = 0;
+    };
+    std::shared_ptr<ZRing> mRing;
+    int mZSlot = -1;
+    aby3g_stream mZStream = nullptr;     // the stream the masks are drawn on
+    std::unique_ptr<Event> mZEv, mZFresh; // draws done / main stream's position for fresh memory
+    void waitZ();      // main stream waits for the draws
+    void releaseZ();   // the ring slot is free once the main stream passes this point
 };
 
 // The two-input binary resharing of an arithmetic value x (BuildingBlocks.cpp

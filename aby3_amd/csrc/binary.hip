@@ -110,15 +110,20 @@ __device__ __forceinline__ bool gate_is_and(u32 t) {
     return t == ABY3G_GATE_AND || t == ABY3G_GATE_OR || t == ABY3G_GATE_NOR || t == ABY3G_GATE_NA_AND;
 }
 
-__device__ __forceinline__ void gate_load(const aby3g_gate& g, const u64* s0, const u64* s1, u64 words, u64 w,
-                                          const u64* __restrict__ z, GateOps& o) {
+// rr: the recv rows of the inputs' share 1 when they are the previous
+// level's AND outputs (~0u: read the engine memory), so that the gates need
+// not wait for the unpack of this launch
+__device__ __forceinline__ void gate_load(const aby3g_gate& g, uint2 rr, const u64* s0, const u64* s1,
+                                          const u64* __restrict__ recv, u64 words, u64 w, const u64* __restrict__ z,
+                                          GateOps& o) {
     // unary gates read in0 twice (in1 of an external gate list may be anything)
     const bool unary = g.type == ABY3G_GATE_COPY || g.type == ABY3G_GATE_INV;
     const u64 in1 = unary ? g.in0 : g.in1;
+    const u32 r1 = unary ? rr.x : rr.y;
     o.x0 = s0[g.in0 * words + w];
-    o.x1 = s1[g.in0 * words + w];
+    o.x1 = rr.x != ~0u ? recv[(u64)rr.x * words + w] : s1[g.in0 * words + w];
     o.y0 = s0[in1 * words + w];
-    o.y1 = s1[in1 * words + w];
+    o.y1 = r1 != ~0u ? recv[(u64)r1 * words + w] : s1[in1 * words + w];
     o.z = gate_is_and(g.type) ? z[(u64)g.z_row * words + w] : 0;
 }
 
@@ -157,8 +162,11 @@ __device__ __forceinline__ void gate_eval(const aby3g_gate& g, const GateOps& o,
 // G / (SLOTS * kLevelUnroll) dependent memory round trips -- the bound for the
 // few-workgroup launches of small row counts (LR: 256 rows, one workgroup).
 constexpr u32 kLevelUnroll = 4;
+// With rrows (per gate, see gate_load) no gate reads the wires this launch
+// unpacks, so the first batch starts without a barrier after the unpack.
 template <u32 SLOTS>
 __global__ void __launch_bounds__(SLOTS * 32) k_bin_level(const aby3g_gate* __restrict__ gates,
+                                                         const uint2* __restrict__ rrows,
                                                          const u32* __restrict__ batch_ends, u32 nbatches,
                                                          const u64* __restrict__ recv,
                                                          const u32* __restrict__ unpack_wires, u32 nunpack,
@@ -172,17 +180,21 @@ __global__ void __launch_bounds__(SLOTS * 32) k_bin_level(const aby3g_gate* __re
     for (u32 j = slot; j < nunpack; j += SLOTS) s1[(u64)unpack_wires[j] * words + w] = recv[(u64)j * words + w];
     u32 begin = 0;
     for (u32 b = 0; b < nbatches; ++b) {
-        __syncthreads();
+        if (b || !rrows) __syncthreads();
         const u32 end = batch_ends[b];
         for (u32 g0 = begin + slot; g0 < end; g0 += kLevelUnroll * SLOTS) {
             aby3g_gate g[kLevelUnroll];
+            uint2 rr[kLevelUnroll];
             GateOps o[kLevelUnroll];
 #pragma unroll
             for (u32 k = 0; k < kLevelUnroll; ++k)
-                if (g0 + k * SLOTS < end) g[k] = gates[g0 + k * SLOTS];
+                if (g0 + k * SLOTS < end) {
+                    g[k] = gates[g0 + k * SLOTS];
+                    rr[k] = rrows ? rrows[g0 + k * SLOTS] : make_uint2(~0u, ~0u);
+                }
 #pragma unroll
             for (u32 k = 0; k < kLevelUnroll; ++k)
-                if (g0 + k * SLOTS < end) gate_load(g[k], s0, s1, words, w, z, o[k]);
+                if (g0 + k * SLOTS < end) gate_load(g[k], rr[k], s0, s1, recv, words, w, z, o[k]);
 #pragma unroll
             for (u32 k = 0; k < kLevelUnroll; ++k)
                 if (g0 + k * SLOTS < end) gate_eval(g[k], o[k], s0, s1, words, w, sendbuf);
@@ -710,16 +722,26 @@ int aby3g_bin_gates(const aby3g_gate* gates, uint32_t ngates, uint64_t* mem, uin
 int aby3g_bin_level(const aby3g_gate* gates, const uint32_t* batch_ends, uint32_t nbatches, const uint64_t* recvbuf,
                     const uint32_t* unpack_wires, uint32_t nunpack, uint64_t* mem, uint64_t wires, uint64_t words,
                     const uint64_t* z, uint64_t* sendbuf, aby3g_stream stream) {
+    return aby3g_bin_level_rr(gates, nullptr, batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z,
+                              sendbuf, stream);
+}
+
+int aby3g_bin_level_rr(const aby3g_gate* gates, const uint32_t* recv_rows, const uint32_t* batch_ends,
+                       uint32_t nbatches, const uint64_t* recvbuf, const uint32_t* unpack_wires, uint32_t nunpack,
+                       uint64_t* mem, uint64_t wires, uint64_t words, const uint64_t* z, uint64_t* sendbuf,
+                       aby3g_stream stream) {
+    const uint2* rrows = reinterpret_cast<const uint2*>(recv_rows);
     return guarded([&] {
+        ABY3G_REQUIRE(!rrows || recvbuf, "recv_rows without a recv buffer");
         ABY3G_REQUIRE(words % kLevelWords == 0, "words must be padded to a multiple of 32 (2048 rows)");
         if ((!nbatches && !nunpack) || !words) return;
         const u32 wgs = (u32)(words / kLevelWords);
         // few workgroups (small row counts): 32 slots per workgroup for gate parallelism
         if (wgs < 128)
-            launch(PROBE_BINARY, k_bin_level<32>, dim3(wgs), dim3(32 * 32), 0, S(stream), gates, batch_ends,
+            launch(PROBE_BINARY, k_bin_level<32>, dim3(wgs), dim3(32 * 32), 0, S(stream), gates, rrows, batch_ends,
                    nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf);
         else
-            launch(PROBE_BINARY, k_bin_level<8>, dim3(wgs), dim3(8 * 32), 0, S(stream), gates, batch_ends, nbatches,
+            launch(PROBE_BINARY, k_bin_level<8>, dim3(wgs), dim3(8 * 32), 0, S(stream), gates, rrows, batch_ends, nbatches,
                    recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf);
     });
 }

@@ -1,5 +1,6 @@
 #include "Sh3BinaryEvaluator.h"
 #include <cstring>
+#include <map>
 
 namespace aby3 {
 
@@ -28,6 +29,33 @@ void Sh3BinaryEvaluator::upload(Gpu& g) {
             gs[i] = aby3g_gate{b.in0, b.in1, b.out, (u32)b.type, c.mBatchZRow[i], c.mBatchSendRow[i]};
         }
         const size_t oGates = put(gs.data(), gs.size() * sizeof(aby3g_gate));
+        // per gate, the recv row of each input that the previous level's AND
+        // outputs deliver (its share 1 is read from the received buffer)
+        std::vector<u32> rr(2 * gs.size(), ~0u);
+        {
+            size_t lg = 0, first = 0;  // level-list index / batch-order index of the level's first gate
+            std::map<u32, u32> prevAnd, curAnd;
+            for (size_t L = 0; L < c.mLevelCounts.size(); ++L) {
+                curAnd.clear();
+                for (u32 k = 0; k < c.mLevelCounts[L]; ++k) {
+                    const BetaGate& lgate = c.mLevelGates[lg + k];
+                    if (isAndType(lgate.type)) {
+                        const u32 row = (u32)curAnd.size();
+                        curAnd[lgate.out] = row;
+                    }
+                }
+                for (u32 k = 0; k < c.mLevelCounts[L]; ++k) {
+                    const BetaGate& b = c.mBatchGates[first + k];
+                    auto a0 = prevAnd.find(b.in0), a1 = prevAnd.find(b.in1);
+                    if (a0 != prevAnd.end()) rr[2 * (first + k)] = a0->second;
+                    if (a1 != prevAnd.end()) rr[2 * (first + k) + 1] = a1->second;
+                }
+                lg += c.mLevelCounts[L];
+                first += c.mLevelCounts[L];
+                prevAnd.swap(curAnd);
+            }
+        }
+        const size_t oRr = put(rr.data(), rr.size() * 4);
         std::vector<u32> ends;
         for (const auto& batches : c.mLevelBatches) {
             d->levelFirstGate.push_back(batches.empty() ? 0 : batches.front().begin);
@@ -55,6 +83,7 @@ void Sh3BinaryEvaluator::upload(Gpu& g) {
         if (!host.empty()) toDevice(d->blob.data(), host.data(), host.size(), g);
         u8* base = d->blob.as<u8>();
         d->gates = reinterpret_cast<const aby3g_gate*>(base + oGates);
+        d->recvRows = reinterpret_cast<const u32*>(base + oRr);
         d->batchEnds = reinterpret_cast<const u32*>(base + oEnds);
         for (size_t o : oLevel) d->outWires.push_back(reinterpret_cast<const u32*>(base + o));
         d->allOutputWires = reinterpret_cast<const u32*>(base + oOut);
@@ -320,9 +349,14 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
     if (nb || nUnpack) {
         const aby3g_gate* gl = nb ? mCur->gates + mCur->levelFirstGate[mLevel] : nullptr;
         const u32* be = nb ? mCur->batchEnds + mCur->levelBatchOffset[mLevel] : nullptr;
-        GPU_CALL(aby3g_bin_level(gl, be, nb, recv ? recv->as<u64>() : nullptr, nUnpack ? mCur->outWires[mLevel - 1] : nullptr,
-                                 nUnpack, mMem.as<u64>(), W, mWords, mZPtr, send ? send->as<u64>() : nullptr,
-                                 g.stream()));
+        static const bool useRr = [] {
+            const char* e = getenv("ABY3G_LEVEL_RR");  // 0: gates wait for the unpack (A/B runs)
+            return !(e && e[0] == '0');
+        }();
+        const u32* rr = (useRr && nb && recv) ? mCur->recvRows + 2 * (u64)mCur->levelFirstGate[mLevel] : nullptr;
+        GPU_CALL(aby3g_bin_level_rr(gl, rr, be, nb, recv ? recv->as<u64>() : nullptr,
+                                    nUnpack ? mCur->outWires[mLevel - 1] : nullptr, nUnpack, mMem.as<u64>(), W, mWords,
+                                    mZPtr, send ? send->as<u64>() : nullptr, g.stream()));
     }
     // the last level with gates has read its masks: the ring slot is free behind it
     if (gatesHere && mLevel + 1 == mCir->mLevelCounts.size()) releaseZ();

@@ -79,6 +79,7 @@ private:
     struct DevCircuit {
         DeviceBuffer blob;
         const aby3g_gate* gates = nullptr;
+        const u32* recvRows = nullptr;         // 2 per gate: recv row of in0 / in1 (aby3g_bin_level_rr)
         const u32* batchEnds = nullptr;        // relative to the level's first gate
         std::vector<u32> levelFirstGate, levelBatchOffset, levelBatches;
         std::vector<const u32*> outWires;      // per level

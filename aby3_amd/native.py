@@ -151,6 +151,8 @@ _SIGS = {
     "aby3g_bin_gates": (c_int, [c_void_p, c_uint32, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p]),
     "aby3g_bin_level": (c_int, [c_void_p, c_void_p, ctypes.c_uint32, c_void_p, c_void_p, ctypes.c_uint32, c_void_p,
                                 c_uint64, c_uint64, c_void_p, c_void_p, c_void_p]),
+    "aby3g_bin_level_rr": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_uint32, c_void_p, c_void_p, ctypes.c_uint32,
+                                   c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p]),
     "aby3g_bits_to_wires2": (c_int, [c_void_p, c_uint64, c_uint64, ctypes.c_uint32, c_void_p, c_uint64, c_uint64,
                                      c_void_p]),
     "aby3g_wires_to_bits2": (c_int, [c_void_p, c_uint64, c_void_p, ctypes.c_uint32, c_uint64, c_void_p, c_uint64,

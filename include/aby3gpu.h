@@ -345,6 +345,15 @@ int aby3g_bin_gates(const aby3g_gate* gates, uint32_t ngates, uint64_t* mem, uin
 int aby3g_bin_level(const aby3g_gate* gates, const uint32_t* batch_ends, uint32_t nbatches, const uint64_t* recvbuf,
                     const uint32_t* unpack_wires, uint32_t nunpack, uint64_t* mem, uint64_t wires, uint64_t words,
                     const uint64_t* z, uint64_t* sendbuf, aby3g_stream stream);
+/* aby3g_bin_level where the gates take share 1 of the previous level's AND
+ * outputs straight from recvbuf: recv_rows (device, 2 per gate, in gate
+ * order) holds the recvbuf row of in0 and in1 when that wire is unpacked by
+ * this launch, else 0xffffffff. The unpack still fills the engine memory
+ * for later levels, but the first batch no longer waits for it. */
+int aby3g_bin_level_rr(const aby3g_gate* gates, const uint32_t* recv_rows, const uint32_t* batch_ends,
+                       uint32_t nbatches, const uint64_t* recvbuf, const uint32_t* unpack_wires, uint32_t nunpack,
+                       uint64_t* mem, uint64_t wires, uint64_t words, const uint64_t* z, uint64_t* sendbuf,
+                       aby3g_stream stream);
 int aby3g_bin_unpack(const uint64_t* recvbuf, const uint32_t* out_wires, uint32_t n, uint64_t* mem, uint64_t wires,
                      uint64_t words, aby3g_stream stream);
 /* setInput (:200-276): bit-transpose a [rows][cols64] i64 share matrix into

@@ -474,6 +474,14 @@ def test_bin_level_matches_unpack_then_batches(gpu, words):
     gpu.bin_level(P(gdev), P(ends), len(batches), P(rd), P(uw), 3, P(m2), wires, words, P(zd), P(s2), None)
     assert np.array_equal(host(m1), host(m2))
     assert np.array_equal(host(s1)[:zrow * words], host(s2)[:zrow * words])
+    # aby3g_bin_level_rr: share 1 of the unpacked wires read from the recv rows
+    rows = {w: j for j, w in enumerate(unpack)}
+    rr = np.array([[rows.get(a, 0xFFFFFFFF), rows.get(b, 0xFFFFFFFF)] for a, b, _, _ in flat], dtype=np.uint32)
+    rrd = torch.from_numpy(rr.reshape(-1).view(np.int32).copy()).to("cuda")
+    m3, s3 = dev(mem.view(np.int64)), empty(4 * words)
+    gpu.bin_level_rr(P(gdev), P(rrd), P(ends), len(batches), P(rd), P(uw), 3, P(m3), wires, words, P(zd), P(s3), None)
+    assert np.array_equal(host(m1), host(m3))
+    assert np.array_equal(host(s1)[:zrow * words], host(s3)[:zrow * words])
 
 
 def test_lincomb_bitops(gpu):

@@ -228,7 +228,22 @@ void DeviceBuffer::reset(Gpu& gpu, size_t bytes) {
     mFences = std::make_unique<Fences>();  // created here: fence() may race from several consumer threads
 }
 
+std::shared_ptr<DeviceBuffer> DeviceBuffer::view(const std::shared_ptr<DeviceBuffer>& parent, size_t off,
+                                                 size_t bytes) {
+    if (!parent || off + bytes > parent->mBytes) throw std::runtime_error("DeviceBuffer::view out of range");
+    auto v = std::make_shared<DeviceBuffer>();
+    v->mGpu = parent->mGpu;
+    v->mPtr = static_cast<char*>(parent->mPtr) + off;
+    v->mBytes = bytes;
+    v->mParent = parent;
+    return v;
+}
+
 void DeviceBuffer::fence(aby3g_stream s) {
+    if (mParent) {
+        mParent->fence(s);
+        return;
+    }
     if (!mPtr) return;
     if (mPool) {
         // the owner's stream: the pool reuses blocks in that stream's order anyway
@@ -242,6 +257,13 @@ void DeviceBuffer::fence(aby3g_stream s) {
 }
 
 void DeviceBuffer::free() {
+    if (mParent) {
+        mParent.reset();
+        mPtr = nullptr;
+        mGpu = nullptr;
+        mBytes = 0;
+        return;
+    }
     if (mPtr && mPool) {
         std::vector<std::unique_ptr<Event>> fences;
         if (mFences) fences = std::move(mFences->events);

@@ -133,6 +133,7 @@ public:
             mPtr = o.mPtr;
             mBytes = o.mBytes;
             mFences = std::move(o.mFences);
+            mParent = std::move(o.mParent);
             o.mGpu = nullptr;
             o.mPtr = nullptr;
             o.mBytes = 0;
@@ -151,6 +152,10 @@ public:
     Gpu* gpu() const { return mGpu; }  // valid while the allocating Gpu lives
     // records "stream s is done with this buffer as of now" (thread-safe)
     void fence(aby3g_stream s);
+    // [off, off + bytes) of `parent` as a buffer of its own: keeps the parent
+    // alive, and its fences are the parent's (one fence after the last use
+    // of any view covers them all)
+    static std::shared_ptr<DeviceBuffer> view(const std::shared_ptr<DeviceBuffer>& parent, size_t off, size_t bytes);
 
 private:
     struct Fences {
@@ -162,6 +167,7 @@ private:
     void* mPtr = nullptr;
     size_t mBytes = 0;
     std::unique_ptr<Fences> mFences;
+    std::shared_ptr<DeviceBuffer> mParent;  // views only
 };
 
 // Convenience copies on the current Gpu's stream.

@@ -108,13 +108,17 @@ void Sh3BinaryEvaluator::setCir(BetaCircuit* cir, u64 width, block prevSeed, blo
     // another stream while the inputs are transposed on the main one
     if (mZPending) waitZ();  // setCir again before evaluating: the old draw lands first
     releaseZ();
+    mSendAll.reset();
+    mAndDone = 0;
     const u64 zWords = (u64)cir->mAndCount * mWords;
     if (zWords) {
         mZStream = g.drawStream() ? g.drawStream() : g.aux();
         const bool other = mZStream != g.stream();
-        mRing = std::static_pointer_cast<ZRing>(
+        auto ring = std::static_pointer_cast<ZRing>(
             g.attachment(0x2a02, [] { return std::static_pointer_cast<void>(std::make_shared<ZRing>()); }));
-        ZRing& r = *mRing;
+        mRing = ring;
+        ZRing& r = *ring;
+        r.stream = g.stream();
         int b = -1;
         for (int k = 0; k < 2 && b < 0; ++k)
             if (!r.busy[(r.next + k) % 2]) b = (r.next + k) % 2;
@@ -157,10 +161,14 @@ void Sh3BinaryEvaluator::waitZ() {
 }
 
 void Sh3BinaryEvaluator::releaseZ() {
-    if (mZSlot < 0 || !mRing) return;
-    ZRing& r = *mRing;
+    auto ring = mRing.lock();
+    if (mZSlot < 0 || !ring) {
+        mZSlot = -1;
+        return;
+    }
+    ZRing& r = *ring;
     if (!r.done[mZSlot]) r.done[mZSlot] = std::make_unique<Event>();
-    r.done[mZSlot]->record(mGpu->stream());
+    r.done[mZSlot]->record(r.stream);
     r.recorded[mZSlot] = true;
     r.busy[mZSlot] = false;
     mZSlot = -1;
@@ -343,8 +351,22 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
     const bool gatesHere = mLevel < mCir->mLevelCounts.size();
     const u32 nb = gatesHere ? mCur->levelBatches[mLevel] : 0;
     const u32 nAnd = gatesHere ? mCir->mLevelAndCounts[mLevel] : 0;
+    if (mLevel == 0 && mAndDone) {  // evaluated again after setCir: a fresh send buffer
+        mSendAll.reset();
+        mAndDone = 0;
+    }
+    static const bool sendAll = [] {
+        const char* e = getenv("ABY3G_SEND_ALL");  // 0: a buffer and a fence per level (A/B runs)
+        return !(e && e[0] == '0');
+    }();
     std::shared_ptr<DeviceBuffer> send;
-    if (nAnd) send = std::make_shared<DeviceBuffer>(g, nAnd * rowBytes);
+    if (nAnd && sendAll) {
+        if (!mSendAll) mSendAll = std::make_shared<DeviceBuffer>(g, (u64)mCir->mAndCount * rowBytes);
+        send = DeviceBuffer::view(mSendAll, mAndDone * rowBytes, nAnd * rowBytes);
+    } else if (nAnd) {
+        send = std::make_shared<DeviceBuffer>(g, nAnd * rowBytes);
+    }
+    mAndDone += nAnd;
     if (nb && mZPending) waitZ();
     if (nb || nUnpack) {
         const aby3g_gate* gl = nb ? mCur->gates + mCur->levelFirstGate[mLevel] : nullptr;
@@ -358,9 +380,13 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
                                     nUnpack ? mCur->outWires[mLevel - 1] : nullptr, nUnpack, mMem.as<u64>(), W, mWords,
                                     mZPtr, send ? send->as<u64>() : nullptr, g.stream()));
     }
-    // the last level with gates has read its masks: the ring slot is free behind it
-    if (gatesHere && mLevel + 1 == mCir->mLevelCounts.size()) releaseZ();
-    if (recv) recv->fence(g.stream());
+
+    if (recv) {
+        // views of one sender buffer: fenced after the last of them is read
+        bool last = true;
+        for (size_t L = mLevel; L < mCir->mLevelAndCounts.size() && last; ++L) last = mCir->mLevelAndCounts[L] == 0;
+        if (last || !sendAll) recv->fence(g.stream());
+    }
     if (nAnd) {
         comm.mNext.asyncSendShared(send, nAnd * rowBytes, g);
         mRecvFutr = comm.mPrev.asyncRecvShared(nAnd * rowBytes, g);

@@ -25,7 +25,8 @@ public:
     ~Sh3BinaryEvaluator() {
         // the masks' buffer is reused behind its draw
         try {
-            if (mZPending && mGpu) waitZ();
+            // (a ring slot whose Gpu is gone needs nothing: the ring went with it)
+            if (mZPending && mGpu && (mZSlot < 0 || !mRing.expired())) waitZ();
             releaseZ();
         } catch (...) {
         }
@@ -101,13 +102,21 @@ private:
         std::unique_ptr<Event> done[2];
         bool busy[2] = {false, false}, recorded[2] = {false, false};
         int next = 0;
+        aby3g_stream stream = nullptr;  // the owning party's main stream
     };
-    std::shared_ptr<ZRing> mRing;
+    std::weak_ptr<ZRing> mRing;  // owned by the Gpu (attachment): gone with it
+    // one send buffer per evaluation, a view of it per level: one pool
+    // allocation per evaluation, and the receiver fences once, after its
+    // last level, instead of per level
+    std::shared_ptr<DeviceBuffer> mSendAll;
+    u64 mAndDone = 0;  // AND outputs of the levels already run (their rows in mSendAll)
     int mZSlot = -1;
     aby3g_stream mZStream = nullptr;     // the stream the masks are drawn on
     std::unique_ptr<Event> mZEv, mZFresh; // draws done / main stream's position for fresh memory
     void waitZ();      // main stream waits for the draws
-    void releaseZ();   // the ring slot is free once the main stream passes this point
+    // the ring slot is free once the main stream passes this point (at the
+    // next setCir or destruction: an evaluation may be re-run on its masks)
+    void releaseZ();
 };
 
 // The two-input binary resharing of an arithmetic value x (BuildingBlocks.cpp

@@ -41,6 +41,9 @@ PEAK_INT8_TOPS = 256 * 4 * 2048 * 2.4e9 / 1e12  # 256 CU x 4 SIMD x 2048 int8 op
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec
 
 
+# timed LR iterations (host-API bound, so a longer sample for a stable figure)
+LR_ITERS = 300
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -270,16 +273,16 @@ def extras(args, nt, dev, world, pg):
     whole odd-even merge sort of 2^20 keys), each checked."""
     res = {}
     with nt.Session(nt.JOB_LR, [args.lr_rows, 128, 256, 16, 11], devices=(dev,) * 3, probe=False) as s:
-        s.run(5)
-        dt = timed(s, 50, pg)
+        s.run(20)
+        dt = timed(s, LR_ITERS, pg)
         linfo = s.info()
         if not s.check():
             raise SystemExit("bench: LR model differs from the plaintext fixed-point restatement")
         res["lr_iteration"] = {
             "workload": f"SGD_Logistic iteration, {args.lr_rows}x128, batch 256, D16, lr 2^-11 (sigmoid piecewise)",
-            "ms_per_iteration": dt / 50 * 1e3,
-            "iterations_per_s": world * 50 / dt,
-            "local_compute_fraction": local_fraction(linfo, dt / 50),
+            "ms_per_iteration": dt / LR_ITERS * 1e3,
+            "iterations_per_s": world * LR_ITERS / dt,
+            "local_compute_fraction": local_fraction(linfo, dt / LR_ITERS),
         }
         if world == 1 and not args.no_cpu_baseline:
             progress("C4 CPU baseline")
@@ -289,7 +292,7 @@ def extras(args, nt, dev, world, pg):
                 "sample": "200 iterations of the oracle's SGD_Logistic restatement (65536x128 dataset, batch 256, "
                           "D16, aB 11), the three parties simulated in sequence on one thread, no network",
             }
-            res["lr_iteration"]["speedup_vs_cpu_baseline"] = cpu_ms / (dt / 50 * 1e3)
+            res["lr_iteration"]["speedup_vs_cpu_baseline"] = cpu_ms / (dt / LR_ITERS * 1e3)
     with nt.Session(nt.JOB_SORT, [1 << 20], devices=(dev,) * 3, probe=False) as s:
         s.run(1)
         reps = 2

@@ -296,6 +296,62 @@ static void replicatedInput() {
     for (u64 i = 0; i < rows; ++i) check(revealed[i] == (a(i, 0) & c(0, 0)), "a & replicated c");
 }
 
+// Several evaluators of one party alive at once: three setCir calls before
+// any evaluation (the third finds both buffers of the Gpu's mask ring held and
+// draws into its own), evaluated in order, the first one evaluated twice on
+// its masks. Every party's output shares must equal those of the same calls
+// made one evaluator at a time (same keys, same messages, only the
+// scheduling and the mask buffers differ).
+static void interleavedEvaluators() {
+    const u64 rows = 5000;
+    i64Matrix a = randMat(rows, 1, 91), b = randMat(rows, 1, 92);
+    using Make = BetaCircuit* (CircuitLibrary::*)(u64);
+    const Make makes[3] = {&CircuitLibrary::int_int_add, &CircuitLibrary::int_comp_helper, &CircuitLibrary::int_eq};
+    // [pattern][party][call] -> both shares of output 0
+    std::vector<std::vector<i64>> got[2][3];
+    for (int pattern = 0; pattern < 2; ++pattern)
+        run3([&](harness::Party& p) {
+            sbMatrix A(rows, 64), B(rows, 64);
+            if (p.idx == 0) {
+                p.enc.localBinMatrix(p.rt, a, A).get();
+                p.enc.localBinMatrix(p.rt, b, B).get();
+            } else {
+                p.enc.remoteBinMatrix(p.rt, A).get();
+                p.enc.remoteBinMatrix(p.rt, B).get();
+            }
+            CircuitLibrary lib;
+            Sh3BinaryEvaluator eng[3];
+            sbMatrix out[4];
+            auto run = [&](int k, sbMatrix& o) {
+                eng[k].setInput(0, A);
+                eng[k].setInput(1, B);
+                eng[k].asyncEvaluate(p.rt.noDependencies()).then([&](Sh3Task&) { eng[k].getOutput(0, o); }).get();
+            };
+            if (pattern == 0) {
+                for (int k = 0; k < 3; ++k) {
+                    eng[k].setCir((lib.*makes[k])(64), rows, p.eval.mShareGen);
+                    run(k, out[k]);
+                    if (k == 0) run(0, out[3]);
+                }
+            } else {
+                for (int k = 0; k < 3; ++k) eng[k].setCir((lib.*makes[k])(64), rows, p.eval.mShareGen);
+                run(0, out[0]);
+                run(0, out[3]);
+                run(1, out[1]);
+                run(2, out[2]);
+            }
+            for (auto& o : out) {
+                got[pattern][p.idx].push_back(o.shareToHost(0));
+                got[pattern][p.idx].push_back(o.shareToHost(1));
+            }
+        });
+    for (int i = 0; i < 3; ++i) {
+        check(got[0][i].size() == 8 && got[1][i].size() == 8, "interleaved: outputs collected");
+        for (size_t k = 0; k < got[0][i].size(); ++k)
+            check(got[0][i][k] == got[1][i][k], "interleaved evaluators: shares equal to one-at-a-time evaluation");
+    }
+}
+
 int main() {
     auto msb = [](u64 a, u64 b) { return (a + b) >> 63; };
     test("bin_msb_64_rows256 (Sh3_BinaryEngine_add_msb_test)",
@@ -328,6 +384,7 @@ int main() {
     test("bool_basic_16 (BoolTest.cpp)", boolBasic16);
     test("arith_compare_16 (Test.cpp gt/ge/eq/mul_ab)", arithCompare16);
     test("cipher_gt_parity_1000", [] { fetchMsbParity(1000); });
+    test("interleaved_evaluators (mask ring, re-evaluation)", interleavedEvaluators);
     test("piecewise_sigmoid_256_D16", [] { piecewiseParity(256, 16); });
     test("setReplicatedInput_and_300", replicatedInput);
     test("odd_even_merge_2x8 (SortTest.cpp)", [] { mergeTest({8, 8}, 1); });

@@ -403,17 +403,11 @@ inline bool b2w_regs() {
     }();
     return v;
 }
-// The mapped (gather / scatter) transposes keep the LDS-tiled kernels: their
-// rows are scattered, and a thread's 64 separate 8-byte row accesses measured
-// slower in the merge sort (C5) than the tiled kernels' wave-wide rows;
-// ABY3G_B2W_MAP=regs selects the register form.
-inline bool b2w_map_regs() {
-    static const bool v = [] {
-        const char* e = getenv("ABY3G_B2W_MAP");
-        return e && e[0] == 'r';
-    }();
-    return v;
-}
+// The mapped (gather / scatter) transposes keep the LDS-tiled kernels below:
+// their rows are scattered, and both register forms measured slower on C5 --
+// 64 separate 8-byte row accesses per thread (118-121 vs 103 ms), and rows
+// gathered wave-wide into an LDS stage then transposed per thread (101 vs
+// 88-90 ms: 194 VGPRs leave too few waves to hide the gathers).
 
 // k_bits_to_wires_tiled over computed values: blockIdx.y = source
 struct WireSrcs {
@@ -634,56 +628,6 @@ __global__ void __launch_bounds__(256) k_wires_to_bits_map(const u64* __restrict
     }
 }
 
-// the mapped transposes with register transposes (one thread per word)
-__global__ void __launch_bounds__(64) k_b2w_map_regs(const i64* __restrict__ in, u64 inRows, u64 cols64, u32 nbits,
-                                                     aby3g_rowmap map, u64 rows, u64* __restrict__ wrows,
-                                                     u64 shareStride, u64 words) {
-    in += (u64)blockIdx.y * inRows * cols64;
-    wrows += (u64)blockIdx.y * shareStride;
-    const u64 wpc = (words + 63) / 64;
-    const u64 c = blockIdx.x / wpc, w = (blockIdx.x % wpc) * 64 + threadIdx.x;
-    if (w >= words) return;
-    u64 R[64];
-#pragma unroll
-    for (int k = 0; k < 64; ++k) {
-        const u64 r = w * 64 + k;
-        u64 v = 0;
-        if (r < rows) {
-            const u64 src = map_row(map, r);
-            if (src < inRows) v = (u64)in[src * cols64 + c];
-        }
-        R[k] = v;
-    }
-    transpose64_regs(R);
-#pragma unroll
-    for (int b = 0; b < 64; ++b)
-        if (c * 64 + b < nbits) wrows[(c * 64 + b) * words + w] = R[b];
-}
-
-__global__ void __launch_bounds__(64) k_w2b_map_regs(const u64* __restrict__ mem, u64 shareStride,
-                                                     const u32* __restrict__ wires, u32 nbits, u64 words,
-                                                     i64* __restrict__ out, u64 outRows, aby3g_rowmap map, u64 rows) {
-    const u64 cols = (nbits + 63) / 64;
-    mem += (u64)blockIdx.y * shareStride;
-    out += (u64)blockIdx.y * outRows * cols;
-    const u64 rw = (rows + 63) / 64;
-    const u64 wpc = (rw + 63) / 64;
-    const u64 c = blockIdx.x / wpc, w = (blockIdx.x % wpc) * 64 + threadIdx.x;
-    if (w >= rw) return;
-    u64 R[64];
-#pragma unroll
-    for (int b = 0; b < 64; ++b) R[b] = (c * 64 + b < nbits) ? mem[(u64)wires[c * 64 + b] * words + w] : 0;
-    transpose64_regs(R);
-#pragma unroll
-    for (int k = 0; k < 64; ++k) {
-        const u64 row = w * 64 + k;
-        if (row < rows) {
-            const u64 dst = map_row(map, row);
-            if (dst < outRows) out[dst * cols + c] = (i64)R[k];
-        }
-    }
-}
-
 // Largest row an affine map reaches over p < rows (strides are unsigned, so
 // the maximum is at the last element of the last or the next-to-last rep).
 static u64 affine_max_row(const aby3g_rowmap& m, u64 rows) {
@@ -856,12 +800,6 @@ int aby3g_bits_to_wires_map(const int64_t* in, uint64_t in_rows, uint64_t cols64
         ABY3G_REQUIRE(words * 64 >= rows, "words too small for rows");
         check_map(map, rows, in_rows);
         if (!nbits || !words) return;
-        if (b2w_map_regs()) {
-            const u64 wgs = ((words + 63) / 64) * ((nbits + 63) / 64);
-            launch(PROBE_OTHER, k_b2w_map_regs, dim3((u32)wgs, 2), dim3(64), 0, S(stream), in, (u64)in_rows,
-                   (u64)cols64, nbits, *map, (u64)rows, wire_rows, (u64)share_stride, (u64)words);
-            return;
-        }
         const u64 tiles = ((words + kTileWords - 1) / kTileWords) * ((nbits + 63) / 64);
         launch(PROBE_OTHER, k_bits_to_wires_map, dim3((u32)tiles, 2), dim3(256), 0, S(stream), in, (u64)in_rows,
                (u64)cols64, nbits, *map, (u64)rows, wire_rows, (u64)share_stride, (u64)words);
@@ -875,12 +813,6 @@ int aby3g_wires_to_bits_map(const uint64_t* mem, uint64_t share_stride, const ui
         ABY3G_REQUIRE(words * 64 >= rows, "words too small for rows");
         check_map(map, rows, out_rows);
         if (!nbits || !rows) return;
-        if (b2w_map_regs()) {
-            const u64 wgs = (((rows + 63) / 64 + 63) / 64) * ((nbits + 63) / 64);
-            launch(PROBE_OTHER, k_w2b_map_regs, dim3((u32)wgs, 2), dim3(64), 0, S(stream), mem, (u64)share_stride,
-                   wires, nbits, (u64)words, out, (u64)out_rows, *map, (u64)rows);
-            return;
-        }
         const u64 tiles = (((rows + 63) / 64 + kTileWords - 1) / kTileWords) * ((nbits + 63) / 64);
         launch(PROBE_OTHER, k_wires_to_bits_map, dim3((u32)tiles, 2), dim3(256), 0, S(stream), mem,
                (u64)share_stride, wires, nbits, (u64)words, out, (u64)out_rows, *map, (u64)rows);

@@ -9,7 +9,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from aby3_amd import native as nt  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--job", choices=["mul", "msb", "lr", "a2b", "bitinj"], required=True)
+ap.add_argument("--job", choices=["mul", "msb", "lr", "a2b", "bitinj", "sort"], required=True)
 ap.add_argument("--steps", type=int, default=4)
 a = ap.parse_args()
 if a.job == "mul":
@@ -18,6 +18,8 @@ elif a.job == "msb":
     s = nt.Session(nt.JOB_MSB, [1 << 20], probe=False)
 elif a.job == "a2b":
     s = nt.Session(nt.JOB_A2B, [1 << 20], probe=False)
+elif a.job == "sort":
+    s = nt.Session(nt.JOB_SORT, [1 << 20], probe=False)
 elif a.job == "bitinj":
     s = nt.Session(nt.JOB_BITINJ, [1 << 16, 64], probe=False)
 else:

@@ -557,10 +557,21 @@ __device__ __forceinline__ u64 map_row(const aby3g_rowmap& m, u64 p) {
 
 // k_bits_to_wires_tiled over mapped source rows (the round's gather fused
 // into setInput). Rows mapped outside the source read as zero.
+// Up to two (map, destination) pairs per launch, blockIdx.z selecting one:
+// the two inputs of a compare-exchange round (its two gathers) or its two
+// outputs (its two scatters) in one grid.
+struct MapPair {
+    aby3g_rowmap map[2];
+    u64* wrows[2];            // k_bits_to_wires_map
+    const u32* wires[2];      // k_wires_to_bits_map
+};
+
 __global__ void __launch_bounds__(256) k_bits_to_wires_map(const i64* __restrict__ in, u64 inRows, u64 cols64,
-                                                           u32 nbits, aby3g_rowmap map, u64 rows,
-                                                           u64* __restrict__ wrows, u64 shareStride, u64 words) {
+                                                           u32 nbits, MapPair jobs, u64 rows, u64 shareStride,
+                                                           u64 words) {
     __shared__ u64 tile[64 * kTilePitch];
+    const aby3g_rowmap& map = jobs.map[blockIdx.z];
+    u64* wrows = jobs.wrows[blockIdx.z];
     in += (u64)blockIdx.y * inRows * cols64;
     wrows += (u64)blockIdx.y * shareStride;
     const u64 tilesPerCol = (words + kTileWords - 1) / kTileWords;
@@ -592,11 +603,12 @@ __global__ void __launch_bounds__(256) k_bits_to_wires_map(const i64* __restrict
 
 // k_wires_to_bits_tiled scattering circuit row p to row map(p) of `out`
 // (the round's scatter fused into getOutput).
-__global__ void __launch_bounds__(256) k_wires_to_bits_map(const u64* __restrict__ mem, u64 shareStride,
-                                                           const u32* __restrict__ wires, u32 nbits, u64 words,
-                                                           i64* __restrict__ out, u64 outRows, aby3g_rowmap map,
+__global__ void __launch_bounds__(256) k_wires_to_bits_map(const u64* __restrict__ mem, u64 shareStride, u32 nbits,
+                                                           u64 words, i64* __restrict__ out, u64 outRows, MapPair jobs,
                                                            u64 rows) {
     __shared__ u64 tile[64 * kTilePitch];
+    const aby3g_rowmap& map = jobs.map[blockIdx.z];
+    const u32* __restrict__ wires = jobs.wires[blockIdx.z];
     const u64 cols = (nbits + 63) / 64;
     mem += (u64)blockIdx.y * shareStride;
     out += (u64)blockIdx.y * outRows * cols;
@@ -795,27 +807,53 @@ int aby3g_wires_to_bits2(const uint64_t* mem, uint64_t share_stride, const uint3
 int aby3g_bits_to_wires_map(const int64_t* in, uint64_t in_rows, uint64_t cols64, uint32_t nbits,
                             const aby3g_rowmap* map, uint64_t rows, uint64_t* wire_rows, uint64_t share_stride,
                             uint64_t words, aby3g_stream stream) {
+    return aby3g_bits_to_wires_map_n(in, in_rows, cols64, nbits, map, &wire_rows, 1, rows, share_stride, words, stream);
+}
+
+int aby3g_bits_to_wires_map_n(const int64_t* in, uint64_t in_rows, uint64_t cols64, uint32_t nbits,
+                              const aby3g_rowmap* maps, uint64_t* const* wire_rows, uint32_t n, uint64_t rows,
+                              uint64_t share_stride, uint64_t words, aby3g_stream stream) {
     return guarded([&] {
+        ABY3G_REQUIRE(n >= 1 && n <= 2, "one or two maps per call");
+        ABY3G_REQUIRE(maps != nullptr && wire_rows != nullptr, "null argument");
         ABY3G_REQUIRE(nbits <= cols64 * 64, "nbits exceeds input columns");
         ABY3G_REQUIRE(words * 64 >= rows, "words too small for rows");
-        check_map(map, rows, in_rows);
+        MapPair jobs{};
+        for (u32 k = 0; k < n; ++k) {
+            check_map(&maps[k], rows, in_rows);
+            jobs.map[k] = maps[k];
+            jobs.wrows[k] = wire_rows[k];
+        }
         if (!nbits || !words) return;
         const u64 tiles = ((words + kTileWords - 1) / kTileWords) * ((nbits + 63) / 64);
-        launch(PROBE_OTHER, k_bits_to_wires_map, dim3((u32)tiles, 2), dim3(256), 0, S(stream), in, (u64)in_rows,
-               (u64)cols64, nbits, *map, (u64)rows, wire_rows, (u64)share_stride, (u64)words);
+        launch(PROBE_OTHER, k_bits_to_wires_map, dim3((u32)tiles, 2, n), dim3(256), 0, S(stream), in, (u64)in_rows,
+               (u64)cols64, nbits, jobs, (u64)rows, (u64)share_stride, (u64)words);
     });
 }
 
 int aby3g_wires_to_bits_map(const uint64_t* mem, uint64_t share_stride, const uint32_t* wires, uint32_t nbits,
                             uint64_t words, int64_t* out, uint64_t out_rows, const aby3g_rowmap* map, uint64_t rows,
                             aby3g_stream stream) {
+    return aby3g_wires_to_bits_map_n(mem, share_stride, &wires, nbits, words, out, out_rows, map, 1, rows, stream);
+}
+
+int aby3g_wires_to_bits_map_n(const uint64_t* mem, uint64_t share_stride, const uint32_t* const* wires,
+                              uint32_t nbits, uint64_t words, int64_t* out, uint64_t out_rows,
+                              const aby3g_rowmap* maps, uint32_t n, uint64_t rows, aby3g_stream stream) {
     return guarded([&] {
+        ABY3G_REQUIRE(n >= 1 && n <= 2, "one or two maps per call");
+        ABY3G_REQUIRE(maps != nullptr && wires != nullptr, "null argument");
         ABY3G_REQUIRE(words * 64 >= rows, "words too small for rows");
-        check_map(map, rows, out_rows);
+        MapPair jobs{};
+        for (u32 k = 0; k < n; ++k) {
+            check_map(&maps[k], rows, out_rows);
+            jobs.map[k] = maps[k];
+            jobs.wires[k] = wires[k];
+        }
         if (!nbits || !rows) return;
         const u64 tiles = (((rows + 63) / 64 + kTileWords - 1) / kTileWords) * ((nbits + 63) / 64);
-        launch(PROBE_OTHER, k_wires_to_bits_map, dim3((u32)tiles, 2), dim3(256), 0, S(stream), mem,
-               (u64)share_stride, wires, nbits, (u64)words, out, (u64)out_rows, *map, (u64)rows);
+        launch(PROBE_OTHER, k_wires_to_bits_map, dim3((u32)tiles, 2, n), dim3(256), 0, S(stream), mem,
+               (u64)share_stride, nbits, (u64)words, out, (u64)out_rows, jobs, (u64)rows);
     });
 }
 

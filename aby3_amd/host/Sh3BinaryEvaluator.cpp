@@ -203,6 +203,25 @@ void Sh3BinaryEvaluator::setInput(u64 i, const sbMatrix& in, const aby3g_rowmap&
     mLevel = 0;
 }
 
+void Sh3BinaryEvaluator::setInputs(u64 i, const aby3g_rowmap& mi, u64 j, const aby3g_rowmap& mj,
+                                   const sbMatrix& in) {
+    if (!mCir) throw RTE_LOC;
+    if (i >= mCir->mInputs.size() || j >= mCir->mInputs.size()) throw std::invalid_argument("input index out of bounds");
+    const auto& wi = mCir->mInputs[i];
+    const auto& wj = mCir->mInputs[j];
+    if (in.bitCount() != wi.size() || in.bitCount() != wj.size()) throw std::invalid_argument("input data wrong size");
+    for (const auto* wires : {&wi, &wj})
+        for (size_t k = 1; k < wires->size(); ++k)
+            if ((*wires)[k] != (*wires)[k - 1] + 1) throw std::runtime_error("expecting contiguous input wires. " LOCATION);
+    Gpu& g = *mGpu;
+    const u64 W = mCir->mWireCount;
+    const aby3g_rowmap maps[2] = {mi, mj};
+    u64* dst[2] = {mMem.as<u64>() + wi[0] * mWords, mMem.as<u64>() + wj[0] * mWords};
+    GPU_CALL(aby3g_bits_to_wires_map_n(in.data(), in.rows(), in.i64Cols(), (u32)wi.size(), maps, dst, 2, mRows,
+                                       W * mWords, mWords, g.stream()));
+    mLevel = 0;
+}
+
 void Sh3BinaryEvaluator::setInputs(const std::vector<WireInput>& in) {
     if (!mCir) throw RTE_LOC;
     Gpu& g = *mGpu;
@@ -428,6 +447,18 @@ void Sh3BinaryEvaluator::getOutput(u64 i, sbMatrix& out) {
     const u32* dw = mCur->allOutputWires + mCur->outputOffsets[i];
     GPU_CALL(aby3g_wires_to_bits2(mMem.as<u64>(), W * mWords, dw, (u32)wires.size(), mWords, out.data(), mRows,
                                   g.stream()));
+}
+
+void Sh3BinaryEvaluator::getOutputs(u64 i, const aby3g_rowmap& mi, u64 j, const aby3g_rowmap& mj, sbMatrix& out) {
+    if (i >= mCir->mOutputs.size() || j >= mCir->mOutputs.size()) throw RTE_LOC;
+    if (out.bitCount() != mCir->mOutputs[i].size() || out.bitCount() != mCir->mOutputs[j].size())
+        throw std::invalid_argument("output matrix wrong size");
+    Gpu& g = *mGpu;
+    const u64 W = mCir->mWireCount;
+    const u32* dw[2] = {mCur->allOutputWires + mCur->outputOffsets[i], mCur->allOutputWires + mCur->outputOffsets[j]};
+    const aby3g_rowmap maps[2] = {mi, mj};
+    GPU_CALL(aby3g_wires_to_bits_map_n(mMem.as<u64>(), W * mWords, dw, (u32)out.bitCount(), mWords, out.data(),
+                                       out.rows(), maps, 2, mRows, g.stream()));
 }
 
 void Sh3BinaryEvaluator::getOutput(u64 i, sbMatrix& out, const aby3g_rowmap& map) {

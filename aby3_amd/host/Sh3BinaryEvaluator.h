@@ -39,6 +39,8 @@ public:
     // setInput from mapped rows of `in` (circuit row p <- row map(p)): the
     // compare-exchange gather of a merge round fused into the transpose
     void setInput(u64 i, const sbMatrix& in, const aby3g_rowmap& map);
+    // setInput(i, in, mi) and setInput(j, in, mj) in one launch
+    void setInputs(u64 i, const aby3g_rowmap& mi, u64 j, const aby3g_rowmap& mj, const sbMatrix& in);
     // a one-row shared input broadcast to every row (Sh3BinaryEvaluator.cpp:105-138)
     void setReplicatedInput(u64 i, const sbMatrix& in);
     // Inputs straight from arithmetic shares, several in one launch (no
@@ -60,6 +62,8 @@ public:
     // getOutput into mapped rows of an existing `out` (row map(p) <- circuit
     // row p; other rows untouched): the round's scatter
     void getOutput(u64 i, sbMatrix& out, const aby3g_rowmap& map);
+    // getOutput(i, out, mi) and getOutput(j, out, mj) in one launch (the maps' rows disjoint)
+    void getOutputs(u64 i, const aby3g_rowmap& mi, u64 j, const aby3g_rowmap& mj, sbMatrix& out);
 
     bool hasMoreRounds() const { return mLevel <= mCir->mLevelCounts.size(); }
     void roundCallback(CommPkg& comm, Sh3Task task);

@@ -53,12 +53,15 @@ void compareExchange(Sh3BinaryEvaluator& eng, const sbMatrix& src, sbMatrix& dst
         aby3g_rowmap m[4] = {gx, gy, sx ? *sx : gx, sy ? *sy : gy};
         for (auto& x : m) x.first += c;
         eng.setCir(cir, n, eval.mShareGen);
-        eng.setInput(0, src, m[0]);
-        eng.setInput(1, src, m[1]);
+        eng.setInputs(0, m[0], 1, m[1], src);  // both gathers in one launch
         eng.asyncEvaluate(rt.noDependencies())
             .then([&](Sh3Task&) {
-                if (sx) eng.getOutput(0, dst, m[2]);
-                if (sy) eng.getOutput(1, dst, m[3]);
+                if (sx && sy)
+                    eng.getOutputs(0, m[2], 1, m[3], dst);  // both scatters in one launch
+                else if (sx)
+                    eng.getOutput(0, dst, m[2]);
+                else if (sy)
+                    eng.getOutput(1, dst, m[3]);
             })
             .get();
     }

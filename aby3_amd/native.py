@@ -157,6 +157,10 @@ _SIGS = {
                                      c_void_p]),
     "aby3g_wires_to_bits2": (c_int, [c_void_p, c_uint64, c_void_p, ctypes.c_uint32, c_uint64, c_void_p, c_uint64,
                                      c_void_p]),
+    "aby3g_bits_to_wires_map_n": (c_int, [c_void_p, c_uint64, c_uint64, ctypes.c_uint32, c_void_p, c_void_p,
+                                          ctypes.c_uint32, c_uint64, c_uint64, c_uint64, c_void_p]),
+    "aby3g_wires_to_bits_map_n": (c_int, [c_void_p, c_uint64, c_void_p, ctypes.c_uint32, c_uint64, c_void_p,
+                                          c_uint64, c_void_p, ctypes.c_uint32, c_uint64, c_void_p]),
     "aby3g_bits_to_wires_map": (c_int, [c_void_p, c_uint64, c_uint64, ctypes.c_uint32, POINTER(RowMap), c_uint64,
                                         c_void_p, c_uint64, c_uint64, c_void_p]),
     "aby3g_wires_to_bits_map": (c_int, [c_void_p, c_uint64, c_void_p, ctypes.c_uint32, c_uint64, c_void_p, c_uint64,

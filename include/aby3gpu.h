@@ -397,6 +397,16 @@ int aby3g_bits_to_wires_map(const int64_t* in, uint64_t in_rows, uint64_t cols64
 int aby3g_wires_to_bits_map(const uint64_t* mem, uint64_t share_stride, const uint32_t* wires, uint32_t nbits,
                             uint64_t words, int64_t* out, uint64_t out_rows, const aby3g_rowmap* map, uint64_t rows,
                             aby3g_stream stream);
+/* One or two mapped transposes in one launch (n <= 2): the two gathers of a
+ * compare-exchange round's inputs (same source, maps[k] -> wire_rows[k]), or
+ * its two scatters (wire lists wires[k] -> maps[k] rows of the same out, the
+ * maps' target rows disjoint). Same semantics as n separate calls. */
+int aby3g_bits_to_wires_map_n(const int64_t* in, uint64_t in_rows, uint64_t cols64, uint32_t nbits,
+                              const aby3g_rowmap* maps, uint64_t* const* wire_rows, uint32_t n, uint64_t rows,
+                              uint64_t share_stride, uint64_t words, aby3g_stream stream);
+int aby3g_wires_to_bits_map_n(const uint64_t* mem, uint64_t share_stride, const uint32_t* const* wires,
+                              uint32_t nbits, uint64_t words, int64_t* out, uint64_t out_rows,
+                              const aby3g_rowmap* maps, uint32_t n, uint64_t rows, aby3g_stream stream);
 
 /* setInput of shares that are linear combinations of arithmetic shares,
  * several inputs / shares in one launch (the two-input binary resharing of

@@ -330,6 +330,38 @@ def test_transposes_mapped(gpu, in_rows, rows, mp):
     assert np.array_equal(host(out).reshape(2, in_rows, 1), exp)
 
 
+@pytest.mark.parametrize("in_rows,half", [(4096, 2048), (5000, 2400)])
+def test_transposes_mapped_pair(gpu, in_rows, half):
+    """bits_to_wires_map_n / wires_to_bits_map_n: a compare-exchange round's
+    two gathers (first / second elements of each pair) and two scatters in
+    one launch each, against numpy."""
+    import torch
+
+    x = rnd(in_rows + half, 2 * in_rows).reshape(2, in_rows, 1)
+    maps = [(0, 0, 2, half, 0), (0, 1, 2, half, 0)]  # even rows, odd rows
+    rms = (nt.RowMap * 2)(*[nt.RowMap(*m, None) for m in maps])
+    srcs = [_map_rows(*m, half) for m in maps]
+    words = 32 * ((half + 2047) // 2048)
+    mem = dev(rnd(3, 2 * 128 * words))  # input 0 at wires 0..63, input 1 at wires 64..127
+    dst = (ctypes.c_void_p * 2)(mem.data_ptr(), mem.data_ptr() + 8 * 64 * words)
+    gpu.bits_to_wires_map_n(P(dev(x)), in_rows, 1, 64, rms, dst, 2, half, 128 * words, words, None)
+    m = host(mem).view(np.uint64).reshape(2, 128, words)
+    for s in range(2):
+        for k in range(2):
+            assert np.array_equal(m[s, 64 * k:64 * k + 64], _bits_ref(x[s, srcs[k]], 64, words))
+    # scatter input k's wires back through the other map: rows swap within each pair
+    ids = [torch.arange(64 * k, 64 * k + 64, dtype=torch.int32, device="cuda") for k in range(2)]
+    wl = (ctypes.c_void_p * 2)(ids[0].data_ptr(), ids[1].data_ptr())
+    swapped = (nt.RowMap * 2)(rms[1], rms[0])
+    out_np = rnd(in_rows + 1, 2 * in_rows).reshape(2, in_rows, 1)
+    out = dev(out_np)
+    gpu.wires_to_bits_map_n(P(mem), 128 * words, wl, 64, words, P(out), in_rows, swapped, 2, half, None)
+    exp = out_np.copy()
+    exp[:, srcs[1]] = x[:, srcs[0]]
+    exp[:, srcs[0]] = x[:, srcs[1]]
+    assert np.array_equal(host(out).reshape(2, in_rows, 1), exp)
+
+
 def test_transposes_mapped_rejects_out_of_range(gpu):
     x = empty(2 * 100)
     mem = empty(2 * 64 * 32)

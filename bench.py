@@ -439,7 +439,11 @@ def main():
     if args.deployment == "parties":
         return main_parties(args, world, rank, local, pg, nt)
 
-    dev = local
+    import ctypes
+
+    ndev = ctypes.c_int(0)
+    nt.lib().device_count(ctypes.byref(ndev))
+    dev = local % max(ndev.value, 1)  # one GPU per rank, also when each rank sees only its own
     M, K, N, D = args.m, args.k, args.n, args.decimal
     # only the share-GEMM launches carry timing events (the roofline kernel);
     # digit and epilogue times come from a second, separately probed pass

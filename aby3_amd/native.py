@@ -12,11 +12,11 @@ import os
 import re
 from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_size_t, c_uint32, c_uint64, c_void_p
 
-# Three co-located parties drive two streams each (main + auxiliary); HIP
-# maps streams onto GPU_MAX_HW_QUEUES hardware queues (default 4), and two
-# parties' streams sharing a queue serialize their kernels. Ask for 8 unless
-# the caller chose otherwise (read once, at HIP initialisation).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (default 4). Three
+# co-located parties use one stream each plus the shared AND-mask draw stream
+# -- four -- so the default fits; 8 queues measured the same, and extra
+# per-party streams with them far slower. Left to the
+# caller's environment.
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(_HERE, "lib")

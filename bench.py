@@ -76,8 +76,19 @@ def dist_setup():
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        # control plane only (barrier, max over ranks): no data crosses ranks
-        dist.init_process_group(backend="gloo")
+        # control plane only (barrier, max over ranks): no data crosses ranks.
+        # gloo reports its connections on the process's stdout, where the
+        # one JSON line goes: point fd 1 at stderr while it connects.
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group(backend="gloo")
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
         pg = dist
     return world, rank, local, pg
 

@@ -290,6 +290,26 @@ def test_bits_to_wires_lin(gpu, rows):
     assert np.array_equal(m[2], _bits_ref(e2, 64, words))
 
 
+def test_bits_to_wires_lin_two_columns(gpu):
+    """bits_to_wires_lin over a 2-column (100-bit) source: the strided row
+    path of the register transpose, trimmed to nbits."""
+    rows, nbits, cols = 3001, 100, 2
+    words = 32 * ((rows + 2047) // 2048)
+    t = rnd(77, rows * cols)
+    t.reshape(rows, cols)[:, 1] &= np.int64((1 << (nbits - 64)) - 1)
+    mem = dev(rnd(78, nbits * words))
+    Src = nt.WireSrc * 1
+    s = Src()
+    dt = dev(t)
+    s[0].cols64, s[0].nbits = cols, nbits
+    s[0].wire_rows = ctypes.cast(mem.data_ptr(), ctypes.POINTER(ctypes.c_uint64))
+    s[0].term[0] = ctypes.cast(dt.data_ptr(), ctypes.POINTER(ctypes.c_int64))
+    s[0].coef[0] = 1
+    gpu.bits_to_wires_lin(s, 1, rows, words, None)
+    m = host(mem).view(np.uint64).reshape(nbits, words)
+    assert np.array_equal(m, _bits_ref(t.reshape(rows, cols), nbits, words))
+
+
 def _map_rows(first, start, step, per_rep, rep_stride, n):
     q = first + np.arange(n, dtype=np.int64)
     return start + (q // per_rep) * rep_stride + (q % per_rep) * step

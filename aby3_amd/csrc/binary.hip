@@ -394,6 +394,25 @@ __global__ void __launch_bounds__(64) k_w2b_regs(const u64* __restrict__ mem, u6
     }
 }
 
+// wires -> bits for a few wires (nbits <= 8, one output column): a thread per
+// output row and share gathers bit (row & 63) of each wire's word (the words
+// are shared by 64 neighbouring threads and come from the cache); the row
+// stores are fully coalesced and no 64 x 64 transpose is done for the one or
+// few bits that exist (a comparison's output bit, the piecewise regions).
+__global__ void __launch_bounds__(256) k_w2b_few(const u64* __restrict__ mem, u64 shareStride,
+                                                 const u32* __restrict__ wires, u32 nbits, u64 words,
+                                                 i64* __restrict__ out, u64 rows) {
+    const u64 r = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (r >= rows) return;
+    mem += (u64)blockIdx.y * shareStride;
+    out += (u64)blockIdx.y * rows;
+    const u64 w = r >> 6;
+    const u32 sh = (u32)(r & 63);
+    u64 v = 0;
+    for (u32 b = 0; b < nbits; ++b) v |= ((mem[(u64)wires[b] * words + w] >> sh) & 1ull) << b;
+    out[r] = (i64)v;
+}
+
 // Variant selection for A/B runs: ABY3G_B2W=tiled keeps the LDS-tiled
 // butterfly kernels below for the plain / linear-combination transposes.
 inline bool b2w_regs() {
@@ -792,6 +811,11 @@ int aby3g_wires_to_bits2(const uint64_t* mem, uint64_t share_stride, const uint3
     return guarded([&] {
         ABY3G_REQUIRE(words * 64 >= rows, "words too small for rows");
         if (!nbits || !rows) return;
+        if (nbits <= 8 && b2w_regs()) {
+            launch(PROBE_OTHER, k_w2b_few, dim3((u32)((rows + 255) / 256), 2), dim3(256), 0, S(stream), mem,
+                   (u64)share_stride, wires, nbits, (u64)words, out, (u64)rows);
+            return;
+        }
         if (b2w_regs()) {
             const u64 wgs = (((rows + 63) / 64 + 63) / 64) * ((nbits + 63) / 64);
             launch(PROBE_OTHER, k_w2b_regs, dim3((u32)wgs, 2), dim3(64), 0, S(stream), mem, (u64)share_stride, wires,

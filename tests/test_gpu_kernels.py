@@ -235,7 +235,8 @@ def test_transposes(gpu, rows, nbits):
     assert np.array_equal(host(out).reshape(rows, cols), x)
 
 
-@pytest.mark.parametrize("rows,nbits", [(1, 1), (3000, 70), (4096, 64), (70001, 64), (5000, 130)])
+@pytest.mark.parametrize("rows,nbits", [(1, 1), (3000, 70), (4096, 64), (70001, 64), (5000, 130), (70001, 1),
+                                        (5000, 7), (2048, 8), (100, 9)])
 def test_transposes_both_shares(gpu, rows, nbits):
     """bits_to_wires2 / wires_to_bits2 (both shares, engine memory layout)."""
     import torch

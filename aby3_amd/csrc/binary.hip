@@ -517,8 +517,8 @@ __global__ void __launch_bounds__(64) k_b2w_lin_regs(WireSrcs ws, u64 rows, u64 
 #pragma unroll
         for (int k = 0; k < 64; ++k)
             if (r0 + k < rows) R[k] += (u64)src.constant;  // padded rows stay zero
+        transpose64_regs(R);  // (a source without terms writes zero wires as they are)
     }
-    transpose64_regs(R);
     u64* __restrict__ out = src.wire_rows;
 #pragma unroll
     for (int b = 0; b < 64; ++b)

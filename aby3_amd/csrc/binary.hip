@@ -254,43 +254,13 @@ __global__ void __launch_bounds__(256) k_wires_to_bits(const u64* __restrict__ m
     if (row < rows) out[row * cols + c] = (i64)mine;
 }
 
-// LDS-tiled transposes (the both-share entry points): a workgroup owns 64
+// LDS-tiled transposes (the mapped forms below): a workgroup owns 64
 // consecutive words (4096 rows) of one 64-bit column. bits -> wires: each
 // wave bit-transposes 16 words (transpose64) into an LDS tile [bit][word], then
 // the tile leaves as 64 contiguous 512-byte wire segments. wires -> bits:
 // the reverse, reading 512-byte wire segments into the tile.
 constexpr u32 kTileWords = 64;
 constexpr u32 kTilePitch = kTileWords + 1;  // u64 per tile row (+1: bank spread)
-
-__global__ void __launch_bounds__(256) k_bits_to_wires_tiled(const i64* __restrict__ in, u64 rows, u64 cols64,
-                                                             u32 nbits, u64* __restrict__ wrows, u64 shareStride,
-                                                             u64 words) {
-    __shared__ u64 tile[64 * kTilePitch];
-    in += (u64)blockIdx.y * rows * cols64;
-    wrows += (u64)blockIdx.y * shareStride;
-    const u64 tilesPerCol = (words + kTileWords - 1) / kTileWords;
-    const u64 c = blockIdx.x / tilesPerCol, w0 = (blockIdx.x % tilesPerCol) * kTileWords;
-    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // all 16 loads of this wave in flight before the first transpose
-    u64 vv[16];
-#pragma unroll
-    for (u32 k = 0; k < 16; ++k) {
-        const u32 wl = wave * 16 + k;
-        const u64 r = (w0 + wl) * 64 + lane;
-        vv[k] = (w0 + wl < words && r < rows) ? (u64)in[r * cols64 + c] : 0;
-    }
-    for (u32 k = 0; k < 16; ++k) {
-        const u32 wl = wave * 16 + k;
-        const u64 mine = transpose64(vv[k], lane);
-        tile[lane * kTilePitch + wl] = mine;
-    }
-    __syncthreads();
-    for (u32 idx = threadIdx.x; idx < 64 * kTileWords; idx += 256) {
-        const u32 b = idx / kTileWords, wl = idx % kTileWords;
-        const u64 bit = c * 64 + b;
-        if (bit < nbits && w0 + wl < words) wrows[bit * words + w0 + wl] = tile[b * kTilePitch + wl];
-    }
-}
 
 // ---- register transposes: one thread per 64-row word ----------------------
 // A thread holds the 64 rows of one word (R[r] = row r) and transposes them
@@ -413,62 +383,17 @@ __global__ void __launch_bounds__(256) k_w2b_few(const u64* __restrict__ mem, u6
     out[r] = (i64)v;
 }
 
-// Variant selection for A/B runs: ABY3G_B2W=tiled keeps the LDS-tiled
-// butterfly kernels below for the plain / linear-combination transposes.
-inline bool b2w_regs() {
-    static const bool v = [] {
-        const char* e = getenv("ABY3G_B2W");
-        return !(e && e[0] == 't');
-    }();
-    return v;
-}
 // The mapped (gather / scatter) transposes keep the LDS-tiled kernels below:
 // their rows are scattered, and both register forms measured slower on C5 --
 // 64 separate 8-byte row accesses per thread (118-121 vs 103 ms), and rows
 // gathered wave-wide into an LDS stage then transposed per thread (101 vs
 // 88-90 ms: 194 VGPRs leave too few waves to hide the gathers).
 
-// k_bits_to_wires_tiled over computed values: blockIdx.y = source
 struct WireSrcs {
     aby3g_wire_src s[ABY3G_WIRE_SRC_MAX];
 };
-__global__ void __launch_bounds__(256) k_bits_to_wires_lin(WireSrcs ws, u64 rows, u64 words) {
-    __shared__ u64 tile[64 * kTilePitch];
-    const aby3g_wire_src& src = ws.s[blockIdx.y];
-    const u64 cols64 = src.cols64;
-    const u64 tilesPerCol = (words + kTileWords - 1) / kTileWords;
-    const u64 c = blockIdx.x / tilesPerCol, w0 = (blockIdx.x % tilesPerCol) * kTileWords;
-    if (c * 64 >= src.nbits) return;  // this source has fewer columns than the grid
-    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    u64 vv[16];
-#pragma unroll
-    for (u32 k = 0; k < 16; ++k) {
-        const u32 wl = wave * 16 + k;
-        const u64 r = (w0 + wl) * 64 + lane;
-        u64 v = 0;
-        if (w0 + wl < words && r < rows) {
-            const u64 i = r * cols64 + c;
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-                if (src.term[t]) v += (u64)src.coef[t] * (u64)src.term[t][i];
-            if (src.copy_out) src.copy_out[i] = (i64)v;
-            if (src.term[0] || src.term[1] || src.term[2] || src.term[3]) v += (u64)src.constant;
-        }
-        vv[k] = v;
-    }
-    for (u32 k = 0; k < 16; ++k) {
-        const u32 wl = wave * 16 + k;
-        tile[lane * kTilePitch + wl] = transpose64(vv[k], lane);
-    }
-    __syncthreads();
-    for (u32 idx = threadIdx.x; idx < 64 * kTileWords; idx += 256) {
-        const u32 b = idx / kTileWords, wl = idx % kTileWords;
-        const u64 bit = c * 64 + b;
-        if (bit < src.nbits && w0 + wl < words) src.wire_rows[bit * words + w0 + wl] = tile[b * kTilePitch + wl];
-    }
-}
-
-// k_bits_to_wires_lin with register transposes. The source descriptor is
+// setInput of linear combinations (aby3g_bits_to_wires_lin), one thread per
+// (word, column) with register transposes. The source descriptor is
 // copied out of the kernarg array first and the copy-out is stored only after
 // every term load: a store through copy_out between loads would force the
 // compiler (which cannot rule out aliasing) to serialise the row loads.
@@ -525,38 +450,6 @@ __global__ void __launch_bounds__(64) k_b2w_lin_regs(WireSrcs ws, u64 rows, u64 
         if (c * 64 + b < src.nbits) out[(c * 64 + b) * words + w] = R[b];
 }
 
-__global__ void __launch_bounds__(256) k_wires_to_bits_tiled(const u64* __restrict__ mem, u64 shareStride,
-                                                             const u32* __restrict__ wires, u32 nbits, u64 words,
-                                                             i64* __restrict__ out, u64 rows) {
-    __shared__ u64 tile[64 * kTilePitch];
-    const u64 cols = (nbits + 63) / 64;
-    mem += (u64)blockIdx.y * shareStride;
-    out += (u64)blockIdx.y * rows * cols;
-    const u64 rw = (rows + 63) / 64;  // words holding real rows
-    const u64 tilesPerCol = (rw + kTileWords - 1) / kTileWords;
-    const u64 c = blockIdx.x / tilesPerCol, w0 = (blockIdx.x % tilesPerCol) * kTileWords;
-    u64 vv[16];
-#pragma unroll
-    for (u32 j = 0; j < 16; ++j) {
-        const u32 idx = threadIdx.x + 256 * j, b = idx / kTileWords, wl = idx % kTileWords;
-        const u64 bit = c * 64 + b;
-        vv[j] = (bit < nbits && w0 + wl < rw) ? mem[(u64)wires[bit] * words + w0 + wl] : 0;
-    }
-#pragma unroll
-    for (u32 j = 0; j < 16; ++j) {
-        const u32 idx = threadIdx.x + 256 * j;
-        tile[(idx / kTileWords) * kTilePitch + idx % kTileWords] = vv[j];
-    }
-    __syncthreads();
-    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (u32 k = 0; k < 16; ++k) {
-        const u32 wl = wave * 16 + k;
-        const u64 mine = transpose64(tile[lane * kTilePitch + wl], lane);
-        const u64 row = (w0 + wl) * 64 + lane;
-        if (w0 + wl < rw && row < rows) out[row * cols + c] = (i64)mine;
-    }
-}
-
 // Row p of a merge round's compare-exchange list -> row of the merge array
 // (aby3g_rowmap). 32-bit division whenever the operands fit.
 __device__ __forceinline__ u64 map_row(const aby3g_rowmap& m, u64 p) {
@@ -574,7 +467,7 @@ __device__ __forceinline__ u64 map_row(const aby3g_rowmap& m, u64 p) {
     return m.start + rep * m.rep_stride + k * m.step;
 }
 
-// k_bits_to_wires_tiled over mapped source rows (the round's gather fused
+// LDS-tiled bits -> wires over mapped source rows (the round's gather fused
 // into setInput). Rows mapped outside the source read as zero.
 // Up to two (map, destination) pairs per launch, blockIdx.z selecting one:
 // the two inputs of a compare-exchange round (its two gathers) or its two
@@ -620,7 +513,7 @@ __global__ void __launch_bounds__(256) k_bits_to_wires_map(const i64* __restrict
     }
 }
 
-// k_wires_to_bits_tiled scattering circuit row p to row map(p) of `out`
+// LDS-tiled wires -> bits scattering circuit row p to row map(p) of `out`
 // (the round's scatter fused into getOutput).
 __global__ void __launch_bounds__(256) k_wires_to_bits_map(const u64* __restrict__ mem, u64 shareStride, u32 nbits,
                                                            u64 words, i64* __restrict__ out, u64 outRows, MapPair jobs,
@@ -762,15 +655,9 @@ int aby3g_bits_to_wires2(const int64_t* in, uint64_t rows, uint64_t cols64, uint
         ABY3G_REQUIRE(nbits <= cols64 * 64, "nbits exceeds input columns");
         ABY3G_REQUIRE(words * 64 >= rows, "words too small for rows");
         if (!nbits || !words) return;
-        if (b2w_regs()) {
-            const u64 wgs = ((words + 63) / 64) * ((nbits + 63) / 64);
-            launch(PROBE_OTHER, k_b2w_regs, dim3((u32)wgs, 2), dim3(64), 0, S(stream), in, rows, cols64, nbits,
-                   wire_rows, share_stride, words);
-            return;
-        }
-        const u64 tiles = ((words + kTileWords - 1) / kTileWords) * ((nbits + 63) / 64);
-        launch(PROBE_OTHER, k_bits_to_wires_tiled, dim3((u32)tiles, 2), dim3(256), 0, S(stream), in, rows, cols64,
-               nbits, wire_rows, share_stride, words);
+        const u64 wgs = ((words + 63) / 64) * ((nbits + 63) / 64);
+        launch(PROBE_OTHER, k_b2w_regs, dim3((u32)wgs, 2), dim3(64), 0, S(stream), in, rows, cols64, nbits, wire_rows,
+               share_stride, words);
     });
 }
 
@@ -789,15 +676,8 @@ int aby3g_bits_to_wires_lin(const aby3g_wire_src* srcs, uint32_t nsrc, uint64_t 
             cols = std::max<u64>(cols, (srcs[k].nbits + 63) / 64);
         }
         if (!cols) return;
-        if (b2w_regs()) {
-            const u64 wgs = ((words + 63) / 64) * cols;
-            launch(PROBE_OTHER, k_b2w_lin_regs, dim3((u32)wgs, nsrc), dim3(64), 0, S(stream), ws, (u64)rows,
-                   (u64)words);
-            return;
-        }
-        const u64 tiles = ((words + kTileWords - 1) / kTileWords) * cols;
-        launch(PROBE_OTHER, k_bits_to_wires_lin, dim3((u32)tiles, nsrc), dim3(256), 0, S(stream), ws, (u64)rows,
-               (u64)words);
+        const u64 wgs = ((words + 63) / 64) * cols;
+        launch(PROBE_OTHER, k_b2w_lin_regs, dim3((u32)wgs, nsrc), dim3(64), 0, S(stream), ws, (u64)rows, (u64)words);
     });
 }
 
@@ -811,20 +691,14 @@ int aby3g_wires_to_bits2(const uint64_t* mem, uint64_t share_stride, const uint3
     return guarded([&] {
         ABY3G_REQUIRE(words * 64 >= rows, "words too small for rows");
         if (!nbits || !rows) return;
-        if (nbits <= 8 && b2w_regs()) {
+        if (nbits <= 8) {
             launch(PROBE_OTHER, k_w2b_few, dim3((u32)((rows + 255) / 256), 2), dim3(256), 0, S(stream), mem,
                    (u64)share_stride, wires, nbits, (u64)words, out, (u64)rows);
             return;
         }
-        if (b2w_regs()) {
-            const u64 wgs = (((rows + 63) / 64 + 63) / 64) * ((nbits + 63) / 64);
-            launch(PROBE_OTHER, k_w2b_regs, dim3((u32)wgs, 2), dim3(64), 0, S(stream), mem, (u64)share_stride, wires,
-                   nbits, (u64)words, out, (u64)rows);
-            return;
-        }
-        const u64 tiles = (((rows + 63) / 64 + kTileWords - 1) / kTileWords) * ((nbits + 63) / 64);
-        launch(PROBE_OTHER, k_wires_to_bits_tiled, dim3((u32)tiles, 2), dim3(256), 0, S(stream), mem, share_stride,
-               wires, nbits, words, out, rows);
+        const u64 wgs = (((rows + 63) / 64 + 63) / 64) * ((nbits + 63) / 64);
+        launch(PROBE_OTHER, k_w2b_regs, dim3((u32)wgs, 2), dim3(64), 0, S(stream), mem, (u64)share_stride, wires, nbits,
+               (u64)words, out, (u64)rows);
     });
 }
 

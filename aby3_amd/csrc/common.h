@@ -290,6 +290,112 @@ inline u32 aes_grid(u64 items, u32 block) {
 
 inline hipStream_t S(aby3g_stream s) { return reinterpret_cast<hipStream_t>(s); }
 
+// ------------------------------------------------------ in-kernel hand-off --
+// A message between co-located parties handed over inside the kernels
+// (aby3g_handoff): the producer stores the payload write-through (sc1) --
+// hs_store / hs_store2 -- and, once every storing wave has drained its
+// stores, one lane stores flags[chunk] = seq (sc1); a consumer workgroup polls
+// the flags of the chunks it reads (one lane, relaxed sc1 loads, s_sleep)
+// and then reads the payload with sc1 loads (hs_load / hs_load2), which
+// bypass its CU's L1 -- the R1 form of the guides' inter-workgroup recipe,
+// no release or acquire fence. A wait gives up after kHandoffTimeoutTicks of
+// the 100 MHz wall clock (a peer stream that cannot progress, e.g. two
+// streams sharing a hardware queue), counts the timeout in the process's
+// status word and lets every later wait on the device give up at once: the results are
+// then wrong, never hung, and the host raises an error (aby3g_handoff_status).
+typedef __attribute__((address_space(1))) u64 gu64;
+typedef __attribute__((address_space(1))) u32 gu32;
+typedef u32 v4u32 __attribute__((ext_vector_type(4)));
+constexpr u64 kHandoffTimeoutTicks = 500000000ull;  // 5 s
+constexpr u64 kHandoffRows = ABY3G_HANDOFF_ROWS;
+
+// the current device's hand-off status word (device memory): timeouts so far
+u32* handoff_status_word();
+
+struct HsWait {
+    const u64* flags;  // null: nothing to wait for
+    u64 seq;
+    u64* ticks;        // optional: wall-clock ticks the first workgroup waited
+    u32* status;
+};
+struct HsPost {
+    u64* flags;  // null: nothing to publish
+    u64 seq;
+};
+inline HsWait hs_wait_arg(const aby3g_handoff* h) {
+    if (!h || !h->flags) return HsWait{nullptr, 0, nullptr, nullptr};
+    return HsWait{h->flags, h->seq, h->wait_ticks, handoff_status_word()};
+}
+inline HsPost hs_post_arg(const aby3g_handoff* h) {
+    if (!h || !h->flags) return HsPost{nullptr, 0};
+    return HsPost{h->flags, h->seq};
+}
+
+// One lane waits until flags[c] >= seq for c in [c0, c1); the workgroup
+// leaves together. Returns false after a timeout (here or elsewhere).
+__device__ __forceinline__ bool hs_wait(const HsWait& w, u64 c0, u64 c1) {
+    if (!w.flags) return true;
+    __shared__ u32 ok;
+    if (threadIdx.x == 0) {
+        const u64 t0 = wall_clock64();
+        u32 good = 1;
+        for (u64 c = c0; c < c1 && good; ++c) {
+            for (u32 spins = 0; __hip_atomic_load((const gu64*)w.flags + c, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT) < w.seq;) {
+                __builtin_amdgcn_s_sleep(1);
+                if ((++spins & 63) == 0) {
+                    if (__hip_atomic_load((gu32*)w.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                        good = 0;
+                        break;
+                    }
+                    if (wall_clock64() - t0 > kHandoffTimeoutTicks) {
+                        __hip_atomic_fetch_add((gu32*)w.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        good = 0;
+                        break;
+                    }
+                }
+            }
+        }
+        if (w.ticks && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0)
+            __hip_atomic_fetch_add((gu64*)w.ticks, wall_clock64() - t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = good;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the payload loads below the poll
+    __syncthreads();
+    return ok != 0;
+}
+
+// Every storing wave drains its write-through stores, then one lane
+// publishes flags[c] = seq for c in [c0, c1). Call from every thread.
+__device__ __forceinline__ void hs_post(const HsPost& p, u64 c0, u64 c1) {
+    if (!p.flags) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        for (u64 c = c0; c < c1; ++c)
+            __hip_atomic_store((gu64*)p.flags + c, p.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// write-through payload stores / L1-bypassing payload loads (8 and 16 bytes)
+__device__ __forceinline__ void hs_store(u64* p, u64 v) {
+    __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ u64 hs_load(const u64* p) {
+    return __hip_atomic_load((const gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// 16 B at byte offset `off` (< 4 GiB) of `base` (wave-uniform), sc1
+__device__ __forceinline__ void hs_store2(void* base, u32 off, u64 a, u64 b) {
+    const auto r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0xffffffffu, 0x00020000);
+    const v4u32 v = {(u32)a, (u32)(a >> 32), (u32)b, (u32)(b >> 32)};
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
+}
+__device__ __forceinline__ void hs_load2(const void* base, u32 off, u64& a, u64& b) {
+    const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0xffffffffu, 0x00020000);
+    const v4u32 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
+    a = (u64)v.x | ((u64)v.y << 32);
+    b = (u64)v.z | ((u64)v.w << 32);
+}
+
 // The calling thread's current device as last set through aby3g_set_device
 // (queried from HIP once per thread otherwise). Threads that drive the
 // library switch devices only through aby3g_set_device.

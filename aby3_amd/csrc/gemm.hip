@@ -8,8 +8,9 @@
 //   sum_{s=0..7} 2^(8s) * sum_{p+q=s} A_p . B_q
 // i.e. 36 int8 digit-pair GEMMs accumulated into 8 exact i32 planes
 // (|plane| <= 8 * K' * 2^14 < 2^31 for K' <= 8192 per split) and recombined
-// in i64 in the epilogue. MFMA: v_mfma_i32_32x32x32_i8, one 32x32 output tile
-// and 8 planes (128 accumulator VGPRs) per wave, 2x2 waves per 64x64 tile.
+// in i64 in the epilogue. MFMA: v_mfma_i32_16x16x64_i8 (k_share_gemm16s), a
+// 128 x 64 output tile per 512-thread workgroup, each wave a 32 x 32 tile of
+// 2 x 2 16x16 blocks with 8 planes (128 accumulator VGPRs).
 //
 // Digit layout in HBM (built once per call by k_digits_*): for every row of
 // A (resp. column of B) and every 32-wide slice of K', the 8 planes x 32
@@ -36,27 +37,11 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 constexpr u32 BN = 64, BK = 32;  // output tile width, K' per stage
 constexpr u32 kRec = 256;        // bytes per (row, stage) record
 
-// Share-GEMM kernel (ABY3G_GEMM_VARIANT, for A/B runs): default the
-// staggered 16x16x64 kernel (k_share_gemm16s); 'b' the 32x32x32 kernel
-// (k_share_gemm) it replaced.
-inline char gemm_variant() {
-    static const char v = [] {
-        const char* e = getenv("ABY3G_GEMM_VARIANT");
-        return (e && e[0] == 'b') ? 'b' : 's';
-    }();
-    return v;
-}
 constexpr u32 TBM = 128;  // output tile height (8 waves of 32 x 32)
 // Share GEMMs of this many parties run side by side on the calling thread's
 // device (aby3g_set_gemm_sharing): split-K fills 1/k of the CUs per GEMM.
 thread_local u32 t_gemm_sharing = 1;
-inline u32 gemm_target_wgs() {
-    static const int env = [] {
-        const char* e = getenv("ABY3G_GEMM_WGS");  // override, for A/B runs
-        return e ? atoi(e) : 0;
-    }();
-    return env > 0 ? (u32)env : 256u / t_gemm_sharing;
-}
+inline u32 gemm_target_wgs() { return 256u / t_gemm_sharing; }
 
 inline u64 roundup(u64 x, u64 m) { return (x + m - 1) / m * m; }
 
@@ -294,127 +279,7 @@ __device__ __forceinline__ TileCoord tile_of(u32 pid, u32 TM, u32 TN, u32 splits
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
 
-// k_share_gemm ('b', the previous default): one 128 x 64 output tile over
-// the K' stages [s0, s1) of its split; 8 waves (two per SIMD), each a 32 x 32
-// tile with 8 digit-plane accumulators, v_mfma_i32_32x32x32_i8.
-//
-// Staging: LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction)
-// into an NBUF-deep ring of stages. The LDS image is lane-linear, so the bank
-// swizzle (chunk g of row r at slot g ^ (r&15)) is applied on the per-lane
-// SOURCE address. Stage i + NBUF - 1 is issued right after the barrier of
-// stage i; the wait is a counted vmcnt (the pieces of the later stages stay
-// in flight) and the barrier a raw s_barrier, so the DMA is not drained by
-// it. Measured (4096^3, random digits): 49-52 % of the spec int8 peak, and
-// 58 % with the DMA removed -- its 32x32x32 MFMAs alone, fragments in
-// registers, sustain only 56 % on random operands (scripts/mfma_peak.hip).
-//
-// Epilogue: recombine the 8 planes in i64; one split -> out = product (-
-// sub), several -> the split's slab of P.
-template <u32 NBUF>
-__global__ void __launch_bounds__(512, 1)
-    k_share_gemm(const u8* __restrict__ Ad, const u8* __restrict__ Bd, u64 M, u64 N, u64 stagesTotal,
-                 u64 stagesPerSplit, u32 TM, u32 TN, u32 splits, i64* __restrict__ P, const i64* __restrict__ sub) {
-    constexpr u32 kWaves = 8, kT = 512;
-    constexpr u32 kStageA = TBM * kRec, kStageB = BN * kRec, kStage = kStageA + kStageB;
-    constexpr u32 kPiecesA = TBM / 4, kPieces = kPiecesA + BN / 4, kPerWave = kPieces / kWaves;
-    static_assert(kPieces % kWaves == 0, "pieces must split evenly over waves");
-    __shared__ __attribute__((aligned(16))) u8 lds[NBUF * kStage];  // [buf][A rows | B rows][256 B]
-    const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const TileCoord tc = tile_of(blockIdx.x, TM, TN, splits);
-    const u64 m0 = (u64)tc.tm * TBM, n0 = (u64)tc.tn * BN;
-    const u64 s0 = (u64)tc.split * stagesPerSplit;
-    const u64 s1 = min(stagesTotal, s0 + stagesPerSplit);
-    i64* dst = P + (splits > 1 ? (u64)tc.split * M * N : 0);
-    if (s0 >= s1) {
-        // empty split: still define its slab
-        for (u32 i = tid; i < TBM * BN; i += kT) {
-            u64 m = m0 + i / BN, n = n0 + i % BN;
-            if (m < M && n < N) dst[m * N + n] = 0;
-        }
-        return;
-    }
-    const u32 nst = (u32)(s1 - s0);
-
-    // this wave's DMA pieces: piece q covers 4 records (A rows, then B rows)
-    const u32 lrow = lane >> 4, lslot = lane & 15;
-    const u8* src[kPerWave];
-    u32 ldsOff[kPerWave];
-#pragma unroll
-    for (u32 j = 0; j < kPerWave; ++j) {
-        const u32 q = wave * kPerWave + j;
-        const bool isA = q < kPiecesA;
-        const u32 r = 4 * (isA ? q : q - kPiecesA) + lrow;
-        const u32 g = lslot ^ (r & 15);
-        src[j] = (isA ? Ad + (m0 + r) * stagesTotal * kRec : Bd + (n0 + r) * stagesTotal * kRec) + g * 16;
-        ldsOff[j] = (isA ? 0 : kStageA) + 4 * (isA ? q : q - kPiecesA) * kRec;
-    }
-    auto issue = [&](u64 st, u32 buf) {
-#pragma unroll
-        for (u32 j = 0; j < kPerWave; ++j)
-            __builtin_amdgcn_global_load_lds((glb_void*)(src[j] + st * kRec), (lds_void*)(lds + buf * kStage + ldsOff[j]),
-                                             16, 0, 0);
-    };
-
-    v16i acc[8];
-#pragma unroll
-    for (int s = 0; s < 8; ++s) acc[s] = v16i{0};
-
-    const u32 wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
-    const u32 fr = lane & 31, fh = lane >> 5;
-    const u32 rowA = wr + fr, rowB = wc + fr;
-    u32 offRA[8], offRB[8];
-#pragma unroll
-    for (int p = 0; p < 8; ++p) {
-        const u32 g = 2 * p + fh;
-        offRA[p] = rowA * kRec + ((g ^ (rowA & 15)) * 16);
-        offRB[p] = kStageA + rowB * kRec + ((g ^ (rowB & 15)) * 16);
-    }
-
-#pragma unroll
-    for (u32 k = 0; k + 1 < NBUF; ++k)
-        if (k < nst) issue(s0 + k, k);
-    u32 buf = 0;
-    for (u32 i = 0; i < nst; ++i) {
-        // stage i landed: leave the pieces of the stages issued after it in flight
-        if (NBUF == 3 && i + 1 < nst)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPerWave) : "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        const u8* ls = lds + buf * kStage;
-        v4i a[8], b[8];
-        if (i + NBUF - 1 < nst) issue(s0 + i + NBUF - 1, (buf + NBUF - 1) % NBUF);
-#pragma unroll
-        for (int p = 0; p < 8; ++p) {
-            a[p] = *reinterpret_cast<const v4i*>(ls + offRA[p]);
-            b[p] = *reinterpret_cast<const v4i*>(ls + offRB[p]);
-        }
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-#pragma unroll
-            for (int p = 0; p <= s; ++p)
-                acc[s] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[p], b[s - p], acc[s], 0, 0, 0);
-        }
-        buf = buf + 1 == NBUF ? 0 : buf + 1;
-    }
-
-    // recombine planes in i64 and store
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        u64 v = 0;
-#pragma unroll
-        for (int s = 0; s < 8; ++s) v += (u64)(i64)acc[s][r] << (8 * s);
-        const u64 m = m0 + wr + (r & 3) + 8 * (r >> 2) + 4 * fh;
-        const u64 n = n0 + wc + fr;
-        if (m < M && n < N) {
-            const u64 i = m * N + n;
-            if (sub) v -= (u64)sub[i];
-            dst[i] = (i64)v;
-        }
-    }
-}
-
-// k_share_gemm16s (default): the same 128 x 64 tile and records with
+// k_share_gemm16s: one 128 x 64 output tile over the K' stages of its split,
 // v_mfma_i32_16x16x64_i8, which sustains ~1.5x the int8 rate of the 32x32x32
 // form on gfx950 with random operands (scripts/mfma_peak.hip: 87 % vs 56 % of
 // the spec peak). Each wave's 32 x 32 tile is 2 x 2 16x16 blocks. One MFMA
@@ -577,8 +442,11 @@ __global__ void __launch_bounds__(512, 1)
 
 // Optional turn-taking of share-GEMM launches on one device (in issue order,
 // whichever stream issues them) through a device-wide event chain (stream
-// waits on the previous GEMM's completion event; no host sync). Measured
-// slower for co-located parties than letting their GEMMs overlap, so off.
+// waits on the previous GEMM's completion event; no host sync): bench.py's
+// roofline pass uses it (aby3g_mfma_turn) so that a launch's event span is
+// its own. Off otherwise: letting co-located parties' GEMMs overlap measured
+// +6 % on C2 -- the next GEMM's workgroups fill the CUs the previous one's
+// tail frees.
 class MfmaTurn {
 public:
     explicit MfmaTurn(hipStream_t s) : s_(s) {
@@ -602,16 +470,8 @@ public:
         mu().unlock();
     }
 
-private:
-    // off by default (ABY3G_MFMA_TURN=1 turns it on, for A/B runs): letting
-    // co-located parties' GEMMs overlap measured +6 % on C2 -- the next
-    // GEMM's workgroups fill the CUs that the previous one's tail frees
-public:
     static std::atomic<int>& mode() {
-        static std::atomic<int> on{[] {
-            const char* e = getenv("ABY3G_MFMA_TURN");
-            return (e && e[0] == '1') ? 1 : 0;
-        }()};
+        static std::atomic<int> on{0};
         return on;
     }
 
@@ -681,12 +541,8 @@ void run_share_gemm(const GemmPlan& p, const Workspace& w, hipStream_t s, i64* o
     const i64* sb = direct ? sub : nullptr;
     const dim3 grid(TM * TN * p.splits);
     const u64 sps = p.kPerSplit / BK;
-    if (gemm_variant() == 'b')
-        launch(PROBE_GEMM, k_share_gemm<2>, grid, dim3(512), 0, s, (const u8*)w.Ad, (const u8*)w.Bd, p.M, p.N, stages,
-               sps, TM, TN, p.splits, dst, sb);
-    else
-        launch(PROBE_GEMM, k_share_gemm16s, grid, dim3(512), 0, s, (const u8*)w.Ad, (const u8*)w.Bd, p.M, p.N, stages,
-               sps, TM, TN, p.splits, dst, sb);
+    launch(PROBE_GEMM, k_share_gemm16s, grid, dim3(512), 0, s, (const u8*)w.Ad, (const u8*)w.Bd, p.M, p.N, stages, sps,
+           TM, TN, p.splits, dst, sb);
 }
 
 // Runs the digit split and the MFMA GEMM.

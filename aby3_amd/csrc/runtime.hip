@@ -92,7 +92,20 @@ const Tables& tables() {
 
 std::mutex g_tab_mu;
 std::map<int, u32*> g_tab_dev;
+std::map<int, u32*> g_status_dev;  // per device: in-kernel hand-off timeouts (under g_tab_mu)
 }  // namespace
+
+u32* handoff_status_word() {
+    const int dev = current_device();
+    std::lock_guard<std::mutex> lk(g_tab_mu);
+    auto it = g_status_dev.find(dev);
+    if (it != g_status_dev.end()) return it->second;
+    u32* p = nullptr;
+    ABY3G_CHECK_HIP(hipMalloc(&p, 256));
+    ABY3G_CHECK_HIP(hipMemset(p, 0, 256));  // synchronous; the word is read only by later launches
+    g_status_dev[dev] = p;
+    return p;
+}
 
 void set_error(const std::string& msg) { t_err = msg; }
 thread_local int t_device = -1;
@@ -297,6 +310,17 @@ int aby3g_stream_write_value(aby3g_stream stream, uint64_t* word, uint64_t value
 int aby3g_stream_wait_value(aby3g_stream stream, uint64_t* word, uint64_t value) {
     return guarded(
         [&] { ABY3G_CHECK_HIP(hipStreamWaitValue64(S(stream), word, value, hipStreamWaitValueGte, ~0ull)); });
+}
+
+int aby3g_handoff_status(uint32_t* timeouts) {
+    return guarded([&] {
+        ABY3G_REQUIRE(timeouts != nullptr, "null argument");
+        u32* w = handoff_status_word();
+        ABY3G_CHECK_HIP(hipDeviceSynchronize());
+        ABY3G_CHECK_HIP(hipMemcpy(timeouts, w, sizeof(u32), hipMemcpyDeviceToHost));
+        if (*timeouts) ABY3G_CHECK_HIP(hipMemset(w, 0, sizeof(u32)));
+        ABY3G_CHECK_HIP(hipDeviceSynchronize());
+    });
 }
 
 static_assert(sizeof(aby3g_ipc_handle) == sizeof(hipIpcMemHandle_t), "IPC handle size");

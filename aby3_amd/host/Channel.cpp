@@ -202,6 +202,23 @@ struct Pipe {
         w.device = gpu.device();
         if (bytes) {
             int k = -1;
+            u64 staged = 0;
+            for (const LinkSlot& ls : lslots) staged += ls.cap;
+            for (size_t i = 0; i < lslots.size() && k < 0; ++i)
+                if (lslots[i].cap >= bytes && link->posted((u32)i).load(std::memory_order_acquire) >= lslots[i].lastSeq)
+                    k = (int)i;
+            if (k < 0 && (lslots.size() >= LinkEnd::kMaxSlots || staged + bytes > LinkEnd::kMaxStagedBytes) &&
+                !lslots.empty()) {
+                // every slot holds a message the receiver has not taken yet and
+                // no more may be added: wait (up to the link timeout) until it
+                // takes the oldest one -- messages are taken in order, so a
+                // sender that runs ahead (party 2 of a truncating asyncMul only
+                // sends) is throttled instead of failing
+                size_t oldest = 0;
+                for (size_t i = 1; i < lslots.size(); ++i)
+                    if (lslots[i].lastSeq < lslots[oldest].lastSeq) oldest = i;
+                link->waitPosted((u32)oldest, lslots[oldest].lastSeq);
+            }
             for (size_t i = 0; i < lslots.size() && k < 0; ++i)
                 if (lslots[i].cap >= bytes && link->posted((u32)i).load(std::memory_order_acquire) >= lslots[i].lastSeq)
                     k = (int)i;
@@ -214,7 +231,6 @@ struct Pipe {
                     lslots[i].ptr = nullptr;
                 }
             if (k < 0) {
-                if (lslots.size() >= LinkEnd::kMaxSlots) throw std::runtime_error("link: too many messages in flight");
                 lslots.emplace_back();
                 k = (int)lslots.size() - 1;
             }
@@ -449,19 +465,21 @@ void Channel::resetStats() {
 double recvWaitUs() { return t_recvWaitUs; }
 
 // Stream-ordered signal words are waited for by a spinning blit kernel: a
-// tool that serialises kernels (rocprofv3 --pmc, AMD_SERIALIZE_KERNEL) would
-// run the waiting kernel alone and never the writer -- there the channels use
-// events. ABY3G_CHANNEL_SIGNAL=0 turns the signal words off explicitly.
-static bool signalWordsAllowed() {
-    static const bool ok = [] {
-        const char* e = getenv("ABY3G_CHANNEL_SIGNAL");
-        if (e && e[0] == '0') return false;
-        const char* ser = getenv("AMD_SERIALIZE_KERNEL");
-        if (ser && ser[0] && ser[0] != '0') return false;
-        return true;
+// tool that serialises kernels (rocprofv3 --pmc, which sets
+// ROCPROF_COUNTER_COLLECTION in the profiled process; AMD_SERIALIZE_KERNEL)
+// would run the waiting kernel alone and never the writer -- there the
+// channels use events.
+bool kernelsSerialized() {
+    static const bool ser = [] {
+        for (const char* v : {"AMD_SERIALIZE_KERNEL", "ROCPROF_COUNTER_COLLECTION"}) {
+            const char* e = getenv(v);
+            if (e && e[0] && e[0] != '0') return true;
+        }
+        return false;
     }();
-    return ok;
+    return ser;
 }
+static bool signalWordsAllowed() { return !kernelsSerialized(); }
 
 std::vector<CommPkg> makeLocalRing(const int* devices) {
     // parties on different devices read each other's buffers in place

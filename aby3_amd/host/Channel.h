@@ -88,6 +88,11 @@ struct CommPkg {
 // Host time this thread has spent inside receives waiting for messages (us).
 double recvWaitUs();
 
+// True when a profiler or the runtime serialises kernels (rocprofv3 --pmc,
+// AMD_SERIALIZE_KERNEL): no kernel or blit may then wait on another stream's
+// progress on the device, so channels hand off through events.
+bool kernelsSerialized();
+
 // Three in-process parties connected in a ring: result[i].mNext talks to
 // party i+1, result[i].mPrev to party i-1. With `devices` (party i runs on
 // devices[i]), device payloads between parties on one device are signalled

@@ -95,6 +95,8 @@ LinkEnd::~LinkEnd() {
 
 std::atomic<u64>& LinkEnd::posted(u32 slot) { return mHdr->posted[slot]; }
 
+void LinkEnd::waitPosted(u32 slot, u64 seq) const { waitFor("a free staging slot", mHdr->posted[slot], seq); }
+
 void LinkEnd::write(const void* src, size_t n) {
     const u8* s = (const u8*)src;
     u64 head = mHdr->head.load(std::memory_order_relaxed);

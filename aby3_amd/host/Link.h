@@ -24,6 +24,7 @@ namespace aby3 {
 class LinkEnd {
 public:
     static constexpr u32 kMaxSlots = 480;      // staging slots per direction
+    static constexpr size_t kMaxStagedBytes = 2ull << 30;  // device bytes of staging per direction
     static constexpr size_t kRingBytes = 4u << 20;
 
     // name: the segment's shm name ("/aby3.<link>.<from>.<to>"); both ends
@@ -43,6 +44,8 @@ public:
     u64* consumedDev(u32 slot) const { return mSigDev + 8 + slot; }
     // host words: the receiver has enqueued the copy-out of slot k's message `seq`
     std::atomic<u64>& posted(u32 slot);
+    // blocks (up to timeoutS()) until posted(slot) >= seq
+    void waitPosted(u32 slot, u64 seq) const;
 
     static double timeoutS();
 

@@ -442,14 +442,6 @@ struct Session {
         turnCv.notify_all();
     }
 
-    static bool drawStreamsOn() {
-        static const bool on = [] {
-            const char* e = getenv("ABY3G_DRAW_STREAM");  // 0: draws stay on the party's stream (A/B runs)
-            return !(e && e[0] == '0');
-        }();
-        return on;
-    }
-
     void worker(int i, int device, int probe) {
         PartyCtx p;
         u64 seen = 0;
@@ -468,7 +460,7 @@ struct Session {
             // (only for parties sharing this process: one party per process
             // with a second stream each put six queues on the device, measured
             // 5x slower on C3)
-            if (colocated && locals.size() > 1 && drawStreamsOn()) {
+            if (colocated && locals.size() > 1) {
                 std::shared_ptr<Gpu::SharedStream> ds;
                 {
                     std::unique_lock<std::mutex> lk(turnMu);

@@ -374,27 +374,17 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
         mSendAll.reset();
         mAndDone = 0;
     }
-    static const bool sendAll = [] {
-        const char* e = getenv("ABY3G_SEND_ALL");  // 0: a buffer and a fence per level (A/B runs)
-        return !(e && e[0] == '0');
-    }();
     std::shared_ptr<DeviceBuffer> send;
-    if (nAnd && sendAll) {
+    if (nAnd) {
         if (!mSendAll) mSendAll = std::make_shared<DeviceBuffer>(g, (u64)mCir->mAndCount * rowBytes);
         send = DeviceBuffer::view(mSendAll, mAndDone * rowBytes, nAnd * rowBytes);
-    } else if (nAnd) {
-        send = std::make_shared<DeviceBuffer>(g, nAnd * rowBytes);
     }
     mAndDone += nAnd;
     if (nb && mZPending) waitZ();
     if (nb || nUnpack) {
         const aby3g_gate* gl = nb ? mCur->gates + mCur->levelFirstGate[mLevel] : nullptr;
         const u32* be = nb ? mCur->batchEnds + mCur->levelBatchOffset[mLevel] : nullptr;
-        static const bool useRr = [] {
-            const char* e = getenv("ABY3G_LEVEL_RR");  // 0: gates wait for the unpack (A/B runs)
-            return !(e && e[0] == '0');
-        }();
-        const u32* rr = (useRr && nb && recv) ? mCur->recvRows + 2 * (u64)mCur->levelFirstGate[mLevel] : nullptr;
+        const u32* rr = (nb && recv) ? mCur->recvRows + 2 * (u64)mCur->levelFirstGate[mLevel] : nullptr;
         GPU_CALL(aby3g_bin_level_rr(gl, rr, be, nb, recv ? recv->as<u64>() : nullptr,
                                     nUnpack ? mCur->outWires[mLevel - 1] : nullptr, nUnpack, mMem.as<u64>(), W, mWords,
                                     mZPtr, send ? send->as<u64>() : nullptr, g.stream()));
@@ -404,7 +394,7 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
         // views of one sender buffer: fenced after the last of them is read
         bool last = true;
         for (size_t L = mLevel; L < mCir->mLevelAndCounts.size() && last; ++L) last = mCir->mLevelAndCounts[L] == 0;
-        if (last || !sendAll) recv->fence(g.stream());
+        if (last) recv->fence(g.stream());
     }
     if (nAnd) {
         comm.mNext.asyncSendShared(send, nAnd * rowBytes, g);

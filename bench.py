@@ -61,6 +61,9 @@ def parse():
     ap.add_argument("--cpu-reps", type=int, default=10)
     ap.add_argument("--no-extras", action="store_true", help="skip the LR-iteration and merge-layer lines")
     ap.add_argument("--lr-rows", type=int, default=1000000)
+    ap.add_argument("--gemm-turns", action="store_true",
+                    help="co-located parties' share GEMMs take turns in every pass (aby3g_mfma_turn), so that a "
+                         "profiler's launch spans are the kernel's own (scripts/gpu_profile.sh)")
     ap.add_argument("--deployment", choices=("replicas", "parties"), default="replicas",
                     help="replicas: every rank runs a whole 3-party job on its GPU; parties: every 3 ranks form "
                          "one job, one party per rank and GPU (the north_star layout; world size a multiple of 3)")
@@ -403,7 +406,12 @@ def main_parties(args, world, rank, local, pg, nt):
     party, group = rank % 3, rank // 3
     colocated = n.value < 3
     M, K, N, D = args.m, args.k, args.n, args.decimal
-    link = f"bench{os.environ.get('MASTER_PORT', '0')}.{group}"
+    # a per-launch nonce in the link name (rank 0's, broadcast): a rerun never
+    # attaches to a segment a killed run left behind under the same port
+    nonce = [os.urandom(4).hex()]
+    if pg is not None:
+        pg.broadcast_object_list(nonce, src=0)
+    link = f"bench{os.environ.get('MASTER_PORT', '0')}.{nonce[0]}.{group}"
     s = nt.Session.party(nt.JOB_MUL_TRUNC, [M, K, N, D, 1], party, link, device=dev, colocated=colocated)
     s.run(2)
     ok = s.check()
@@ -456,6 +464,8 @@ def main():
     nt.lib().device_count(ctypes.byref(ndev))
     dev = local % max(ndev.value, 1)  # one GPU per rank, also when each rank sees only its own
     M, K, N, D = args.m, args.k, args.n, args.decimal
+    if args.gemm_turns:
+        nt.lib().mfma_turn(1)
     # only the share-GEMM launches carry timing events (the roofline kernel);
     # digit and epilogue times come from a second, separately probed pass
     progress("C2 asyncMul + truncation session")
@@ -487,7 +497,7 @@ def main():
         rp.probe_reset()
         rp.run(30)
         gemm_ms, gemm_n = rp.probe(nt.PROBE_GEMM)
-    nt.lib().mfma_turn(0)
+    nt.lib().mfma_turn(1 if args.gemm_turns else 0)
     # kernel-time breakdown from a separate pass with every family probed
     # (event pairs around every launch perturb the timing, so not the timed run)
     with nt.Session(nt.JOB_MUL_TRUNC, [M, K, N, D, 1], devices=(dev, dev, dev), probe=True) as bd:

@@ -81,6 +81,32 @@ int aby3g_signal_alloc(uint64_t** word); /* zeroed, on the current device */
 int aby3g_stream_write_value(aby3g_stream stream, uint64_t* word, uint64_t value);
 int aby3g_stream_wait_value(aby3g_stream stream, uint64_t* word, uint64_t value);
 
+/* In-kernel hand-off between co-located parties (one device, one process;
+ * replaces the stream write + stream wait of a channel message). A message
+ * of `rows` rows is split into chunks of ABY3G_HANDOFF_ROWS rows; the kernel
+ * that produces it stores the payload write-through and, per chunk it wrote,
+ * publishes flags[chunk] = seq once its stores have drained; a kernel that
+ * consumes it waits, per workgroup and only for the chunks that workgroup
+ * reads, until flags[chunk] >= seq, and reads the payload with L1-bypassing
+ * loads. `flags` is a zeroed device array (one u64 per chunk) that a channel
+ * direction reuses with increasing seq. wait_ticks (optional, consumer side):
+ * the first workgroup's wait in 100 MHz wall-clock ticks is added there (the
+ * device-side time a party spends blocked on its peers). Entry points taking
+ * an aby3g_handoff accept NULL or flags == NULL for "no hand-off".
+ * A waiting kernel can only progress while the producer's stream has a
+ * hardware queue of its own; a wait gives up after 5 s, counts a timeout and
+ * makes every later wait on the device give up too (wrong results, no hang). */
+#define ABY3G_HANDOFF_ROWS 2048
+typedef struct {
+    uint64_t* flags;
+    uint64_t seq;
+    uint64_t* wait_ticks;
+} aby3g_handoff;
+/* Timed-out hand-off waits on the current device since the last call, then
+ * resets the count (synchronizes the device). Nonzero: results since the
+ * last call are invalid. */
+int aby3g_handoff_status(uint32_t* timeouts);
+
 /* Cross-process transport: one party per process (the
  * reference's parties are processes joined by cryptoTools Channels over TCP,
  * Sh3Types.h:32-34, Eval/dis_exec.sh:10-12). A channel's staging slots are
@@ -176,7 +202,7 @@ typedef struct {
 } aby3g_trunc_streams;
 
 /* Share-GEMM launches on one device take turns (1) or may overlap (0, the
- * default; ABY3G_MFMA_TURN=1 sets the initial mode): co-located parties'
+ * default): co-located parties'
  * overlapping GEMMs finish sooner together, but a launch's span then includes
  * the CUs spent on the others' -- bench.py's roofline pass takes turns. */
 int aby3g_mfma_turn(int on);

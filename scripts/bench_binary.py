@@ -1,8 +1,7 @@
 """Standalone timings of the binary engine's bit-slicing passes at C3's size
 (2^20 rows, one stream, nothing beside them): the two-input resharing
 transpose (party 0's four sources), the plain two-share transposes and the
-output transposes, with their algorithmic byte rates and output checksums
-(run once per ABY3G_B2W variant and compare)."""
+output transposes, with their algorithmic byte rates and output checksums."""
 import ctypes
 import os
 import sys

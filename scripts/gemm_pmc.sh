@@ -1,12 +1,12 @@
 #!/bin/bash
-# one PMC pass per variant over the standalone share GEMM: gemm_pmc.sh <size> <counters> <variants...>
+# one PMC pass over the standalone share GEMM: gemm_pmc.sh <size> <counters>
 R=$GRAFT_REPO_ROOT
-SZ=$1; CT=$2; shift 2
+SZ=$1; CT=$2
 cd /tmp && export TMPDIR=/tmp
-for v in "$@"; do
+for v in gemm; do
   O=$R/gpurun_out/pmc_$v
   mkdir -p $O
-  ABY3G_GEMM_VARIANT=$v timeout -s KILL 120 rocprofv3 --pmc $CT --output-format csv -d $O -o run -- python3 $R/scripts/bench_gemm.py $SZ > $O/log 2>&1 || exit $?
+  timeout -s KILL 120 rocprofv3 --pmc $CT --output-format csv -d $O -o run -- python3 $R/scripts/bench_gemm.py $SZ > $O/log 2>&1 || exit $?
   python3 - $O <<'PY'
 import csv, collections, sys, glob
 f = glob.glob(sys.argv[1] + "/**/run_counter_collection.csv", recursive=True)[0]

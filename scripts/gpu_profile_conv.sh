@@ -10,7 +10,7 @@ for job in a2b bitinj; do
   timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$job -o run -- \
       python3 $R/scripts/prof_job.py --job $job --steps 10 > $O/trace_$job.log 2>&1 || exit $?
   for c in FETCH_SIZE WRITE_SIZE; do
-    ABY3G_CHANNEL_SIGNAL=0 timeout -k 10 120 rocprofv3 --pmc $c --output-format csv -d $O/pmc_${job}_$c -o run -- \
+    timeout -k 10 120 rocprofv3 --pmc $c --output-format csv -d $O/pmc_${job}_$c -o run -- \
         python3 $R/scripts/prof_job.py --job $job --steps 4 > $O/pmc_${job}_$c.log 2>&1 || exit $?
   done
 done

@@ -67,6 +67,70 @@ static void mulTest(MulMode mode, u64 M, u64 K, u64 N, bool trunc, u64 d, u64 se
     }
 }
 
+// Sh3_Evaluator_asyncMul_test (Sh3EvaluatorTests.cpp:20-135): per trial, ten
+// dependent multiplications chained through Sh3Task::then,
+//   task = asyncMul(task, A, B, C); task = task.then(A = C + A);
+// with one .get() at the end; every party's shares of C and A are compared
+// with the oracle's after the chain, and the revealed C with the plaintext
+// recurrence c = a * b; a = c + a (mod 2^64).
+static void chainedMulTest(MulMode mode, u64 dim, u64 trials, u64 seed) {
+    const orc::MulMode om = mode == MulMode::Gemm ? orc::MUL_GEMM : orc::MUL_HADAMARD;
+    for (u64 t = 0; t < trials; ++t) {
+        i64Matrix a = randMat(dim, dim, seed + 2 * t), b = randMat(dim, dim, seed + 2 * t + 1);
+        ShareSink gotC, gotA;
+        std::vector<i64> revealed;
+        run3([&](harness::Party& p) {
+            si64Matrix A(dim, dim), B(dim, dim), C(dim, dim);
+            if (p.idx == 0) {
+                p.enc.localIntMatrix(p.rt, a, A).get();
+                p.enc.localIntMatrix(p.rt, b, B).get();
+            } else {
+                p.enc.remoteIntMatrix(p.rt, A).get();
+                p.enc.remoteIntMatrix(p.rt, B).get();
+            }
+            Sh3Task task = p.rt.noDependencies();
+            for (u64 j = 0; j < dim; ++j) {
+                task = p.eval.asyncMul(task, A, B, C, mode);
+                task = task.then([&](CommPkg&, Sh3Task& self) {
+                    // A = C + A, both shares (sMatrix operator+)
+                    GPU_CALL(aby3g_i64_lincomb(2 * A.size(), 1, C.data(), 1, A.data(), 0, A.data(),
+                                               self.getRuntime().gpu().stream()));
+                });
+            }
+            task.get();
+            gotC.put(p.idx, C);
+            gotA.put(p.idx, A);
+            i64Matrix r;
+            p.enc.revealAll(p.rt, C, r).get();
+            if (p.idx == 0) revealed = r.mData;
+        });
+        auto enc = orc::makeEncryptors(0);
+        auto ev = orc::makeEvaluators(1);
+        orc::Shared A = orc::shareInt(enc, 0, toOrc(a)), B = orc::shareInt(enc, 0, toOrc(b)), C;
+        for (u64 j = 0; j < dim; ++j) {
+            C = orc::mul(ev, om, A, B);
+            for (int p = 0; p < 3; ++p)
+                for (int k = 0; k < 2; ++k)
+                    for (u64 i = 0; i < A[p].s[k].v.size(); ++i)
+                        A[p].s[k].v[i] = (i64)((u64)C[p].s[k].v[i] + (u64)A[p].s[k].v[i]);
+        }
+        gotC.expectEq(C, "chained asyncMul: C");
+        gotA.expectEq(A, "chained asyncMul: A = C + A");
+        // plaintext recurrence
+        orc::SMat As, Bs;
+        As.s[0] = toOrc(a);
+        As.s[1] = orc::Mat(dim, dim);
+        Bs.s[0] = toOrc(b);
+        Bs.s[1] = orc::Mat(dim, dim);
+        orc::Mat c;
+        for (u64 j = 0; j < dim; ++j) {
+            orc::localProduct(om, As, Bs, c);
+            for (u64 i = 0; i < c.size(); ++i) As.s[0].v[i] = (i64)((u64)c.v[i] + (u64)As.s[0].v[i]);
+        }
+        check(revealed == c.v, "chained asyncMul: revealed C differs from the plaintext recurrence");
+    }
+}
+
 static void bitMulTest(bool pub, u64 n, u64 seed) {
     i64Matrix a = randMat(n, 1, seed), bits = randMat(n, 1, seed + 7, 0, 1);
     const i64 apub = 0x123456789abcdefll;
@@ -188,6 +252,11 @@ int main() {
     test("asyncMul_trunc_gemm_alias_C_is_A_512_D16", [] { mulTest(MulMode::Gemm, 512, 512, 512, true, 16, 13, 1); });
     test("asyncMul_trunc_gemm_alias_C_is_B_300x300x40", [] { mulTest(MulMode::Gemm, 300, 300, 40, true, 16, 14, 2); });
     test("asyncMul_trunc_hadamard_alias_C_is_B_100x7_D8", [] { mulTest(MulMode::Hadamard, 100, 7, 7, true, 8, 15, 2); });
+    // Sh3_Evaluator_asyncMul_test: 10 trials of 10 dependent 10x10 products (the
+    // reference expects the upstream GEMM; the fork's Hadamard form as well)
+    test("asyncMul_chained_then_gemm_10x10 (Sh3_Evaluator_asyncMul_test)",
+         [] { chainedMulTest(MulMode::Gemm, 10, 10, 100); });
+    test("asyncMul_chained_then_hadamard_10x10", [] { chainedMulTest(MulMode::Hadamard, 10, 10, 200); });
     test("asyncMul_si64_x_sb (sh3_asyncArithBinMul_test)", [] { bitMulTest(false, 100, 9); });
     test("asyncMul_i64_x_sb (sh3_asyncPubArithBinMul_test)", [] { bitMulTest(true, 100, 10); });
     test("asyncMul_si64_x_sb_1000", [] { bitMulTest(false, 1000, 11); });

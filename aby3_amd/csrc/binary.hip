@@ -115,20 +115,22 @@ __device__ __forceinline__ bool gate_is_and(u32 t) {
 // not wait for the unpack of this launch
 __device__ __forceinline__ void gate_load(const aby3g_gate& g, uint2 rr, const u64* s0, const u64* s1,
                                           const u64* __restrict__ recv, u64 words, u64 w, const u64* __restrict__ z,
-                                          GateOps& o) {
+                                          GateOps& o, bool sc1) {  // sc1: compile-time constant at every call
     // unary gates read in0 twice (in1 of an external gate list may be anything)
     const bool unary = g.type == ABY3G_GATE_COPY || g.type == ABY3G_GATE_INV;
     const u64 in1 = unary ? g.in0 : g.in1;
     const u32 r1 = unary ? rr.x : rr.y;
     o.x0 = s0[g.in0 * words + w];
-    o.x1 = rr.x != ~0u ? recv[(u64)rr.x * words + w] : s1[g.in0 * words + w];
+    // received shares handed over in-kernel are read past this CU's L1 (sc1)
+    o.x1 = rr.x != ~0u ? (sc1 ? hs_load(recv + (u64)rr.x * words + w) : recv[(u64)rr.x * words + w])
+                       : s1[g.in0 * words + w];
     o.y0 = s0[in1 * words + w];
-    o.y1 = r1 != ~0u ? recv[(u64)r1 * words + w] : s1[in1 * words + w];
+    o.y1 = r1 != ~0u ? (sc1 ? hs_load(recv + (u64)r1 * words + w) : recv[(u64)r1 * words + w]) : s1[in1 * words + w];
     o.z = gate_is_and(g.type) ? z[(u64)g.z_row * words + w] : 0;
 }
 
 __device__ __forceinline__ void gate_eval(const aby3g_gate& g, const GateOps& o, u64* s0, u64* s1, u64 words, u64 w,
-                                          u64* __restrict__ sendbuf) {
+                                          u64* __restrict__ sendbuf, bool wt) {
     const u64 x0 = o.x0, x1 = o.x1, y0 = o.y0, y1 = o.y1;
     u64 o0, o1;
     switch (g.type) {
@@ -148,7 +150,10 @@ __device__ __forceinline__ void gate_eval(const aby3g_gate& g, const GateOps& o,
                 r = (~x0 & y0) ^ (~x0 & y1) ^ (~x1 & y0);
             r ^= o.z;
             s0[g.out * words + w] = r;
-            sendbuf[(u64)g.send_row * words + w] = r;
+            if (wt)  // a message handed over in-kernel: write-through
+                hs_store(sendbuf + (u64)g.send_row * words + w, r);
+            else
+                sendbuf[(u64)g.send_row * words + w] = r;
             return;
         }
     }
@@ -164,20 +169,31 @@ __device__ __forceinline__ void gate_eval(const aby3g_gate& g, const GateOps& o,
 constexpr u32 kLevelUnroll = 4;
 // With rrows (per gate, see gate_load) no gate reads the wires this launch
 // unpacks, so the first batch starts without a barrier after the unpack.
-template <u32 SLOTS>
+// In-kernel hand-off (co-located parties): a workgroup owns exactly one
+// ABY3G_HANDOFF_ROWS chunk (its 32 words), so it waits only for the previous
+// party's workgroup of the same rows (hw: the received AND shares) and
+// publishes its own send rows for the next party's same workgroup (hp) --
+// the levels of the three parties pipeline chunk by chunk.
+static_assert(kLevelWords * 64 == ABY3G_HANDOFF_ROWS, "a level workgroup is one hand-off chunk");
+template <u32 SLOTS, bool HS>
 __global__ void __launch_bounds__(SLOTS * 32) k_bin_level(const aby3g_gate* __restrict__ gates,
                                                          const uint2* __restrict__ rrows,
                                                          const u32* __restrict__ batch_ends, u32 nbatches,
                                                          const u64* __restrict__ recv,
                                                          const u32* __restrict__ unpack_wires, u32 nunpack,
                                                          u64* __restrict__ mem, u64 wires, u64 words,
-                                                         const u64* __restrict__ z, u64* __restrict__ sendbuf) {
+                                                         const u64* __restrict__ z, u64* __restrict__ sendbuf,
+                                                         HsWait hw, HsPost hp) {
+    // HS: the in-kernel hand-off instantiation (sc1 payload accesses, waits
+    // and posts); the other is the plain streaming kernel
+    if (HS && !hs_wait(hw, blockIdx.x, blockIdx.x + 1)) return;
     const u32 lane = threadIdx.x & 31, slot = threadIdx.x >> 5;
     const u64 w = (u64)blockIdx.x * kLevelWords + lane;
     u64* s0 = mem;
     u64* s1 = mem + wires * words;
 #pragma unroll 4
-    for (u32 j = slot; j < nunpack; j += SLOTS) s1[(u64)unpack_wires[j] * words + w] = recv[(u64)j * words + w];
+    for (u32 j = slot; j < nunpack; j += SLOTS)
+        s1[(u64)unpack_wires[j] * words + w] = (HS && hw.flags) ? hs_load(recv + (u64)j * words + w) : recv[(u64)j * words + w];
     u32 begin = 0;
     for (u32 b = 0; b < nbatches; ++b) {
         if (b || !rrows) __syncthreads();
@@ -194,13 +210,14 @@ __global__ void __launch_bounds__(SLOTS * 32) k_bin_level(const aby3g_gate* __re
                 }
 #pragma unroll
             for (u32 k = 0; k < kLevelUnroll; ++k)
-                if (g0 + k * SLOTS < end) gate_load(g[k], rr[k], s0, s1, recv, words, w, z, o[k]);
+                if (g0 + k * SLOTS < end) gate_load(g[k], rr[k], s0, s1, recv, words, w, z, o[k], HS);
 #pragma unroll
             for (u32 k = 0; k < kLevelUnroll; ++k)
-                if (g0 + k * SLOTS < end) gate_eval(g[k], o[k], s0, s1, words, w, sendbuf);
+                if (g0 + k * SLOTS < end) gate_eval(g[k], o[k], s0, s1, words, w, sendbuf, HS);
         }
         begin = end;
     }
+    if (HS) hs_post(hp, blockIdx.x, blockIdx.x + 1);
 }
 
 __global__ void __launch_bounds__(kGateBlock) k_bin_unpack(const u64* __restrict__ recv, const u32* __restrict__ outw,
@@ -598,19 +615,47 @@ int aby3g_bin_level_rr(const aby3g_gate* gates, const uint32_t* recv_rows, const
                        uint32_t nbatches, const uint64_t* recvbuf, const uint32_t* unpack_wires, uint32_t nunpack,
                        uint64_t* mem, uint64_t wires, uint64_t words, const uint64_t* z, uint64_t* sendbuf,
                        aby3g_stream stream) {
+    return aby3g_bin_level_hs(gates, recv_rows, batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words,
+                              z, sendbuf, nullptr, nullptr, stream);
+}
+
+int aby3g_bin_level_hs(const aby3g_gate* gates, const uint32_t* recv_rows, const uint32_t* batch_ends,
+                       uint32_t nbatches, const uint64_t* recvbuf, const uint32_t* unpack_wires, uint32_t nunpack,
+                       uint64_t* mem, uint64_t wires, uint64_t words, const uint64_t* z, uint64_t* sendbuf,
+                       const aby3g_handoff* wait, const aby3g_handoff* post, aby3g_stream stream) {
     const uint2* rrows = reinterpret_cast<const uint2*>(recv_rows);
     return guarded([&] {
         ABY3G_REQUIRE(!rrows || recvbuf, "recv_rows without a recv buffer");
         ABY3G_REQUIRE(words % kLevelWords == 0, "words must be padded to a multiple of 32 (2048 rows)");
+        ABY3G_REQUIRE(!(wait && wait->flags) || nunpack, "a hand-off wait without received shares");
+        ABY3G_REQUIRE(!(post && post->flags) || sendbuf, "a hand-off post without a send buffer");
         if ((!nbatches && !nunpack) || !words) return;
+        // one workgroup per chunk; in-kernel hand-offs are used only for
+        // launches of at most 64 chunks (Channel::handoffPost), so the spinning
+        // workgroups of two parties' launches never fill the device
         const u32 wgs = (u32)(words / kLevelWords);
+        const HsWait hw = hs_wait_arg(wait);
+        const HsPost hp = hs_post_arg(post);
         // few workgroups (small row counts): 32 slots per workgroup for gate parallelism
-        if (wgs < 128)
-            launch(PROBE_BINARY, k_bin_level<32>, dim3(wgs), dim3(32 * 32), 0, S(stream), gates, rrows, batch_ends,
-                   nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf);
-        else
-            launch(PROBE_BINARY, k_bin_level<8>, dim3(wgs), dim3(8 * 32), 0, S(stream), gates, rrows, batch_ends, nbatches,
-                   recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf);
+        const bool hs = hw.flags || hp.flags;
+        // with hand-offs the send rows are stored write-through and the
+        // received ones read past L1 (both ways, so one instantiation covers
+        // a launch that only waits or only posts)
+        if (wgs < 128) {
+            if (hs)
+                launch(PROBE_BINARY, k_bin_level<32, true>, dim3(wgs), dim3(32 * 32), 0, S(stream), gates, rrows,
+                       batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp);
+            else
+                launch(PROBE_BINARY, k_bin_level<32, false>, dim3(wgs), dim3(32 * 32), 0, S(stream), gates, rrows,
+                       batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp);
+        } else {
+            if (hs)
+                launch(PROBE_BINARY, k_bin_level<8, true>, dim3(wgs), dim3(8 * 32), 0, S(stream), gates, rrows,
+                       batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp);
+            else
+                launch(PROBE_BINARY, k_bin_level<8, false>, dim3(wgs), dim3(8 * 32), 0, S(stream), gates, rrows,
+                       batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp);
+        }
     });
 }
 

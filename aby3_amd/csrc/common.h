@@ -300,16 +300,18 @@ inline hipStream_t S(aby3g_stream s) { return reinterpret_cast<hipStream_t>(s); 
 // bypass its CU's L1 -- the R1 form of the guides' inter-workgroup recipe,
 // no release or acquire fence. A wait gives up after kHandoffTimeoutTicks of
 // the 100 MHz wall clock (a peer stream that cannot progress, e.g. two
-// streams sharing a hardware queue), counts the timeout in the process's
-// status word and lets every later wait on the device give up at once: the results are
-// then wrong, never hung, and the host raises an error (aby3g_handoff_status).
+// streams sharing a hardware queue), sets the device's status word (pinned
+// host memory, a plain system-scope store) and lets every later wait on the
+// device give up at once: the results are then wrong, never hung, and the
+// host raises an error (aby3g_handoff_status).
 typedef __attribute__((address_space(1))) u64 gu64;
 typedef __attribute__((address_space(1))) u32 gu32;
 typedef u32 v4u32 __attribute__((ext_vector_type(4)));
 constexpr u64 kHandoffTimeoutTicks = 500000000ull;  // 5 s
 constexpr u64 kHandoffRows = ABY3G_HANDOFF_ROWS;
 
-// the current device's hand-off status word (device memory): timeouts so far
+// the current device's hand-off status word (pinned host memory, mapped):
+// nonzero once a wait timed out
 u32* handoff_status_word();
 
 struct HsWait {
@@ -344,12 +346,12 @@ __device__ __forceinline__ bool hs_wait(const HsWait& w, u64 c0, u64 c1) {
                                                   __HIP_MEMORY_SCOPE_AGENT) < w.seq;) {
                 __builtin_amdgcn_s_sleep(1);
                 if ((++spins & 63) == 0) {
-                    if (__hip_atomic_load((gu32*)w.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    if (__hip_atomic_load(w.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
                         good = 0;
                         break;
                     }
                     if (wall_clock64() - t0 > kHandoffTimeoutTicks) {
-                        __hip_atomic_fetch_add((gu32*)w.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(w.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                         good = 0;
                         break;
                     }

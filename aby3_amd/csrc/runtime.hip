@@ -95,16 +95,19 @@ std::map<int, u32*> g_tab_dev;
 std::map<int, u32*> g_status_dev;  // per device: in-kernel hand-off timeouts (under g_tab_mu)
 }  // namespace
 
+// Pinned host memory, so neither the kernels' timeout path nor the host's
+// reads need a stream: HIP's null stream is never touched (it would take one
+// of the process's hardware queues and make two party streams share one).
 u32* handoff_status_word() {
     const int dev = current_device();
     std::lock_guard<std::mutex> lk(g_tab_mu);
     auto it = g_status_dev.find(dev);
     if (it != g_status_dev.end()) return it->second;
-    u32* p = nullptr;
-    ABY3G_CHECK_HIP(hipMalloc(&p, 256));
-    ABY3G_CHECK_HIP(hipMemset(p, 0, 256));  // synchronous; the word is read only by later launches
-    g_status_dev[dev] = p;
-    return p;
+    void* p = nullptr;
+    ABY3G_CHECK_HIP(hipHostMalloc(&p, 256, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(p, 0, 256);
+    g_status_dev[dev] = (u32*)p;
+    return (u32*)p;
 }
 
 void set_error(const std::string& msg) { t_err = msg; }
@@ -315,11 +318,9 @@ int aby3g_stream_wait_value(aby3g_stream stream, uint64_t* word, uint64_t value)
 int aby3g_handoff_status(uint32_t* timeouts) {
     return guarded([&] {
         ABY3G_REQUIRE(timeouts != nullptr, "null argument");
-        u32* w = handoff_status_word();
-        ABY3G_CHECK_HIP(hipDeviceSynchronize());
-        ABY3G_CHECK_HIP(hipMemcpy(timeouts, w, sizeof(u32), hipMemcpyDeviceToHost));
-        if (*timeouts) ABY3G_CHECK_HIP(hipMemset(w, 0, sizeof(u32)));
-        ABY3G_CHECK_HIP(hipDeviceSynchronize());
+        volatile u32* w = handoff_status_word();
+        *timeouts = *w;
+        if (*timeouts) *w = 0;
     });
 }
 

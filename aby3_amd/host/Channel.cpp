@@ -28,6 +28,9 @@ struct Msg {
     // to *sigWord when the payload is ready (cheaper than an event hand-off)
     u64* sigWord = nullptr;
     u64 sigValue = 0;
+    // or published chunk by chunk by the producing kernel (in-kernel hand-off)
+    u64* hsFlags = nullptr;
+    u64 hsSeq = 0;
     // from another process (LinkEnd): the payload sits in the sender's
     // staging slot `lslot` (generation lgen, IPC handle lh) once the link's
     // ready word reaches lseq
@@ -58,6 +61,10 @@ struct LinkSlot {
 };
 }  // namespace
 
+// in-kernel hand-offs: messages of at most kHandoffMaxChunks chunks (128 Ki rows)
+constexpr u64 kHandoffMaxChunks = 64;
+constexpr u64 kHandoffChunks = kHandoffMaxChunks;  // flags per direction
+
 // how long a receive polls before it sleeps on the condition variable
 constexpr int kSpinUs = 500;
 thread_local double t_recvWaitUs = 0;
@@ -74,6 +81,11 @@ struct Pipe {
     int signalDevice = -1;
     u64* word = nullptr;  // allocated by the sender on first use
     u64 devSeq = 0;       // device payloads signalled so far (sender thread only)
+    // in-kernel hand-offs (Channel::handoffPost): one flag per chunk of
+    // ABY3G_HANDOFF_ROWS rows, reused by every message with increasing seq
+    bool kernelHandoff = false;
+    u64* hsFlags = nullptr;  // kHandoffChunks flags, zeroed on the sender's stream at its first message
+    u64 hsCap = 0, hsSeq = 0;
 
     // cross-process direction: this process holds one end of it
     std::unique_ptr<LinkEnd> link;
@@ -109,10 +121,11 @@ struct Pipe {
                 aby3g_device_sync();
                 aby3g_free(s->ptr);
             }
-        if (word) {
+        if (word || hsFlags) {
             aby3g_set_device(signalDevice);
             aby3g_device_sync();
-            aby3g_free(word);
+            if (word) aby3g_free(word);
+            if (hsFlags) aby3g_free(hsFlags);
         }
     }
 
@@ -307,6 +320,9 @@ struct RecvFuture::State {
     std::shared_ptr<DeviceBuffer> out;
     bool done = false;
     std::mutex mu;
+    // set by getSharedHandoff for the duration of its getShared
+    std::mutex hsMu;
+    aby3g_handoff* handoff = nullptr;
 };
 
 void RecvFuture::get() const {
@@ -352,6 +368,16 @@ void RecvFuture::get() const {
     st.done = true;
 }
 
+std::shared_ptr<DeviceBuffer> RecvFuture::getSharedHandoff(aby3g_handoff& wait) const {
+    if (!mState || !mState->shared) throw std::runtime_error("RecvFuture::getSharedHandoff on a non-shared receive");
+    wait = aby3g_handoff{nullptr, 0, nullptr};
+    std::lock_guard<std::mutex> lk(mState->hsMu);
+    mState->handoff = &wait;
+    auto out = getShared();
+    mState->handoff = nullptr;
+    return out;
+}
+
 std::shared_ptr<DeviceBuffer> RecvFuture::getShared() const {
     if (!mState || !mState->shared) throw std::runtime_error("RecvFuture::getShared on a non-shared receive");
     State& st = *mState;
@@ -375,7 +401,14 @@ std::shared_ptr<DeviceBuffer> RecvFuture::getShared() const {
         throw std::runtime_error("channel: message size mismatch (expected " + std::to_string(st.bytes) + ", got " +
                                  std::to_string(m.bytes) + ")");
     GPU_CALL(aby3g_set_device(st.gpu->device()));
-    if (m.sigWord)
+    if (m.hsFlags) {
+        if (!st.handoff)
+            throw std::runtime_error("channel: a message published in-kernel must be received by a waiting kernel "
+                                     "(RecvFuture::getSharedHandoff)");
+        st.handoff->flags = m.hsFlags;
+        st.handoff->seq = m.hsSeq;
+        st.handoff->wait_ticks = st.gpu->waitTicks();
+    } else if (m.sigWord)
         GPU_CALL(aby3g_stream_wait_value(st.gpu->stream(), m.sigWord, m.sigValue));
     else
         GPU_CALL(aby3g_stream_wait_event(st.gpu->stream(), m.ready->get()));
@@ -399,6 +432,51 @@ void Channel::asyncSendShared(std::shared_ptr<DeviceBuffer> buf, size_t bytes, G
     m.shared = std::move(buf);
     if (mOut->signalDevice != gpu.device()) m.ready = std::make_shared<Event>();
     mOut->signalReady(m, gpu, m.ready.get());
+    mOut->push(std::move(m));
+}
+
+aby3g_handoff Channel::handoffPost(Gpu& gpu, u64 rows) {
+    if (!mOut) throw std::runtime_error("channel not connected");
+    Pipe& p = *mOut;
+    if (!p.kernelHandoff || p.link || p.signalDevice != gpu.device() || kernelsSerialized())
+        return aby3g_handoff{nullptr, 0, nullptr};
+    if (!p.hsFlags) {
+        // First message of this direction: the flags are zeroed on the
+        // sender's stream and this message still goes by a stream hand-off,
+        // whose wait orders every later in-kernel poll of the receiver after
+        // the zeroing (no null-stream memset or device sync, which would take
+        // a hardware queue of the process or wait on a polling kernel).
+        void* f = nullptr;
+        GPU_CALL(aby3g_set_device(gpu.device()));
+        GPU_CALL(aby3g_malloc(&f, kHandoffChunks * 8));
+        GPU_CALL(aby3g_memset(f, 0, kHandoffChunks * 8, gpu.stream()));
+        p.hsFlags = (u64*)f;
+        p.hsCap = kHandoffChunks;
+        return aby3g_handoff{nullptr, 0, nullptr};
+    }
+    const u64 chunks = std::max<u64>(1, (rows + ABY3G_HANDOFF_ROWS - 1) / ABY3G_HANDOFF_ROWS);
+    // Large messages keep the stream hand-off: a consumer launch of many
+    // workgroups would hold its CUs spinning while the producer still runs
+    // (measured slower on C3 / C5 at 512 chunks); small ones are latency-bound
+    if (chunks > kHandoffMaxChunks) return aby3g_handoff{nullptr, 0, nullptr};
+    return aby3g_handoff{p.hsFlags, ++p.hsSeq, nullptr};
+}
+
+void Channel::asyncSendShared(std::shared_ptr<DeviceBuffer> buf, size_t bytes, Gpu& gpu, const aby3g_handoff& posted) {
+    if (!posted.flags) {
+        asyncSendShared(std::move(buf), bytes, gpu);
+        return;
+    }
+    if (!mOut) throw std::runtime_error("channel not connected");
+    if (!buf || buf->bytes() < bytes) throw std::runtime_error("asyncSendShared: buffer smaller than the message");
+    if (posted.flags != mOut->hsFlags || posted.seq != mOut->hsSeq)
+        throw std::runtime_error("asyncSendShared: the hand-off is not this channel's latest (handoffPost)");
+    Msg m;
+    m.device = true;
+    m.bytes = bytes;
+    m.shared = std::move(buf);
+    m.hsFlags = posted.flags;
+    m.hsSeq = posted.seq;
     mOut->push(std::move(m));
 }
 
@@ -481,7 +559,16 @@ bool kernelsSerialized() {
 }
 static bool signalWordsAllowed() { return !kernelsSerialized(); }
 
-std::vector<CommPkg> makeLocalRing(const int* devices) {
+int hwQueuesPerDevice() {
+    static const int n = [] {
+        const char* e = getenv("GPU_MAX_HW_QUEUES");
+        const int v = e ? atoi(e) : 0;
+        return v > 0 ? v : 4;
+    }();
+    return n;
+}
+
+std::vector<CommPkg> makeLocalRing(const int* devices, bool kernelHandoff) {
     // parties on different devices read each other's buffers in place
     // (zero-copy messages): that needs peer access both ways
     if (devices)
@@ -495,7 +582,10 @@ std::vector<CommPkg> makeLocalRing(const int* devices) {
         for (int j = 0; j < 3; ++j)
             if (i != j) {
                 p[i][j] = std::make_shared<Pipe>();
-                if (devices && devices[i] == devices[j]) p[i][j]->signalDevice = devices[i];
+                if (devices && devices[i] == devices[j]) {
+                    p[i][j]->signalDevice = devices[i];
+                    p[i][j]->kernelHandoff = kernelHandoff;
+                }
             }
     std::vector<CommPkg> c(3);
     for (int i = 0; i < 3; ++i) {

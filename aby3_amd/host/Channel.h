@@ -36,6 +36,12 @@ public:
     // and returns the sender's buffer itself. After enqueueing its last read
     // of it, the receiver calls buffer->fence(its stream).
     std::shared_ptr<DeviceBuffer> getShared() const;
+    // getShared for a consumer kernel that can wait on the device itself
+    // (aby3g_handoff): when the sender's kernel published the message chunk by
+    // chunk (Channel::handoffPost), fills `wait` and enqueues nothing; else
+    // enqueues the stream wait as getShared does and leaves wait.flags null.
+    // wait.wait_ticks is the receiver's Gpu::waitTicks().
+    std::shared_ptr<DeviceBuffer> getSharedHandoff(aby3g_handoff& wait) const;
     bool valid() const { return (bool)mState; }
 
     struct State;
@@ -70,6 +76,14 @@ public:
     // xGMI when on another GPU) and fences it when done.
     void asyncSendShared(std::shared_ptr<DeviceBuffer> buf, size_t bytes, Gpu& gpu);
     RecvFuture asyncRecvShared(size_t bytes, Gpu& gpu);
+    // In-kernel hand-off of the next zero-copy message (co-located parties on
+    // one device whose ring was made with kernel hand-offs): the flags and
+    // sequence number for the producing kernel to publish a message of `rows`
+    // rows (aby3g_handoff); flags null when this channel cannot do it. The
+    // producer is enqueued with it, then the message is sent with
+    // asyncSendShared(buf, bytes, gpu, posted): no stream operation.
+    aby3g_handoff handoffPost(Gpu& gpu, u64 rows);
+    void asyncSendShared(std::shared_ptr<DeviceBuffer> buf, size_t bytes, Gpu& gpu, const aby3g_handoff& posted);
 
     u64 bytesSent() const;
     u64 bytesRecv() const;
@@ -93,11 +107,20 @@ double recvWaitUs();
 // progress on the device, so channels hand off through events.
 bool kernelsSerialized();
 
+// Hardware queues HIP gives a process per device (GPU_MAX_HW_QUEUES, default
+// 4): streams beyond it share queues, and a kernel waiting in a shared queue
+// would block the work queued behind it.
+int hwQueuesPerDevice();
+
 // Three in-process parties connected in a ring: result[i].mNext talks to
 // party i+1, result[i].mPrev to party i-1. With `devices` (party i runs on
 // devices[i]), device payloads between parties on one device are signalled
 // through stream-ordered words instead of events.
-std::vector<CommPkg> makeLocalRing(const int* devices = nullptr);
+// kernelHandoff: messages between parties on one device may be handed over
+// inside the kernels (Channel::handoffPost); only for parties whose streams
+// each own a hardware queue (one stream per party, at most GPU_MAX_HW_QUEUES
+// streams on the device), which the caller vouches for.
+std::vector<CommPkg> makeLocalRing(const int* devices = nullptr, bool kernelHandoff = false);
 
 // One party per process (the reference's deployment): the CommPkg of `party`
 // in this process, its four directions carried by shared-memory links named

@@ -92,6 +92,7 @@ Gpu::~Gpu() {
     mForkEv.reset();
     mAuxEv.reset();
     if (mAux && !mAuxAliased) aby3g_stream_destroy(mAux);
+    if (mWaitTicks) aby3g_free(mWaitTicks);
     aby3g_stream_destroy(mStream);
     if (t_current == this) t_current = nullptr;
 }
@@ -114,6 +115,25 @@ void Gpu::bind() {
 void Gpu::sync() {
     GPU_CALL(aby3g_stream_sync(mStream));
     if (mAux) GPU_CALL(aby3g_stream_sync(mAux));
+}
+
+u64* Gpu::waitTicks() {
+    if (!mWaitTicks) {
+        GPU_CALL(aby3g_set_device(mDevice));
+        void* p = nullptr;
+        GPU_CALL(aby3g_malloc(&p, 8));
+        // zeroed in this stream's order: only this party's kernels add to it
+        GPU_CALL(aby3g_memset(p, 0, 8, mStream));
+        mWaitTicks = (u64*)p;
+    }
+    return mWaitTicks;
+}
+
+double Gpu::waitUs() {
+    if (!mWaitTicks) return 0.0;
+    u64 t = 0;
+    toHost(&t, mWaitTicks, 8, *this);
+    return (double)t * 0.01;  // 100 MHz wall clock
 }
 
 aby3g_stream Gpu::aux() {

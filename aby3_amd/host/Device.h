@@ -98,6 +98,12 @@ public:
     // object made by `make` on the first call with `key`, released with the Gpu.
     std::shared_ptr<void> attachment(u64 key, const std::function<std::shared_ptr<void>()>& make);
 
+    // Device-side time this party's kernels spent waiting for peers inside
+    // the kernels (in-kernel hand-offs: aby3g_handoff.wait_ticks), a device
+    // counter in 100 MHz ticks written only by kernels on this party's stream.
+    u64* waitTicks();
+    double waitUs();  // reads the counter (synchronizes this party's stream)
+
     // thread-local current Gpu (set by bind(), e.g. by Sh3Runtime::init)
     static Gpu& current();
     static bool hasCurrent();
@@ -112,6 +118,7 @@ private:
     std::mutex mAttachMu;
     std::map<u64, std::shared_ptr<void>> mAttach;
     std::shared_ptr<SharedStream> mDraw;
+    u64* mWaitTicks = nullptr;
 };
 
 // Owning device allocation from a party's pool (move-only). A buffer handed

@@ -415,6 +415,8 @@ struct Session {
     std::vector<CommPkg> comms;
     double hostEnqueueUs[3] = {0, 0, 0}, hostDrainUs[3] = {0, 0, 0}, hostRecvWaitUs[3] = {0, 0, 0};
     double hostApiUs[3] = {0, 0, 0}, hostApiCalls[3] = {0, 0, 0};
+    double deviceWaitUs[3] = {0, 0, 0};  // in-kernel waits for peers per step (Gpu::waitUs)
+    int devices[3] = {0, 0, 0};
     bool colocated = false;  // two or more parties on one device
     // co-located parties' shared draw stream per device (Gpu::SharedStream),
     // created once every local party has made its own stream
@@ -505,6 +507,7 @@ struct Session {
             try {
                 if (!err.empty()) throw std::runtime_error("session failed earlier");
                 if (c == 1) {
+                    const double dw0 = p.rt.gpu().waitUs();
                     const auto t0 = std::chrono::steady_clock::now();
                     const double w0 = recvWaitUs();
                     double a0 = 0, a1 = 0;
@@ -520,6 +523,7 @@ struct Session {
                     const auto t2 = std::chrono::steady_clock::now();
                     hostEnqueueUs[i] = n ? std::chrono::duration<double, std::micro>(t1 - t0).count() / n : 0;
                     hostDrainUs[i] = std::chrono::duration<double, std::micro>(t2 - t1).count();
+                    deviceWaitUs[i] = n ? (p.rt.gpu().waitUs() - dw0) / n : 0;
                 } else if (c == 3) {
                     double ms = 0;
                     uint64_t cnt = 0;
@@ -596,7 +600,12 @@ aby3h_session* aby3h_session_create(int job, const uint64_t* params, int nparams
             int dv[3] = {0, 0, 0};
             if (devices)
                 for (int i = 0; i < 3; ++i) dv[i] = devices[i];
-            s.comms = makeLocalRing(dv);
+            for (int i = 0; i < 3; ++i) s.devices[i] = dv[i];
+            // all three parties on one device: one stream each (aux aliased)
+            // plus the shared draw stream, each with a hardware queue of its
+            // own, so their kernels may hand messages over on the device
+            const bool oneDevice = dv[0] == dv[1] && dv[1] == dv[2];
+            s.comms = makeLocalRing(dv, oneDevice && hwQueuesPerDevice() >= 4);
         }
         s.colocated = !devices || devices[0] == devices[1] || devices[1] == devices[2] || devices[0] == devices[2];
         {
@@ -633,6 +642,7 @@ aby3h_session* aby3h_party_create(int job, const uint64_t* params, int nparams, 
         s.locals = {party};
         s.comms.resize(3);
         s.comms[(size_t)party] = makeProcessRing(party, link, device);
+        s.devices[party] = device;
         s.colocated = colocated != 0;
         s.turnNext = party;  // stream-creation turns: only this party's here
         {
@@ -657,9 +667,26 @@ aby3h_session* aby3h_party_create(int job, const uint64_t* params, int nparams, 
 }
 
 int aby3h_session_run(aby3h_session* h, uint64_t steps) {
-    h->s.command(1, steps);
-    if (!h->s.err.empty()) {
-        t_err = h->s.err;
+    Session& s = h->s;
+    s.command(1, steps);
+    if (s.err.empty()) {
+        // an in-kernel hand-off that gave up invalidates the run (common.h)
+        try {
+            for (int q : s.locals) {
+                u32 timeouts = 0;
+                GPU_CALL(aby3g_set_device(s.devices[q]));
+                GPU_CALL(aby3g_handoff_status(&timeouts));
+                if (timeouts)
+                    throw std::runtime_error(std::to_string(timeouts) +
+                                             " in-kernel hand-off wait(s) timed out: a party stream without a "
+                                             "hardware queue of its own?");
+            }
+        } catch (const std::exception& e) {
+            s.err = e.what();
+        }
+    }
+    if (!s.err.empty()) {
+        t_err = s.err;
         return 1;
     }
     return 0;
@@ -694,6 +721,9 @@ int aby3h_session_info(aby3h_session* h, double* out, int n) {
     tmp[ABY3H_INFO_HOST_RECV_WAIT_US] = h->s.hostRecvWaitUs[q];
     tmp[ABY3H_INFO_HOST_API_US] = h->s.hostApiUs[q];
     tmp[ABY3H_INFO_HOST_API_CALLS] = h->s.hostApiCalls[q];
+    double dw = 0;
+    for (int l : h->s.locals) dw += h->s.deviceWaitUs[l];
+    tmp[ABY3H_INFO_DEVICE_WAIT_US] = dw / (double)h->s.locals.size();
     for (int i = 0; i < n && i < ABY3H_INFO_COUNT; ++i) out[i] = tmp[i];
     return 0;
 }

@@ -361,11 +361,17 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
     // share 1 of last level's AND outputs arrived from prev (:555-573); they
     // are unpacked, straight from the sender's buffer, by the same launch that
     // runs this level's gates
+    // Co-located parties hand the AND shares over inside the level kernels
+    // (aby3g_handoff): this launch waits, per 2048-row workgroup, for the
+    // previous party's same rows and publishes its own send rows for the next
+    // party -- no stream operation between the parties' streams. Otherwise
+    // the channel enqueues a stream wait here and the flags stay null.
     u32 nUnpack = 0;
     std::shared_ptr<DeviceBuffer> recv;
+    aby3g_handoff hw{nullptr, 0, nullptr}, hp{nullptr, 0, nullptr};
     if (mLevel) {
         nUnpack = mCir->mLevelAndCounts[mLevel - 1];
-        if (nUnpack) recv = mRecvFutr.getShared();
+        if (nUnpack) recv = mRecvFutr.getSharedHandoff(hw);
     }
     const bool gatesHere = mLevel < mCir->mLevelCounts.size();
     const u32 nb = gatesHere ? mCur->levelBatches[mLevel] : 0;
@@ -380,14 +386,15 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
         send = DeviceBuffer::view(mSendAll, mAndDone * rowBytes, nAnd * rowBytes);
     }
     mAndDone += nAnd;
+    if (nAnd) hp = comm.mNext.handoffPost(g, mRows);
     if (nb && mZPending) waitZ();
     if (nb || nUnpack) {
         const aby3g_gate* gl = nb ? mCur->gates + mCur->levelFirstGate[mLevel] : nullptr;
         const u32* be = nb ? mCur->batchEnds + mCur->levelBatchOffset[mLevel] : nullptr;
         const u32* rr = (nb && recv) ? mCur->recvRows + 2 * (u64)mCur->levelFirstGate[mLevel] : nullptr;
-        GPU_CALL(aby3g_bin_level_rr(gl, rr, be, nb, recv ? recv->as<u64>() : nullptr,
+        GPU_CALL(aby3g_bin_level_hs(gl, rr, be, nb, recv ? recv->as<u64>() : nullptr,
                                     nUnpack ? mCur->outWires[mLevel - 1] : nullptr, nUnpack, mMem.as<u64>(), W, mWords,
-                                    mZPtr, send ? send->as<u64>() : nullptr, g.stream()));
+                                    mZPtr, send ? send->as<u64>() : nullptr, &hw, &hp, g.stream()));
     }
 
     if (recv) {
@@ -397,7 +404,7 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
         if (last) recv->fence(g.stream());
     }
     if (nAnd) {
-        comm.mNext.asyncSendShared(send, nAnd * rowBytes, g);
+        comm.mNext.asyncSendShared(send, nAnd * rowBytes, g, hp);
         mRecvFutr = comm.mPrev.asyncRecvShared(nAnd * rowBytes, g);
     }
     ++mLevel;

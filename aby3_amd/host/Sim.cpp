@@ -26,8 +26,10 @@ struct SimParty {
 };
 
 void run3(int device, const std::function<void(SimParty&)>& f, bool mlSeeded = false) {
+    // one stream per party (aux aliased below), so the parties' kernels hand
+    // their messages over on the device (Channel::handoffPost)
     const int dv[3] = {device, device, device};
-    auto comms = makeLocalRing(dv);
+    auto comms = makeLocalRing(dv, hwQueuesPerDevice() >= 3);
     std::exception_ptr err[3];
     std::thread th[3];
     for (int i = 0; i < 3; ++i)
@@ -36,6 +38,7 @@ void run3(int device, const std::function<void(SimParty&)>& f, bool mlSeeded = f
                 SimParty p;
                 p.idx = i;
                 p.rt.init(i, comms[i], device);
+                p.rt.gpu().aliasAux();
                 if (mlSeeded) {  // aby3ML::init (aby3ML.cpp:4-17)
                     const MlSeeds ms = mlSeeds(i);
                     p.enc.init(i, ms.encPrev, ms.encNext);
@@ -53,6 +56,10 @@ void run3(int device, const std::function<void(SimParty&)>& f, bool mlSeeded = f
     for (auto& t : th) t.join();
     for (auto& e : err)
         if (e) std::rethrow_exception(e);
+    u32 timeouts = 0;  // an in-kernel hand-off that gave up invalidates the call
+    GPU_CALL(aby3g_set_device(device));
+    GPU_CALL(aby3g_handoff_status(&timeouts));
+    if (timeouts) throw std::runtime_error("in-kernel hand-off wait timed out");
 }
 
 i64Matrix hostMat(const int64_t* p, u64 r, u64 c) {

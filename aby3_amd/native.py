@@ -213,7 +213,8 @@ class _Lib:
 
 JOB_MUL_TRUNC, JOB_MUL, JOB_MSB, JOB_LR, JOB_SORT, JOB_A2B, JOB_BITINJ = range(7)
 INFO = dict(mults_per_step=0, gemm_int8_ops=1, and_words=2, gate_words=3, gate_bytes=4, bytes_sent=5,
-            host_enqueue_us=6, host_drain_us=7, host_recv_wait_us=8, host_api_us=9, host_api_calls=10)
+            host_enqueue_us=6, host_drain_us=7, host_recv_wait_us=8, host_api_us=9, host_api_calls=10,
+            device_wait_us=11)
 
 _HOST_SIGS = {
     "aby3h_last_error": (c_char_p, []),

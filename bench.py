@@ -134,9 +134,30 @@ def load_pmc(kind: str, cfg: dict, field: str = "hbm_bytes_per_launch"):
     return best
 
 
-def local_fraction(info, step_s):
-    """1 - (party 0's host wait for peer messages) / wall clock, per step."""
-    return max(0.0, 1.0 - info["host_recv_wait_us"] * 1e-6 / step_s) if step_s > 0 else None
+def compute_fraction(nt, job, params, dev, steps, warmup=3):
+    """The local-compute fraction of wall clock, measured on the device: a
+    separate pass of the job with every kernel launch bracketed by HIP events
+    (all families, all parties): per party and step, the time its stream
+    spends inside its own kernels minus the time those kernels spent waiting
+    in-kernel for a peer's message (aby3g_handoff wait_ticks), over the pass's
+    wall clock per step. Hand-offs by stream operations (waits outside the
+    kernels) and dispatch gaps count as not computing. The probes add host
+    work per launch, so the pass runs a little slower than the timed one."""
+    with nt.Session(job, params, devices=(dev,) * 3, probe=True) as s:
+        s.run(warmup)
+        s.probe_reset()
+        t0 = time.perf_counter()
+        s.run(steps)
+        wall_us = (time.perf_counter() - t0) * 1e6 / steps
+        fam_ms = [s.probe(fam)[0] / steps for fam in range(6)]  # all parties, per step
+        kernel_us = sum(fam_ms) * 1e3 / 3  # per party
+        wait_us = s.info()["device_wait_us"]
+    return {
+        "family_ms_per_step": fam_ms,
+        "local_compute_fraction": max(0.0, min(1.0, (kernel_us - wait_us) / wall_us)),
+        "kernel_us_per_step": kernel_us, "in_kernel_wait_us_per_step": wait_us, "probed_step_us": wall_us,
+        "method": "per party: HIP-event kernel time - in-kernel peer waits, over the wall clock of a probed pass",
+    }
 
 
 def timed(sess, steps, pg):
@@ -296,8 +317,9 @@ def extras(args, nt, dev, world, pg):
             "workload": f"SGD_Logistic iteration, {args.lr_rows}x128, batch 256, D16, lr 2^-11 (sigmoid piecewise)",
             "ms_per_iteration": dt / LR_ITERS * 1e3,
             "iterations_per_s": world * LR_ITERS / dt,
-            "local_compute_fraction": local_fraction(linfo, dt / LR_ITERS),
         }
+        res["lr_iteration"]["local_compute"] = compute_fraction(nt, nt.JOB_LR, [args.lr_rows, 128, 256, 16, 11],
+                                                                dev, 100)
         if world == 1 and not args.no_cpu_baseline:
             progress("C4 CPU baseline")
             cpu_ms = cpu_lr_ms(nt, iters=200)
@@ -442,7 +464,7 @@ def main_parties(args, world, rank, local, pg, nt):
             "global_batch": groups,
             "parallelism": f"parties3x{groups}",
         },
-        "local_compute_fraction": local_fraction(info, dt / args.steps),
+        "host_recv_wait_us_per_step": info["host_recv_wait_us"],
     }
     if rank == 0:
         print(json.dumps(out))
@@ -498,15 +520,13 @@ def main():
         rp.run(30)
         gemm_ms, gemm_n = rp.probe(nt.PROBE_GEMM)
     nt.lib().mfma_turn(1 if args.gemm_turns else 0)
-    # kernel-time breakdown from a separate pass with every family probed
-    # (event pairs around every launch perturb the timing, so not the timed run)
-    with nt.Session(nt.JOB_MUL_TRUNC, [M, K, N, D, 1], devices=(dev, dev, dev), probe=True) as bd:
-        bd.run(3)
-        bd.probe_reset()
-        bd.run(10)
-        breakdown = {name: bd.probe(fam)[0] / 10 for name, fam in
-                     (("share_gemm", nt.PROBE_GEMM), ("digit_planes", nt.PROBE_DIGITS),
-                      ("trunc_epilogue", nt.PROBE_EPILOGUE))}
+    # kernel-time breakdown and the device-side local-compute fraction from a
+    # separate pass with every family probed (event pairs around every launch
+    # perturb the timing, so not the timed run)
+    c2_local = compute_fraction(nt, nt.JOB_MUL_TRUNC, [M, K, N, D, 1], dev, 10)
+    breakdown = {name: c2_local["family_ms_per_step"][fam] for name, fam in
+                 (("share_gemm", nt.PROBE_GEMM), ("digit_planes", nt.PROBE_DIGITS),
+                  ("trunc_epilogue", nt.PROBE_EPILOGUE))}
 
     mults = info["mults_per_step"]
     value = world * args.steps * mults / dt
@@ -555,10 +575,11 @@ def main():
             "ops_per_launch": info["gemm_int8_ops"],
         },
         "kernel_ms_per_step": breakdown,
-        # host time party 0 spends blocked on its peers' messages, as a share
-        # of the step (the parties' threads enqueue asynchronously; the GPU
-        # streams wait on each other without a host round trip)
-        "local_compute_fraction": local_fraction(info, dt / args.steps),
+        # share of the wall clock a party's GPU stream spends computing (its
+        # kernels, minus their in-kernel waits for peers), from a probed pass
+        "local_compute_fraction": c2_local["local_compute_fraction"],
+        "local_compute": c2_local,
+        "host_recv_wait_us_per_step": info["host_recv_wait_us"],
     }
 
     if not args.no_binary:
@@ -586,7 +607,7 @@ def main():
             "unit": "AND word-gates/s (1 AND-type gate on one 64-row word)",
             "ms_per_step": bdt / args.binary_steps * 1e3,
             "and_words_per_step": binfo["and_words"],
-            "local_compute_fraction": local_fraction(binfo, bdt / args.binary_steps),
+            "local_compute": compute_fraction(nt, nt.JOB_MSB, [args.binary_rows], dev, args.binary_steps),
             "roofline": {
                 "bound": "hbm",
                 "kernel": "k_bin_level (one launch per level: unpack of the received AND shares + the level's gate batches)",

@@ -62,7 +62,8 @@ enum {
     ABY3H_INFO_HOST_RECV_WAIT_US = 8, /* last run: host time per step waiting for peers' messages (party 0) */
     ABY3H_INFO_HOST_API_US = 9,       /* last run: host time per step inside aby3g_* calls (party 0) */
     ABY3H_INFO_HOST_API_CALLS = 10,   /* last run: aby3g_* calls per step (party 0) */
-    ABY3H_INFO_COUNT = 11
+    ABY3H_INFO_DEVICE_WAIT_US = 11,   /* last run: in-kernel wait for peers per step and party (us, mean of the local parties) */
+    ABY3H_INFO_COUNT = 12
 };
 
 const char* aby3h_last_error(void);

@@ -102,9 +102,10 @@ typedef struct {
     uint64_t seq;
     uint64_t* wait_ticks;
 } aby3g_handoff;
-/* Timed-out hand-off waits on the current device since the last call, then
- * resets the count (synchronizes the device). Nonzero: results since the
- * last call are invalid. */
+/* Nonzero when an in-kernel hand-off wait on the current device timed out
+ * since the last call (then resets it). Read after the streams drained; no
+ * GPU call (the status word is pinned host memory). Nonzero: results since
+ * the last call are invalid. */
 int aby3g_handoff_status(uint32_t* timeouts);
 
 /* Cross-process transport: one party per process (the
@@ -380,6 +381,15 @@ int aby3g_bin_level_rr(const aby3g_gate* gates, const uint32_t* recv_rows, const
                        uint32_t nbatches, const uint64_t* recvbuf, const uint32_t* unpack_wires, uint32_t nunpack,
                        uint64_t* mem, uint64_t wires, uint64_t words, const uint64_t* z, uint64_t* sendbuf,
                        aby3g_stream stream);
+/* aby3g_bin_level_rr with in-kernel hand-offs between co-located parties:
+ * `wait` for the received AND shares in recvbuf (the previous party's level
+ * launch published them), `post` for this level's send rows (the next
+ * party's level launch waits for them). A workgroup is one
+ * ABY3G_HANDOFF_ROWS chunk of rows. Either may be NULL. */
+int aby3g_bin_level_hs(const aby3g_gate* gates, const uint32_t* recv_rows, const uint32_t* batch_ends,
+                       uint32_t nbatches, const uint64_t* recvbuf, const uint32_t* unpack_wires, uint32_t nunpack,
+                       uint64_t* mem, uint64_t wires, uint64_t words, const uint64_t* z, uint64_t* sendbuf,
+                       const aby3g_handoff* wait, const aby3g_handoff* post, aby3g_stream stream);
 int aby3g_bin_unpack(const uint64_t* recvbuf, const uint32_t* out_wires, uint32_t n, uint64_t* mem, uint64_t wires,
                      uint64_t words, aby3g_stream stream);
 /* setInput (:200-276): bit-transpose a [rows][cols64] i64 share matrix into

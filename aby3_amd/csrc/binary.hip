@@ -106,10 +106,6 @@ struct GateOps {
     u64 x0, x1, y0, y1, z;
 };
 
-__device__ __forceinline__ bool gate_is_and(u32 t) {
-    return t == ABY3G_GATE_AND || t == ABY3G_GATE_OR || t == ABY3G_GATE_NOR || t == ABY3G_GATE_NA_AND;
-}
-
 // rr: the recv rows of the inputs' share 1 when they are the previous
 // level's AND outputs (~0u: read the engine memory), so that the gates need
 // not wait for the unpack of this launch
@@ -134,21 +130,12 @@ __device__ __forceinline__ void gate_eval(const aby3g_gate& g, const GateOps& o,
     const u64 x0 = o.x0, x1 = o.x1, y0 = o.y0, y1 = o.y1;
     u64 o0, o1;
     switch (g.type) {
-        case ABY3G_GATE_COPY: o0 = x0; o1 = x1; break;
-        case ABY3G_GATE_INV: o0 = ~x0; o1 = ~x1; break;
-        case ABY3G_GATE_XOR: o0 = x0 ^ y0; o1 = x1 ^ y1; break;
-        case ABY3G_GATE_NXOR: o0 = ~(x0 ^ y0); o1 = ~(x1 ^ y1); break;
+        case ABY3G_GATE_COPY:
+        case ABY3G_GATE_INV:
+        case ABY3G_GATE_XOR:
+        case ABY3G_GATE_NXOR: gate_local(g.type, x0, x1, y0, y1, o0, o1); break;
         default: {
-            u64 r;
-            if (g.type == ABY3G_GATE_AND)
-                r = (x0 & y0) ^ (x0 & y1) ^ (x1 & y0);
-            else if (g.type == ABY3G_GATE_OR)
-                r = (x0 & y0) ^ (x0 & y1) ^ (x1 & y0) ^ x0 ^ y0;
-            else if (g.type == ABY3G_GATE_NOR)
-                r = (~x0 & ~y0) ^ (~x0 & ~y1) ^ (~x1 & ~y0);
-            else /* NA_AND */
-                r = (~x0 & y0) ^ (~x0 & y1) ^ (~x1 & y0);
-            r ^= o.z;
+            const u64 r = gate_and_share(g.type, x0, x1, y0, y1) ^ o.z;
             s0[g.out * words + w] = r;
             if (wt)  // a message handed over in-kernel: write-through
                 hs_store(sendbuf + (u64)g.send_row * words + w, r);

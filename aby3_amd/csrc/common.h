@@ -290,6 +290,31 @@ inline u32 aes_grid(u64 items, u32 block) {
 
 inline hipStream_t S(aby3g_stream s) { return reinterpret_cast<hipStream_t>(s); }
 
+// ------------------------------------------------------------ gate formulas --
+// One gate of the bit-sliced engine on one 64-row word of both shares
+// (Sh3BinaryEvaluator.cpp:700-1065). AND-type gates (AND, OR, NOR, na_And)
+// produce only share 0, x0y0 ^ x0y1 ^ x1y0 (on the inverted inputs for NOR /
+// na_And) ^ z; share 1 arrives from the previous party next round.
+__device__ __forceinline__ bool gate_is_and(u32 t) {
+    return t == ABY3G_GATE_AND || t == ABY3G_GATE_OR || t == ABY3G_GATE_NOR || t == ABY3G_GATE_NA_AND;
+}
+// share 0 of an AND-type gate before its mask
+__device__ __forceinline__ u64 gate_and_share(u32 type, u64 x0, u64 x1, u64 y0, u64 y1) {
+    if (type == ABY3G_GATE_AND) return (x0 & y0) ^ (x0 & y1) ^ (x1 & y0);
+    if (type == ABY3G_GATE_OR) return (x0 & y0) ^ (x0 & y1) ^ (x1 & y0) ^ x0 ^ y0;
+    if (type == ABY3G_GATE_NOR) return (~x0 & ~y0) ^ (~x0 & ~y1) ^ (~x1 & ~y0);
+    return (~x0 & y0) ^ (~x0 & y1) ^ (~x1 & y0);  // NA_AND
+}
+// both shares of a local gate (COPY, INV, XOR, NXOR)
+__device__ __forceinline__ void gate_local(u32 type, u64 x0, u64 x1, u64 y0, u64 y1, u64& o0, u64& o1) {
+    switch (type) {
+        case ABY3G_GATE_COPY: o0 = x0; o1 = x1; break;
+        case ABY3G_GATE_INV: o0 = ~x0; o1 = ~x1; break;
+        case ABY3G_GATE_XOR: o0 = x0 ^ y0; o1 = x1 ^ y1; break;
+        default: o0 = ~(x0 ^ y0); o1 = ~(x1 ^ y1); break;  // NXOR
+    }
+}
+
 // ------------------------------------------------------ in-kernel hand-off --
 // A message between co-located parties handed over inside the kernels
 // (aby3g_handoff): the producer stores the payload write-through (sc1) --

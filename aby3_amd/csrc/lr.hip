@@ -1,0 +1,566 @@
+// One SGD_Logistic iteration (aby3-ML/Regression.h:249-293) of one party as
+// ONE launch of one workgroup, for three parties co-located on one device
+// (aby3g_lr_iteration, include/aby3gpu.h).
+//
+// The op-by-op path issues ~35 launches and ~17 stream hand-offs per party
+// and iteration on a batch of 256 rows: every step is a few microseconds of
+// work behind a launch and a hand-off. Here the whole iteration runs inside
+// one workgroup per party, phase after phase, and the parties' messages go
+// through mailboxes with the in-kernel hand-off of common.h (write-through
+// payload, one flag per message and epoch, polled by one lane). The
+// randomness is drawn exactly where the op-by-op path draws it (stream
+// positions, draw indices and OT counters come from the host), so the shares
+// are bit-identical to that path's -- tests/test_lr_driver.py holds both
+// against the oracle.
+//
+// Phases (reference lines):
+//   0  AND masks of the circuit: z[k][w] = draw k * words + w of the setCir
+//      keys (Sh3BinaryEvaluator.cpp:1406-1434), only the words with rows
+//   1  xw = mul(XX, w) >> D: the batch rows gathered on the fly
+//      (extractBatch, Regression.h:42-58), the share product
+//      XX0 (w0 + w1) + XX1 w0, the truncation pair, z to P0 / P1, the
+//      finalize (Sh3Evaluator.cpp:651-730)
+//   2  regions = int_Sh3Piecewise_helper(xw): P0 reshares x0 + x2 to P1, the
+//      inputs are bit-sliced straight into the circuit's wires, the levels
+//      run with one message per level (Sh3Piecewise.cpp:381-516,
+//      Sh3BinaryEvaluator.cpp:539-1196)
+//   3  f = region1 * (half + slope x) [OT product, Sh3Evaluator.cpp:119-263]
+//        + region2 * one [public product, :418-501]
+//   4  err = f - YY; update = mulTruncate(XX^T, err, aB); w -= update
+#include "common.h"
+
+namespace aby3g {
+
+namespace {
+
+constexpr u32 kLrThreads = 512;
+constexpr u32 kLrWaves = kLrThreads / 64;
+constexpr u32 kLrMaxB = 2048;
+constexpr u32 kLrMaxD = 4096;
+// the circuit's engine memory and AND masks live in LDS (beside the 64 KiB
+// AES table) when they fit: the levels' gate batches are chains of dependent
+// word accesses, at LDS instead of L2 latency
+constexpr u64 kLrDynLdsMax = 88 << 10;
+
+// mailbox flags (one u64 each; value = epoch of the last message published)
+enum : u32 { F_Z1 = 0, F_V = 1, F_OT1 = 2, F_OT2 = 3, F_PM = 4, F_Z2 = 5, F_LVL = 8 };
+
+// The expanded AES keys of an iteration (kernel argument).
+struct LrKeys {
+    AesKey prev, next;      // the ShareGen streams
+    AesKey zsp, zsn;        // zero-share keys
+    AesKey mp, mn;          // circuit masks (setCir)
+    AesKey otn, otp;        // SharedOT keys
+};
+
+// Mailbox and scratch layouts, in u64 words.
+struct Layout {
+    u64 W, Wpad;
+    // mailbox: flags, then two regions (epoch parity)
+    u64 flags, region;
+    u64 z1, v, lvl, ots, oth, otc, pma, pmb, z2;
+    // scratch
+    u64 xw, a, fr, f2, yy, err, z1own, z2own, upd, reg, zmask, mem, prod, total;
+    __host__ __device__ Layout(u32 B, u32 d, const aby3g_lr_circuit& c) {
+        W = (B + 63) / 64;
+        Wpad = 32 * (((u64)B + 2047) / 2048);
+        flags = ((F_LVL + (u64)c.nlevels + 31) / 32) * 32;
+        u64 o = 0;
+        z1 = o, o += B;
+        v = o, o += B;
+        lvl = o, o += (u64)c.nand * W;
+        ots = o, o += 2 * (u64)B;
+        oth = o, o += B;
+        otc = o, o += B;
+        pma = o, o += 2 * (u64)B;
+        pmb = o, o += 2 * (u64)B;
+        z2 = o, o += d;
+        region = (o + 31) / 32 * 32;
+        o = 0;
+        xw = o, o += 2 * (u64)B;
+        a = o, o += 2 * (u64)B;
+        fr = o, o += 2 * (u64)B;
+        f2 = o, o += 2 * (u64)B;
+        yy = o, o += 2 * (u64)B;
+        err = o, o += 2 * (u64)B;
+        z1own = o, o += B;
+        z2own = o, o += d;
+        upd = o, o += 2 * (u64)d;
+        reg = o, o += 6 * (u64)B;
+        zmask = o, o += (u64)c.nand * W;
+        mem = o, o += 2 * (u64)c.wires * W;
+        prod = o, o += (B > d ? B : d);
+        total = o;
+    }
+    __host__ __device__ u64 mailboxWords() const { return flags + 2 * region; }
+};
+
+// word j of PRNG(k): half (j & 1) of AES(k, j >> 1)
+__device__ __forceinline__ u64 stream_word(const u32* T, const AesKey& k, u64 j) {
+    u64 lo, hi;
+    aes_ctr_block(T, threadIdx.x & 31, k, j >> 1, lo, hi);
+    return (j & 1) ? hi : lo;
+}
+
+// waits for a neighbour's flag `f` (one lane polls; the workgroup leaves
+// together); false after a timeout
+__device__ __forceinline__ bool lr_wait(const u64* box, u32 f, u64 epoch, u64* ticks, u32* status) {
+    return hs_wait(HsWait{box, epoch, ticks, status}, f, f + 1);
+}
+// publishes this party's flag `f` after every wave's write-through stores
+__device__ __forceinline__ void lr_post(u64* box, u32 f, u64 epoch) { hs_post(HsPost{box, epoch}, f, f + 1); }
+
+// The truncation pair over n elements (Sh3Evaluator.cpp:503-566, 667-673):
+// t0 = next-stream word (nw0 + i), t1 = prev-stream word (pw0 + i);
+// z = prod - (t0 >> 2) published into `out` (write-through) and kept in own,
+// C = (t0 >> (d+2), t1 >> (d+2)) into c0 / c1.
+__device__ __forceinline__ void lr_trunc_pair(const u32* T, const LrKeys& K, u64 nw0, u64 pw0, u32 n, u32 d,
+                                              const u64* prod, u64* out, u64* own, u64* c0, u64* c1) {
+    for (u32 i = threadIdx.x; i < n; i += kLrThreads) {
+        const i64 t0 = (i64)stream_word(T, K.next, nw0 + i);
+        const i64 t1 = (i64)stream_word(T, K.prev, pw0 + i);
+        const u64 z = prod[i] - (u64)(t0 >> 2);
+        own[i] = z;
+        hs_store(out + i, z);
+        c0[i] = (u64)(t0 >> (d + 2));
+        c1[i] = (u64)(t1 >> (d + 2));
+    }
+}
+
+// Round 2 of the truncating product, parties 0 and 1 (Sh3Evaluator.cpp:
+// 703-719): C[party] += (z_next + z_prev + z_own) >> d.
+__device__ __forceinline__ void lr_trunc_finalize(const u64* zn, const u64* zp, const u64* own, u32 n, u32 d,
+                                                  u64* cp) {
+    for (u32 i = threadIdx.x; i < n; i += kLrThreads) {
+        const i64 s = (i64)(hs_load(zn + i) + hs_load(zp + i) + own[i]);
+        cp[i] += (u64)(s >> d);
+    }
+}
+
+// phase stamps for profiling (aby3g_lr_iter.phase_ticks): wall clock of slot s
+__device__ __forceinline__ void lr_stamp(u64* ticks, u32 s) {
+    if (ticks && threadIdx.x == 0) ticks[s] = wall_clock64();
+}
+
+__global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict__ T0g, aby3g_lr_iter it, LrKeys K,
+                                                           u32* status, int memInLds) {
+    __shared__ u32 lds[kAesLdsWords];
+    __shared__ u64 part[kLrThreads];
+    extern __shared__ __attribute__((aligned(16))) u64 dyn[];  // [2][wires][W] engine memory, then [nand][W] masks
+    u64* const PT = it.phase_ticks;
+    lr_stamp(PT, 0);
+    aes_fill_lds(lds, T0g);
+    const u32* T = lds;
+    const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int p = it.party;
+    const u32 B = it.B, d = it.d;
+    const u64 n = it.n;
+    const aby3g_lr_circuit& cir = it.cir;
+    const Layout L(B, d, cir);
+    const u64 W = L.W;
+    u64* sc = (u64*)it.scratch;
+    u64* box = (u64*)it.mailbox;
+    const u64* nbox = (const u64*)it.next_mailbox;
+    const u64* pbox = (const u64*)it.prev_mailbox;
+    const u64 par = (it.epoch & 1) * L.region;
+    u64* my = box + L.flags + par;                   // this epoch's outgoing region
+    const u64* nx = nbox + L.flags + par;            // next party's
+    const u64* pv = pbox + L.flags + par;            // prev party's
+    const u64 ep = it.epoch;
+    u64* ticks = it.wait_ticks;
+    const u64* X0 = (const u64*)it.X;
+    const u64* X1 = X0 + n * d;
+    const u64* Y0 = (const u64*)it.Y;
+    const u64* Y1 = Y0 + n;
+    u64* w0 = (u64*)it.w;
+    u64* w1 = w0 + d;
+    u64* xw0 = sc + L.xw;
+    u64* xw1 = xw0 + B;
+    u64* prod = sc + L.prod;
+
+    u64* mem = memInLds ? dyn : sc + L.mem;
+    u64* zmw = memInLds ? dyn + 2 * (u64)cir.wires * W : sc + L.zmask;
+
+    // ---- phase 0: the circuit's AND masks, words with rows only ----
+    {
+        u64* zm = zmw;
+        const u64 Wh = (W + 1) / 2;
+        for (u64 q = tid; q < (u64)cir.nand * Wh; q += kLrThreads) {
+            const u64 k = q / Wh, wp = q % Wh;
+            const u64 c = (k * L.Wpad + 2 * wp) >> 1;  // Wpad is even: draws 2wp, 2wp + 1 share a block
+            u64 a0, a1, b0, b1;
+            aes_ctr_block2(T, tid & 31, K.mp, c, K.mn, c, a0, a1, b0, b1);
+            zm[k * W + 2 * wp] = a0 ^ b0;
+            if (2 * wp + 1 < W) zm[k * W + 2 * wp + 1] = a1 ^ b1;
+        }
+    }
+
+    lr_stamp(PT, 1);
+    // ---- phase 1: xw = mul(XX, w) with truncation (shift D) ----
+    // a wave per row, lanes over k; 8 rows of a wave at a time, so that every
+    // lane has 16 independent row loads in flight (the rows are scattered
+    // over the dataset: HBM latency, not bandwidth)
+    constexpr u32 kRowsAtOnce = 8;
+    for (u32 r0 = wave * kRowsAtOnce; r0 < B; r0 += kLrWaves * kRowsAtOnce) {
+        u64 acc[kRowsAtOnce];
+        u64 rowOf[kRowsAtOnce];
+#pragma unroll
+        for (u32 j = 0; j < kRowsAtOnce; ++j) {
+            acc[j] = 0;
+            rowOf[j] = r0 + j < B ? it.batch[r0 + j] : 0;
+        }
+        for (u32 k = lane; k < d; k += 64) {
+            const u64 ws = w0[k] + w1[k], wa = w0[k];
+            u64 a0[kRowsAtOnce], a1[kRowsAtOnce];
+#pragma unroll
+            for (u32 j = 0; j < kRowsAtOnce; ++j) {
+                a0[j] = r0 + j < B ? X0[rowOf[j] * d + k] : 0;
+                a1[j] = r0 + j < B ? X1[rowOf[j] * d + k] : 0;
+            }
+#pragma unroll
+            for (u32 j = 0; j < kRowsAtOnce; ++j) acc[j] += a0[j] * ws + a1[j] * wa;
+        }
+#pragma unroll
+        for (u32 j = 0; j < kRowsAtOnce; ++j) {
+            u64 a = acc[j];
+#pragma unroll
+            for (int o = 32; o; o >>= 1) a += __shfl_xor(a, o, 64);
+            if (lane == 0 && r0 + j < B) prod[r0 + j] = a;
+        }
+    }
+    __syncthreads();
+    lr_stamp(PT, 2);
+    lr_trunc_pair(T, K, it.t1_next_off / 8, it.t1_prev_off / 8, B, it.D, prod, my + L.z1, sc + L.z1own, xw0, xw1);
+    lr_post(box, F_Z1, ep);
+    lr_stamp(PT, 3);
+    if (p < 2) {
+        if (!lr_wait(nbox, F_Z1, ep, ticks, status) || !lr_wait(pbox, F_Z1, ep, ticks, status)) return;
+        lr_trunc_finalize(nx + L.z1, pv + L.z1, sc + L.z1own, B, it.D, p == 0 ? xw0 : xw1);
+    }
+    __syncthreads();
+
+    lr_stamp(PT, 4);
+    // ---- phase 2: regions of the piecewise sigmoid ----
+    // P0 reshares x0 + x2 (its two shares) to P1
+    const u64* vrecv = nullptr;
+    if (p == 0) {
+        for (u32 i = tid; i < B; i += kLrThreads) hs_store(my + L.v + i, xw0[i] + xw1[i]);
+        lr_post(box, F_V, ep);
+    } else if (p == 1) {
+        if (!lr_wait(pbox, F_V, ep, ticks, status)) return;
+        vrecv = pv + L.v;
+    }
+    // inputs straight into the wires (setTwoInputSharing): source s in
+    // {aa_0, aa_1, b}, share h; a wave ballots bit b of its 64 rows
+    const u64 WS = (u64)cir.wires * W;  // share stride
+    for (u32 job = wave; job < 6 * W; job += kLrWaves) {
+        const u32 src = job / (2 * (u32)W), h = (job / (u32)W) & 1, w = job % (u32)W;
+        const u32 r = w * 64 + lane;
+        u64 val = 0;
+        if (r < B) {
+            if (src < 2) {
+                if (p == 0 && h == 0) val = xw0[r] + xw1[r] + (u64)it.thr_off[src];
+                if (p == 1 && h == 1) val = hs_load(vrecv + r) + (u64)it.thr_off[src];
+            } else {
+                if (p == 1 && h == 0) val = xw0[r];
+                if (p == 2 && h == 1) val = xw1[r];
+            }
+        }
+        u64* base = mem + h * WS + (u64)cir.in_wire[src] * W + w;
+        for (u32 b = 0; b < 64; ++b) {
+            const u64 word = __ballot((val >> b) & 1);
+            if (lane == 0) base[(u64)b * W] = word;
+        }
+    }
+    __syncthreads();
+    lr_stamp(PT, 5);
+    // the levels (roundCallback): unpack the previous level's received AND
+    // shares, then this level's batches, then publish its AND shares
+    const u64* zm = zmw;
+    for (u32 lv = 0; lv <= cir.nlevels; ++lv) {
+        if (lv > 0 && cir.levels[lv - 1].nand) {
+            const aby3g_lr_level& pl = cir.levels[lv - 1];
+            if (!lr_wait(pbox, F_LVL + lv - 1, ep, ticks, status)) return;
+            const u64* rows = pv + L.lvl + (u64)pl.and_wire_off * W;
+            for (u64 q = tid; q < (u64)pl.nand * W; q += kLrThreads) {
+                const u64 j = q / W, w = q % W;
+                mem[WS + (u64)cir.and_wires[pl.and_wire_off + j] * W + w] = hs_load(rows + q);
+            }
+            __syncthreads();
+        }
+        if (lv == cir.nlevels) break;
+        const aby3g_lr_level& lvr = cir.levels[lv];
+        u64* send = my + L.lvl + (u64)lvr.and_wire_off * W;
+        u32 begin = 0;
+        for (u32 b = 0; b < lvr.nbatch; ++b) {
+            const u32 end = cir.batch_ends[lvr.batch_off + b];
+            for (u64 q = tid; q < (u64)(end - begin) * W; q += kLrThreads) {
+                const aby3g_gate g = cir.gates[lvr.first_gate + begin + q / W];
+                const u64 w = q % W;
+                const bool unary = g.type == ABY3G_GATE_COPY || g.type == ABY3G_GATE_INV;
+                const u32 in1 = unary ? g.in0 : g.in1;
+                const u64 x0 = mem[(u64)g.in0 * W + w], x1 = mem[WS + (u64)g.in0 * W + w];
+                const u64 y0 = mem[(u64)in1 * W + w], y1 = mem[WS + (u64)in1 * W + w];
+                if (gate_is_and(g.type)) {
+                    const u64 r = gate_and_share(g.type, x0, x1, y0, y1) ^ zm[(u64)g.z_row * W + w];
+                    mem[(u64)g.out * W + w] = r;
+                    hs_store(send + (u64)g.send_row * W + w, r);
+                } else {
+                    u64 o0, o1;
+                    gate_local(g.type, x0, x1, y0, y1, o0, o1);
+                    mem[(u64)g.out * W + w] = o0;
+                    mem[WS + (u64)g.out * W + w] = o1;
+                }
+            }
+            __syncthreads();
+            begin = end;
+        }
+        if (lvr.nand) lr_post(box, F_LVL + lv, ep);
+    }
+    lr_stamp(PT, 6);
+    // regions (getOutput, 1 bit each): reg[t][h][i]
+    u64* reg = sc + L.reg;
+    for (u32 i = tid; i < B; i += kLrThreads)
+        for (u32 t = 0; t < 3; ++t)
+            for (u32 h = 0; h < 2; ++h)
+                reg[(2 * t + h) * B + i] = (mem[h * WS + (u64)cir.out_wire[t] * W + (i >> 6)] >> (i & 63)) & 1;
+    __syncthreads();
+
+    // ---- phase 3: f = region1 (half + slope x) + region2 one ----
+    u64* A0 = sc + L.a;
+    u64* A1 = A0 + B;
+    u64* fr0 = sc + L.fr;
+    u64* fr1 = fr0 + B;
+    u64* g0 = sc + L.f2;
+    u64* g1 = g0 + B;
+    const u64* r1a = reg + 2 * B;  // region 1, share 0 / 1
+    const u64* r1b = reg + 3 * B;
+    const u64* r2a = reg + 4 * B;  // region 2
+    const u64* r2b = reg + 5 * B;
+    for (u32 i = tid; i < B; i += kLrThreads) {  // getFunctionValues (Sh3Piecewise.cpp:518-567)
+        A0[i] = (u64)it.slope * xw0[i] + (p == 0 ? (u64)it.half : 0);
+        A1[i] = (u64)it.slope * xw1[i] + (p == 1 ? (u64)it.half : 0);
+    }
+    __syncthreads();
+    lr_stamp(PT, 7);
+    const u64 otw = p == 0 ? it.ot_prev_off / 8 : p == 1 ? it.ot_prev_off / 8 : it.ot_next_off / 8;
+    if (p == 0) {
+        const u64 nw = it.ot_next_off / 8;
+        for (u32 i = tid; i < B; i += kLrThreads) {
+            // OT product, sender + helper (Sh3Evaluator.cpp:132-163)
+            const u64 zr = stream_word(T, K.prev, otw + 2 * i), c1 = stream_word(T, K.prev, otw + 2 * i + 1);
+            const u64 c0 = stream_word(T, K.next, nw + i);
+            fr0[i] = c0;
+            fr1[i] = c1;
+            const u32 bb0 = (u32)((r1a[i] ^ r1b[i]) & 1), bb1 = (u32)(r1a[i] & 1);
+            const u64 zz = 0 - (c0 + c1) - zr;
+            u64 s[2];
+            s[bb0] = zz;
+            s[bb0 ^ 1] = A0[i] + A1[i] + zz;
+            u64 lo, hi, hlo, hhi;
+            aes_ctr_block2(T, tid & 31, K.otn, it.ot_ctr + i, K.otn, it.ot_ctr + B + i, lo, hi, hlo, hhi);
+            hs_store(my + L.ots + 2 * i, lo ^ s[0]);
+            hs_store(my + L.ots + 2 * i + 1, hi ^ s[1]);
+            hs_store(my + L.oth + i, bb1 ? hhi : hlo);
+            // public product (Sh3Evaluator.cpp:430-447)
+            const u64 j = it.pm_draw + i;
+            u64 zp[2], zq[2];
+            aes_ctr_block2(T, tid & 31, K.zsp, j >> 1, K.zsn, j >> 1, zp[0], zp[1], zq[0], zq[1]);
+            const u64 zs = zp[j & 1] - zq[j & 1];
+            const u32 bb = (u32)((r2a[i] ^ r2b[i]) & 1);
+            u64 t[2];
+            t[bb] = zs;
+            t[bb ^ 1] = (u64)it.one + zs;
+            u64 nlo, nhi, plo, phi;
+            aes_ctr_block2(T, tid & 31, K.otn, it.pm_ctr_next + i, K.otp, it.pm_ctr_prev + i, nlo, nhi, plo, phi);
+            hs_store(my + L.pma + 2 * i, nlo ^ t[0]);
+            hs_store(my + L.pma + 2 * i + 1, nhi ^ t[1]);
+            hs_store(my + L.pmb + 2 * i, plo ^ t[0]);
+            hs_store(my + L.pmb + 2 * i + 1, phi ^ t[1]);
+        }
+        lr_post(box, F_OT1, ep);
+        lr_post(box, F_PM, ep);
+        if (!lr_wait(nbox, F_PM, ep, ticks, status) || !lr_wait(pbox, F_PM, ep, ticks, status)) return;
+        for (u32 i = tid; i < B; i += kLrThreads) {
+            g0[i] = hs_load(nx + L.pmb + i);  // P1's share of the product
+            g1[i] = hs_load(pv + L.pmb + i);  // P2's
+        }
+    } else if (p == 1) {
+        for (u32 i = tid; i < B; i += kLrThreads) {
+            fr1[i] = stream_word(T, K.prev, otw + i);  // OT receiver's share 1 (:165-200)
+            const u64 j = it.pm_draw + i;              // public product, helper (:452-487)
+            u64 zp[2], zq[2];
+            aes_ctr_block2(T, tid & 31, K.zsp, j >> 1, K.zsn, j >> 1, zp[0], zp[1], zq[0], zq[1]);
+            const u64 zs = zp[j & 1] - zq[j & 1];
+            g1[i] = zs;
+            u64 lo, hi;
+            aes_ctr_block(T, tid & 31, K.otn, it.pm_ctr_next + i, lo, hi);
+            hs_store(my + L.pma + i, (r2a[i] & 1) ? hi : lo);  // help -> P2
+            hs_store(my + L.pmb + i, zs);                      // mine -> P0
+        }
+        lr_post(box, F_PM, ep);
+        if (!lr_wait(pbox, F_OT1, ep, ticks, status) || !lr_wait(nbox, F_OT1, ep, ticks, status)) return;
+        for (u32 i = tid; i < B; i += kLrThreads) {
+            // c0 = recv(P2's send, P0's help; choice b1) + recv(P0's send, P2's help; choice b0)
+            const u64 m1 = hs_load(nx + L.ots + 2 * i + (r1b[i] & 1)) ^ hs_load(pv + L.oth + i);
+            const u64 m0 = hs_load(pv + L.ots + 2 * i + (r1a[i] & 1)) ^ hs_load(nx + L.oth + i);
+            fr0[i] = m1 + m0;
+            hs_store(my + L.otc + i, m1 + m0);  // -> P2
+        }
+        lr_post(box, F_OT2, ep);
+        if (!lr_wait(pbox, F_PM, ep, ticks, status) || !lr_wait(nbox, F_PM, ep, ticks, status)) return;
+        for (u32 i = tid; i < B; i += kLrThreads)
+            g0[i] = hs_load(pv + L.pma + 2 * i + (r2a[i] & 1)) ^ hs_load(nx + L.pma + i);
+    } else {
+        for (u32 i = tid; i < B; i += kLrThreads) {
+            // OT product, sender + helper (:202-240)
+            const u64 zr = stream_word(T, K.next, otw + 2 * i), c0 = stream_word(T, K.next, otw + 2 * i + 1);
+            fr0[i] = c0;
+            const u32 bb0 = (u32)(r1b[i] & 1), bb1 = (u32)((r1a[i] ^ r1b[i]) & 1);
+            u64 s[2];
+            s[bb1] = zr;
+            s[bb1 ^ 1] = A1[i] + zr;
+            u64 hlo, hhi, lo, hi;
+            aes_ctr_block2(T, tid & 31, K.otp, it.ot_ctr + i, K.otp, it.ot_ctr + B + i, hlo, hhi, lo, hi);
+            hs_store(my + L.oth + i, bb0 ? hhi : hlo);
+            hs_store(my + L.ots + 2 * i, lo ^ s[0]);
+            hs_store(my + L.ots + 2 * i + 1, hi ^ s[1]);
+            // public product, helper
+            const u64 j = it.pm_draw + i;
+            u64 zp[2], zq[2];
+            aes_ctr_block2(T, tid & 31, K.zsp, j >> 1, K.zsn, j >> 1, zp[0], zp[1], zq[0], zq[1]);
+            const u64 zs = zp[j & 1] - zq[j & 1];
+            g0[i] = zs;
+            u64 plo, phi;
+            aes_ctr_block(T, tid & 31, K.otp, it.pm_ctr_prev + i, plo, phi);
+            hs_store(my + L.pma + i, (r2b[i] & 1) ? phi : plo);  // help -> P1
+            hs_store(my + L.pmb + i, zs);                        // mine -> P0
+        }
+        lr_post(box, F_OT1, ep);
+        lr_post(box, F_PM, ep);
+        if (!lr_wait(pbox, F_OT2, ep, ticks, status)) return;
+        for (u32 i = tid; i < B; i += kLrThreads) fr1[i] = hs_load(pv + L.otc + i);
+        if (!lr_wait(nbox, F_PM, ep, ticks, status) || !lr_wait(pbox, F_PM, ep, ticks, status)) return;
+        for (u32 i = tid; i < B; i += kLrThreads)
+            g1[i] = hs_load(nx + L.pmb + 2 * i + (r2b[i] & 1)) ^ hs_load(pv + L.pma + i);
+    }
+    __syncthreads();
+
+    lr_stamp(PT, 8);
+    // ---- phase 4: err = f - YY; update = mulTruncate(XX^T, err); w -= update ----
+    u64* e0 = sc + L.err;
+    u64* e1 = e0 + B;
+    for (u32 i = tid; i < B; i += kLrThreads) {
+        const u64 row = it.batch[i];
+        e0[i] = fr0[i] + g0[i] - Y0[row];
+        e1[i] = fr1[i] + g1[i] - Y1[row];
+    }
+    __syncthreads();
+    // prod[k] = sum_i XX0[i][k] (e0 + e1)[i] + XX1[i][k] e0[i]: thread (k, i-group)
+    for (u32 k0 = 0; k0 < d; k0 += kLrThreads) {
+        const u32 dk = min(d - k0, kLrThreads);
+        const u32 G = kLrThreads / dk;  // i-groups
+        const u32 k = k0 + tid % dk, gi = tid / dk;
+        u64 acc = 0;
+        if (gi < G) {
+            // 8 rows per step: 16 independent loads in flight per thread
+            u32 i = gi;
+            for (; i + 7 * G < B; i += 8 * G) {
+                u64 a0[8], a1[8];
+#pragma unroll
+                for (u32 j = 0; j < 8; ++j) {
+                    const u64 row = it.batch[i + j * G];
+                    a0[j] = X0[row * d + k];
+                    a1[j] = X1[row * d + k];
+                }
+#pragma unroll
+                for (u32 j = 0; j < 8; ++j) {
+                    const u32 ii = i + j * G;
+                    acc += a0[j] * (e0[ii] + e1[ii]) + a1[j] * e0[ii];
+                }
+            }
+            for (; i < B; i += G) {
+                const u64 row = it.batch[i];
+                acc += X0[row * d + k] * (e0[i] + e1[i]) + X1[row * d + k] * e0[i];
+            }
+        }
+        part[tid] = acc;
+        __syncthreads();
+        if (tid < dk) {
+            u64 s = 0;
+            for (u32 g = 0; g < G; ++g) s += part[g * dk + tid];
+            prod[k0 + tid] = s;
+        }
+        __syncthreads();
+    }
+    lr_stamp(PT, 9);
+    const u32 sh2 = it.D + it.aB;
+    u64* u0 = sc + L.upd;
+    u64* u1 = u0 + d;
+    lr_trunc_pair(T, K, it.t2_next_off / 8, it.t2_prev_off / 8, d, sh2, prod, my + L.z2, sc + L.z2own, u0, u1);
+    lr_post(box, F_Z2, ep);
+    lr_stamp(PT, 10);
+    if (p < 2) {
+        if (!lr_wait(nbox, F_Z2, ep, ticks, status) || !lr_wait(pbox, F_Z2, ep, ticks, status)) return;
+        lr_trunc_finalize(nx + L.z2, pv + L.z2, sc + L.z2own, d, sh2, p == 0 ? u0 : u1);
+    }
+    __syncthreads();
+    for (u32 k = tid; k < d; k += kLrThreads) {
+        w0[k] -= u0[k];
+        w1[k] -= u1[k];
+    }
+    lr_stamp(PT, 11);
+}
+
+}  // namespace
+
+}  // namespace aby3g
+
+using namespace aby3g;
+
+extern "C" {
+
+uint64_t aby3g_lr_mailbox_bytes(uint32_t B, uint32_t d, const aby3g_lr_circuit* cir) {
+    return cir ? Layout(B, d, *cir).mailboxWords() * 8 : 0;
+}
+
+uint64_t aby3g_lr_scratch_bytes(uint32_t B, uint32_t d, const aby3g_lr_circuit* cir) {
+    return cir ? Layout(B, d, *cir).total * 8 : 0;
+}
+
+int aby3g_lr_iteration(const aby3g_lr_iter* it, aby3g_stream stream) {
+    return guarded([&] {
+        ABY3G_REQUIRE(it != nullptr, "null argument");
+        ABY3G_REQUIRE(it->party >= 0 && it->party <= 2, "party out of range");
+        ABY3G_REQUIRE(it->B >= 1 && it->B <= kLrMaxB && it->d >= 1 && it->d <= kLrMaxD, "shape outside the fused form");
+        ABY3G_REQUIRE(it->D + it->aB + 2 < 64, "shift too large");
+        ABY3G_REQUIRE(it->epoch >= 1, "epochs start at 1");
+        ABY3G_REQUIRE(it->X && it->Y && it->w && it->batch && it->scratch && it->mailbox && it->next_mailbox &&
+                          it->prev_mailbox && it->cir.gates && it->cir.levels,
+                      "null pointer");
+        ABY3G_REQUIRE(it->t1_next_off % 8 == 0 && it->t1_prev_off % 8 == 0 && it->t2_next_off % 8 == 0 &&
+                          it->t2_prev_off % 8 == 0 && it->ot_next_off % 8 == 0 && it->ot_prev_off % 8 == 0,
+                      "stream offsets must be multiples of 8");
+        LrKeys K;
+        K.prev = expand_key(it->prev_seed);
+        K.next = expand_key(it->next_seed);
+        K.zsp = expand_key(it->zs_prev);
+        K.zsn = expand_key(it->zs_next);
+        K.mp = expand_key(it->mask_prev);
+        K.mn = expand_key(it->mask_next);
+        K.otn = expand_key(it->ot_next_key);
+        K.otp = expand_key(it->ot_prev_key);
+        const Layout L(it->B, it->d, it->cir);
+        const u64 dynBytes = (2 * (u64)it->cir.wires + it->cir.nand) * L.W * 8;
+        const int inLds = dynBytes <= kLrDynLdsMax;
+        static const bool attr = [] {  // dynamic LDS beyond the default limit, once per process
+            return hipFuncSetAttribute((const void*)k_lr_iter, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)kLrDynLdsMax) == hipSuccess;
+        }();
+        ABY3G_REQUIRE(attr || !inLds, "could not raise the fused iteration's dynamic LDS limit");
+        launch(PROBE_OTHER, k_lr_iter, dim3(1), dim3(kLrThreads), inLds ? dynBytes : 0, S(stream), aes_table(), *it, K,
+               handoff_status_word(), inLds);
+    });
+}
+
+}  // extern "C"

@@ -462,6 +462,13 @@ aby3g_handoff Channel::handoffPost(Gpu& gpu, u64 rows) {
     return aby3g_handoff{p.hsFlags, ++p.hsSeq, nullptr};
 }
 
+bool Channel::handoffCapable(const Gpu& gpu) const {
+    if (!mOut || !mIn || kernelsSerialized()) return false;
+    for (const Pipe* p : {mOut.get(), mIn.get()})
+        if (!p->kernelHandoff || p->link || p->signalDevice != gpu.device()) return false;
+    return true;
+}
+
 void Channel::asyncSendShared(std::shared_ptr<DeviceBuffer> buf, size_t bytes, Gpu& gpu, const aby3g_handoff& posted) {
     if (!posted.flags) {
         asyncSendShared(std::move(buf), bytes, gpu);

@@ -83,6 +83,10 @@ public:
     // producer is enqueued with it, then the message is sent with
     // asyncSendShared(buf, bytes, gpu, posted): no stream operation.
     aby3g_handoff handoffPost(Gpu& gpu, u64 rows);
+    // Both directions join parties on `gpu`'s device in this process whose
+    // ring allows kernel hand-offs (a fused launch may then address the
+    // peer's device memory and poll it).
+    bool handoffCapable(const Gpu& gpu) const;
     void asyncSendShared(std::shared_ptr<DeviceBuffer> buf, size_t bytes, Gpu& gpu, const aby3g_handoff& posted);
 
     u64 bytesSent() const;

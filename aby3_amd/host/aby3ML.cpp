@@ -1,5 +1,6 @@
 #include "aby3ML.h"
 #include <algorithm>
+#include <cstring>
 #include <random>
 
 namespace aby3 {
@@ -12,18 +13,230 @@ void aby3ML::mulTruncate(const si64Matrix& left, const si64Matrix& right, si64Ma
     mEval.asyncMul(mRt.noDependencies(), left, right, dest, mD + shift, MulMode::Gemm).get();
 }
 
-void aby3ML::logisticFunc(const si64Matrix& Y, si64Matrix& out) {
+Sh3Piecewise& aby3ML::logistic() {
     if (mLogistic.mThresholds.empty()) {
         mLogistic.mThresholds = {Sh3Piecewise::Coef(-0.5), Sh3Piecewise::Coef(0.5)};
         mLogistic.mCoefficients.resize(3);
         mLogistic.mCoefficients[1] = {Sh3Piecewise::Coef(0.5), Sh3Piecewise::Coef(1)};
         mLogistic.mCoefficients[2] = {Sh3Piecewise::Coef(1)};
     }
-    mLogistic.eval(mRt.noDependencies(), Y, out, mD, mEval).get();
+    return mLogistic;
 }
+
+void aby3ML::logisticFunc(const si64Matrix& Y, si64Matrix& out) {
+    logistic().eval(mRt.noDependencies(), Y, out, mD, mEval).get();
+}
+
+// ---- the fused iteration (aby3g_lr_iteration) ------------------------------
+// One launch per party and iteration. The host side keeps the op-by-op
+// path's bookkeeping exactly -- every stream offset, zero-share draw, OT
+// counter and setCir key is taken here in the order that path takes them --
+// so the kernel reproduces its shares bit for bit.
+struct FusedLr {
+    CircuitLibrary lib;        // the same int_Sh3Piecewise_helper(64, 2) as Sh3Piecewise builds
+    DeviceBuffer circuit;      // levelized gate list (aby3g_lr_circuit arrays)
+    aby3g_lr_circuit cir{};
+    DeviceBuffer scratch, mailbox;
+    const void* nextBox = nullptr;
+    const void* prevBox = nullptr;
+    u64 epoch = 0;
+    u64 d = 0, B = 0;
+    i64 thrOff[2] = {0, 0}, half = 0, slope = 0, one = 0;
+
+    // The fused form applies to the logistic piecewise of aby3ML (regions
+    // {}, {c, integer slope}, {c}) with randomization on, B <= 2048 rows, and
+    // a ring of co-located parties; every party decides alike.
+    static std::shared_ptr<FusedLr> make(aby3ML& ml, u64 d, u64 B) {
+        Gpu& g = ml.mRt.gpu();
+        CommPkg& comm = ml.mRt.mComm;
+        if (!comm.mNext.handoffCapable(g) || !comm.mPrev.handoffCapable(g)) return nullptr;
+        if (ml.mEval.DEBUG_disable_randomization || B == 0 || B > 2048 || d == 0 || d > 4096) return nullptr;
+        Sh3Piecewise& pw = ml.logistic();
+        const auto& co = pw.mCoefficients;
+        if (pw.mThresholds.size() != 2 || co.size() != 3 || !co[0].empty() || co[1].size() != 2 ||
+            !co[1][1].mIsInteger || co[2].size() != 1)
+            return nullptr;
+        auto f = std::make_shared<FusedLr>();
+        f->d = d;
+        f->B = B;
+        for (int t = 0; t < 2; ++t) f->thrOff[t] = (i64)(0 - (u64)pw.mThresholds[t].getFixedPoint(ml.mD));
+        f->half = co[1][0].getFixedPoint(ml.mD);
+        f->slope = co[1][1].getInteger();
+        f->one = co[2][0].getFixedPoint(ml.mD);
+        f->upload(g);
+        const u64 mb = aby3g_lr_mailbox_bytes((u32)B, (u32)d, &f->cir);
+        f->mailbox.reset(g, mb);
+        f->scratch.reset(g, aby3g_lr_scratch_bytes((u32)B, (u32)d, &f->cir));
+        // zeroed before any peer can poll it: the address leaves only after
+        // this stream has drained the memset
+        GPU_CALL(aby3g_memset(f->mailbox.data(), 0, mb, g.stream()));
+        g.sync();
+        const u64 mine = (u64)(uintptr_t)f->mailbox.data();
+        comm.mNext.asyncSendCopy(mine);
+        comm.mPrev.asyncSendCopy(mine);
+        u64 nb = 0, pb = 0;
+        comm.mNext.recv(nb);
+        comm.mPrev.recv(pb);
+        f->nextBox = (const void*)(uintptr_t)nb;
+        f->prevBox = (const void*)(uintptr_t)pb;
+        return f;
+    }
+
+    // the levelized circuit as device arrays: gates in batch order, batch
+    // ends, per level (first gate, batches, AND gates, AND output wires)
+    void upload(Gpu& g) {
+        BetaCircuit* c = lib.int_Sh3Piecewise_helper(64, 2);
+        if (!c->levelized()) c->levelByAndDepth();
+        if (c->mInputs.size() != 3 || c->mOutputs.size() != 3) throw std::runtime_error("piecewise helper shape");
+        for (const auto& in : c->mInputs) {
+            if (in.size() != 64) throw std::runtime_error("piecewise helper inputs");
+            for (size_t k = 1; k < in.size(); ++k)
+                if (in[k] != in[k - 1] + 1) throw std::runtime_error("piecewise helper inputs not contiguous");
+        }
+        for (const auto& o : c->mOutputs)
+            if (o.size() != 1) throw std::runtime_error("piecewise helper outputs");
+        std::vector<aby3g_gate> gates(c->mBatchGates.size());
+        for (size_t i = 0; i < gates.size(); ++i) {
+            const BetaGate& b = c->mBatchGates[i];
+            gates[i] = aby3g_gate{b.in0, b.in1, b.out, (u32)b.type, c->mBatchZRow[i], c->mBatchSendRow[i]};
+        }
+        std::vector<u32> ends, andWires;
+        std::vector<aby3g_lr_level> levels;
+        size_t gi = 0;
+        for (size_t L = 0; L < c->mLevelCounts.size(); ++L) {
+            aby3g_lr_level lv{};
+            const auto& batches = c->mLevelBatches[L];
+            lv.first_gate = batches.empty() ? 0 : batches.front().begin;
+            lv.nbatch = (u32)batches.size();
+            lv.batch_off = (u32)ends.size();
+            for (const auto& b : batches) ends.push_back(b.begin + b.count - lv.first_gate);
+            lv.and_wire_off = (u32)andWires.size();
+            for (u32 k = 0; k < c->mLevelCounts[L]; ++k, ++gi)
+                if (isAndType(c->mLevelGates[gi].type)) andWires.push_back(c->mLevelGates[gi].out);
+            lv.nand = (u32)andWires.size() - lv.and_wire_off;
+            if (lv.nand != c->mLevelAndCounts[L]) throw std::runtime_error("level AND count");
+            levels.push_back(lv);
+        }
+        std::vector<u8> host;
+        auto put = [&](const void* p, size_t bytes) {
+            const size_t off = (host.size() + 15) / 16 * 16;
+            host.resize(off + bytes);
+            if (bytes) std::memcpy(host.data() + off, p, bytes);
+            return off;
+        };
+        const size_t oG = put(gates.data(), gates.size() * sizeof(aby3g_gate));
+        const size_t oE = put(ends.data(), ends.size() * 4);
+        const size_t oL = put(levels.data(), levels.size() * sizeof(aby3g_lr_level));
+        const size_t oA = put(andWires.data(), andWires.size() * 4);
+        circuit.reset(g, host.size());
+        toDevice(circuit.data(), host.data(), host.size(), g);
+        const u8* base = circuit.as<u8>();
+        cir.nlevels = (u32)levels.size();
+        cir.wires = c->mWireCount;
+        cir.nand = c->mAndCount;
+        cir.ngates = (u32)gates.size();
+        for (int i = 0; i < 3; ++i) {
+            cir.in_wire[i] = c->mInputs[(size_t)i][0];
+            cir.out_wire[i] = c->mOutputs[(size_t)i][0];
+        }
+        cir.gates = reinterpret_cast<const aby3g_gate*>(base + oG);
+        cir.batch_ends = reinterpret_cast<const u32*>(base + oE);
+        cir.levels = reinterpret_cast<const aby3g_lr_level*>(base + oL);
+        cir.and_wires = reinterpret_cast<const u32*>(base + oA);
+    }
+
+    void step(aby3ML& ml, const si64Matrix& X, const si64Matrix& Y, si64Matrix& w, const u32* batchIdx, u64 aB,
+              u64* phaseTicks) {
+        Gpu& g = ml.mRt.gpu();
+        Sh3Evaluator& ev = ml.mEval;
+        Sh3ShareGen& gen = ev.mShareGen;
+        const int p = (int)ml.mRt.mPartyIdx;
+        aby3g_lr_iter it{};
+        it.party = p;
+        it.B = (u32)B;
+        it.d = (u32)d;
+        it.D = (u32)ml.mD;
+        it.aB = (u32)aB;
+        it.n = X.rows();
+        it.X = X.data();
+        it.Y = Y.data();
+        it.w = w.data();
+        it.batch = batchIdx;
+        it.cir = cir;
+        it.scratch = scratch.data();
+        it.mailbox = mailbox.data();
+        it.next_mailbox = nextBox;
+        it.prev_mailbox = prevBox;
+        it.epoch = ++epoch;
+        it.wait_ticks = g.waitTicks();
+        it.phase_ticks = phaseTicks;
+        std::memcpy(it.prev_seed, gen.mPrevSeed.data(), 16);
+        std::memcpy(it.next_seed, gen.mNextSeed.data(), 16);
+        std::memcpy(it.zs_prev, gen.mKeyPrev.data(), 16);
+        std::memcpy(it.zs_next, gen.mKeyNext.data(), 16);
+        std::memcpy(it.ot_next_key, ev.mOtNextKey.data(), 16);
+        std::memcpy(it.ot_prev_key, ev.mOtPrevKey.data(), 16);
+        // mul(XX, w): the truncation pair (Sh3Evaluator.cpp:526-527)
+        it.t1_next_off = gen.takeNext(8 * B);
+        it.t1_prev_off = gen.takePrev(8 * B);
+        // the piecewise circuit's setCir keys (Sh3BinaryEvaluator.h:96-102)
+        const block kp = gen.getPrevBlock(), kn = gen.getNextBlock();
+        std::memcpy(it.mask_prev, kp.data(), 16);
+        std::memcpy(it.mask_next, kn.data(), 16);
+        // region 1: the OT product (Sh3Evaluator.cpp:132-263)
+        if (p == 0) {
+            it.ot_prev_off = gen.takePrev(16 * B);
+            it.ot_next_off = gen.takeNext(8 * B);
+            it.ot_ctr = ev.mOtNextIdx;
+            ev.mOtNextIdx += 2 * B;
+        } else if (p == 1) {
+            it.ot_prev_off = gen.takePrev(8 * B);
+        } else {
+            it.ot_next_off = gen.takeNext(16 * B);
+            it.ot_ctr = ev.mOtPrevIdx;
+            ev.mOtPrevIdx += 2 * B;
+        }
+        // region 2: the public product (:430-487)
+        it.pm_draw = gen.takeDraws(B);
+        if (p == 0 || p == 1) {
+            it.pm_ctr_next = ev.mOtNextIdx;
+            ev.mOtNextIdx += B;
+        }
+        if (p == 0 || p == 2) {
+            it.pm_ctr_prev = ev.mOtPrevIdx;
+            ev.mOtPrevIdx += B;
+        }
+        // mulTruncate(XX^T, err): the truncation pair
+        it.t2_next_off = gen.takeNext(8 * d);
+        it.t2_prev_off = gen.takePrev(8 * d);
+        it.thr_off[0] = thrOff[0];
+        it.thr_off[1] = thrOff[1];
+        it.half = half;
+        it.slope = slope;
+        it.one = one;
+        GPU_CALL(aby3g_lr_iteration(&it, g.stream()));
+    }
+};
+
+void sgdLogisticStepOps(aby3ML& ml, const si64Matrix& X, const si64Matrix& Y, si64Matrix& w, const u32* batchIdx,
+                        u64 B, u64 aB, SgdState& st);
 
 void sgdLogisticStep(aby3ML& ml, const si64Matrix& X, const si64Matrix& Y, si64Matrix& w, const u32* batchIdx,
                      u64 B, u64 aB, SgdState& st) {
+    if (!st.fusedChecked) {
+        st.fused = FusedLr::make(ml, X.cols(), B);
+        st.fusedChecked = true;
+    }
+    if (st.fused && st.fused->B == B && st.fused->d == X.cols()) {
+        st.fused->step(ml, X, Y, w, batchIdx, aB, st.phaseTicks);
+        return;
+    }
+    sgdLogisticStepOps(ml, X, Y, w, batchIdx, B, aB, st);
+}
+
+// the op-by-op iteration (every step a C-ABI call, messages over the channels)
+void sgdLogisticStepOps(aby3ML& ml, const si64Matrix& X, const si64Matrix& Y, si64Matrix& w, const u32* batchIdx,
+                        u64 B, u64 aB, SgdState& st) {
     Gpu& g = ml.mRt.gpu();
     const u64 d = X.cols();
     // extractBatch (Regression.h:42-58)

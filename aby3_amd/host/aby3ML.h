@@ -18,6 +18,8 @@ public:
     void mulTruncate(const si64Matrix& left, const si64Matrix& right, si64Matrix& dest, u64 shift);
     // logisticFunc: piecewise sigmoid, thresholds -0.5 / 0.5, f = 0 | 0.5 + x | 1 (aby3ML.h:121-139)
     void logisticFunc(const si64Matrix& Y, si64Matrix& out);
+    // the sigmoid's piecewise description (set up on first use)
+    Sh3Piecewise& logistic();
 
     Sh3Runtime& mRt;
     Sh3Encryptor& mEnc;
@@ -26,9 +28,17 @@ public:
     Sh3Piecewise mLogistic;
 };
 
+struct FusedLr;
 struct SgdState {
     si64Matrix XX, YY, XXt, xw, fxw, err, update;
     DeviceBuffer idx;
+    // The fused iteration (aby3g_lr_iteration): one launch per party and
+    // iteration when the three parties share a device and process (their ring
+    // allows kernel hand-offs); set up by the first step, which all three
+    // parties take together.
+    std::shared_ptr<FusedLr> fused;
+    bool fusedChecked = false;
+    u64* phaseTicks = nullptr;  // optional device [16]: the fused launch's phase stamps (profiling)
 };
 
 // One SGD_Logistic iteration on the batch of B row indices at device pointer

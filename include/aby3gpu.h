@@ -465,6 +465,80 @@ typedef struct {
 int aby3g_bits_to_wires_lin(const aby3g_wire_src* srcs, uint32_t nsrc, uint64_t rows, uint64_t words,
                             aby3g_stream stream);
 
+/* ----------------------------------------- fused SGD_Logistic iteration -- */
+/* One whole SGD_Logistic iteration (aby3-ML/Regression.h:249-293) of one
+ * party in ONE launch, for three parties co-located on one device in one
+ * process: extractBatch, mul(XX, w) with truncation (Sh3Evaluator.cpp:
+ * 651-730), the piecewise sigmoid (Sh3Piecewise.cpp:184-567: the two-input
+ * resharing, the int_Sh3Piecewise_helper circuit level by level, the OT
+ * product and the public-constant product, Sh3Evaluator.cpp:119-263,
+ * 418-501), err = f - YY, mulTruncate(XX^T, err, aB) and w -= update.
+ * Every message goes through the parties' mailboxes with in-kernel hand-offs
+ * (aby3g_handoff's write-through payload + flag form); the randomness is the
+ * op-by-op path's, at the stream positions, draw indices and OT counters the
+ * host passes, so the shares are bit-identical to that path's.
+ *
+ * The levelized circuit, as device arrays (host-built from the levelized
+ * gate list; gates in batch order as for aby3g_bin_level). */
+typedef struct {
+    uint32_t first_gate;   /* index into gates of the level's first gate */
+    uint32_t nbatch;       /* batches of mutually independent gates */
+    uint32_t batch_off;    /* into batch_ends (relative to first_gate) */
+    uint32_t nand;         /* AND-type gates = send rows of the level */
+    uint32_t and_wire_off; /* into and_wires: the level's AND outputs in send-row order */
+    uint32_t pad[3];
+} aby3g_lr_level;
+typedef struct {
+    uint32_t nlevels, wires, nand, ngates;
+    uint32_t in_wire[3];  /* first wires of the 64-bit inputs aa_0, aa_1, b */
+    uint32_t out_wire[3]; /* the region outputs c_0, c_1, c_2 (1 bit each) */
+    const aby3g_gate* gates;
+    const uint32_t* batch_ends;
+    const aby3g_lr_level* levels;
+    const uint32_t* and_wires;
+} aby3g_lr_circuit;
+
+/* Arguments of one iteration of one party. Mailboxes: aby3g_lr_mailbox_bytes
+ * each, zeroed before the first iteration; a party writes only its own and
+ * reads its neighbours' (next = party + 1, prev = party + 2 mod 3). epoch:
+ * 1 for the first iteration, +1 per iteration, the same for the three. */
+typedef struct {
+    int32_t party;
+    uint32_t B, d, D, aB;
+    uint64_t n;              /* dataset rows */
+    const int64_t* X;        /* [2][n][d] */
+    const int64_t* Y;        /* [2][n][1] */
+    int64_t* w;              /* [2][d][1], updated in place */
+    const uint32_t* batch;   /* B row ids (getSubset) */
+    aby3g_lr_circuit cir;    /* int_Sh3Piecewise_helper(64, 2) */
+    void* scratch;           /* aby3g_lr_scratch_bytes */
+    void* mailbox;
+    const void* next_mailbox;
+    const void* prev_mailbox;
+    uint64_t epoch;
+    uint64_t* wait_ticks;    /* optional: in-kernel wait (100 MHz ticks) added here */
+    uint64_t* phase_ticks;   /* optional: [16] wall-clock stamps of the phases (profiling) */
+    /* the evaluator's ShareGen streams (seeds) and zero-share keys */
+    uint8_t prev_seed[16], next_seed[16];
+    uint8_t zs_prev[16], zs_next[16];
+    uint64_t t1_next_off, t1_prev_off;  /* mul(XX, w): truncation pair stream positions (bytes) */
+    uint64_t t2_next_off, t2_prev_off;  /* mulTruncate(XX^T, err): ditto */
+    uint8_t mask_prev[16], mask_next[16];  /* setCir keys of the circuit (getPrevBlock / getNextBlock) */
+    uint64_t ot_prev_off, ot_next_off;  /* the OT product's stream positions (bytes; per party) */
+    uint8_t ot_next_key[16], ot_prev_key[16];
+    uint64_t ot_ctr;                    /* the OT product's SharedOT counter (P0: next, P2: prev) */
+    uint64_t pm_ctr_next, pm_ctr_prev;  /* the public product's counters (P0 both; P1 next; P2 prev) */
+    uint64_t pm_draw;                   /* the public product's first zero-share draw */
+    int64_t thr_off[2];                 /* circuit input offsets -t_0, -t_1 (fixed point) */
+    int64_t half;                       /* region 1: half + slope * x */
+    int64_t slope;
+    int64_t one;                        /* region 2: the public constant */
+} aby3g_lr_iter;
+uint64_t aby3g_lr_mailbox_bytes(uint32_t B, uint32_t d, const aby3g_lr_circuit* cir);
+uint64_t aby3g_lr_scratch_bytes(uint32_t B, uint32_t d, const aby3g_lr_circuit* cir);
+/* ABY3G_EINVAL for shapes the fused form does not take (B > 2048, d > 4096). */
+int aby3g_lr_iteration(const aby3g_lr_iter* it, aby3g_stream stream);
+
 /* ------------------------------------------------ element-wise helpers -- */
 /* out[i] = ca*a[i] + cb*b[i] + c (mod 2^64); b may be NULL. Covers share
  * sums/differences (BuildingBlocks.cpp:475-480, Sh3Piecewise.cpp:403-470,

@@ -1,0 +1,90 @@
+// Phase profile of the fused SGD_Logistic iteration (aby3g_lr_iteration):
+// three co-located parties run `iters` iterations on a 10^6 x 128 dataset
+// (B = 256), every launch stamping its phases (wall clock, 100 MHz); prints
+// per party the median duration of each phase over the last half of the run.
+// Build: scripts/lr_phases.sh
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <thread>
+#include "aby3ML.h"
+
+using namespace aby3;
+
+int main(int argc, char** argv) {
+    const u64 n = argc > 1 ? atoll(argv[1]) : 1000000, d = 128, B = 256, D = 16, aB = 11;
+    const u64 iters = argc > 2 ? atoll(argv[2]) : 200;
+    i64Matrix X, Y, w0(d, 1);
+    logisticModelGen(logisticModel(d), n, D, X, Y);
+    std::vector<u32> idx(iters * B);
+    BatchSampler s(n);
+    std::vector<u64> b(B);
+    for (u64 t = 0; t < iters; ++t) {
+        s.next(b);
+        for (u64 i = 0; i < B; ++i) idx[t * B + i] = (u32)b[i];
+    }
+    const int dv[3] = {0, 0, 0};
+    auto comms = makeLocalRing(dv, true);
+    std::vector<std::vector<u64>> stamps(3);
+    double wallUs = 0;
+    std::thread th[3];
+    for (int p = 0; p < 3; ++p)
+        th[p] = std::thread([&, p] {
+            Sh3Runtime rt;
+            Sh3Encryptor enc;
+            Sh3Evaluator ev;
+            rt.init(p, comms[p], 0);
+            rt.gpu().aliasAux();
+            const MlSeeds ms = mlSeeds(p);
+            enc.init(p, ms.encPrev, ms.encNext);
+            ev.init(p, ms.evalPrev, ms.evalNext);
+            si64Matrix sX(n, d), sY(n, 1), sW(d, 1);
+            if (p == 0) {
+                enc.localIntMatrix(rt, X, sX).get();
+                enc.localIntMatrix(rt, Y, sY).get();
+                enc.localIntMatrix(rt, w0, sW).get();
+            } else {
+                enc.remoteIntMatrix(rt, sX).get();
+                enc.remoteIntMatrix(rt, sY).get();
+                enc.remoteIntMatrix(rt, sW).get();
+            }
+            aby3ML ml(rt, enc, ev, D);
+            SgdState st;
+            DeviceBuffer dIdx(rt.gpu(), idx.size() * 4), ticks(rt.gpu(), iters * 16 * 8);
+            toDevice(dIdx.data(), idx.data(), idx.size() * 4, rt.gpu());
+            rt.gpu().sync();
+            const auto t0 = std::chrono::steady_clock::now();
+            for (u64 t = 0; t < iters; ++t) {
+                st.phaseTicks = ticks.as<u64>() + 16 * t;
+                sgdLogisticStep(ml, sX, sY, sW, dIdx.as<u32>() + t * B, B, aB, st);
+            }
+            rt.gpu().sync();
+            if (p == 0)
+                wallUs = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+            stamps[p].resize(iters * 16);
+            toHost(stamps[p].data(), ticks.data(), iters * 16 * 8, rt.gpu());
+            if (!st.fused) std::printf("party %d: fused form NOT taken\n", p);
+        });
+    for (auto& t : th) t.join();
+    std::printf("wall %.1f us per iteration (%llu iterations)\n", wallUs / iters, (unsigned long long)iters);
+    const char* names[11] = {"aes table", "masks", "xw product", "trunc pair+post", "z wait+finalize",
+                             "reshare+inputs", "levels", "regions+fvals", "OT+public products", "err+XtE product",
+                             "trunc pair 2 / finalize / w"};
+    for (int p = 0; p < 3; ++p) {
+        std::printf("party %d:", p);
+        double tot = 0;
+        for (int ph = 0; ph < 11; ++ph) {
+            std::vector<double> v;
+            for (u64 t = iters / 2; t < iters; ++t)
+                v.push_back(0.01 * (double)(stamps[p][16 * t + ph + 1] - stamps[p][16 * t + ph]));
+            std::sort(v.begin(), v.end());
+            std::printf(" %s %.1f |", names[ph], v[v.size() / 2]);
+            tot += v[v.size() / 2];
+        }
+        std::vector<double> gap;  // launch-to-launch gap: end of t-1 to start of t
+        for (u64 t = iters / 2; t < iters; ++t) gap.push_back(0.01 * (double)(stamps[p][16 * t] - stamps[p][16 * (t - 1) + 11]));
+        std::sort(gap.begin(), gap.end());
+        std::printf(" total %.1f us, gap between launches %.1f us\n", tot, gap[gap.size() / 2]);
+    }
+    return 0;
+}

@@ -42,6 +42,12 @@ def test_oram_gpu():
 
 
 @pytest.mark.gpu
+def test_lr_iteration_both_forms_gpu():
+    # SGD_Logistic op by op and fused (aby3g_lr_iteration), share-exact vs the oracle
+    _run("test_lr", 600)
+
+
+@pytest.mark.gpu
 def test_convert_protocols_gpu():
     _run("test_convert", 600)
 

@@ -153,6 +153,13 @@ _SIGS = {
                                 c_uint64, c_uint64, c_void_p, c_void_p, c_void_p]),
     "aby3g_bin_level_rr": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_uint32, c_void_p, c_void_p, ctypes.c_uint32,
                                    c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p]),
+    # the aby3g_handoff / aby3g_lr_iter / aby3g_lr_circuit structs go by pointer
+    "aby3g_bin_level_hs": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_uint32, c_void_p, c_void_p, ctypes.c_uint32,
+                                   c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "aby3g_handoff_status": (c_int, [POINTER(ctypes.c_uint32)]),
+    "aby3g_lr_mailbox_bytes": (c_uint64, [ctypes.c_uint32, ctypes.c_uint32, c_void_p]),
+    "aby3g_lr_scratch_bytes": (c_uint64, [ctypes.c_uint32, ctypes.c_uint32, c_void_p]),
+    "aby3g_lr_iteration": (c_int, [c_void_p, c_void_p]),
     "aby3g_bits_to_wires2": (c_int, [c_void_p, c_uint64, c_uint64, ctypes.c_uint32, c_void_p, c_uint64, c_uint64,
                                      c_void_p]),
     "aby3g_wires_to_bits2": (c_int, [c_void_p, c_uint64, c_void_p, ctypes.c_uint32, c_uint64, c_void_p, c_uint64,

@@ -39,6 +39,8 @@ OVERRIDES = {
     "aby3g_probe_read": "*ms = 0; *launches = 0; return 0;",
     "aby3g_handoff_status": "*timeouts = 0; return 0;",
     "aby3g_aes_block_host": "for (int i = 0; i < 16; ++i) out[i] = key[i] ^ (uint8_t)(ctr >> (8 * (i & 7))); return 0;",
+    "aby3g_lr_mailbox_bytes": "return 4096;",
+    "aby3g_lr_scratch_bytes": "return 4096;",
     "aby3g_mul_workspace_bytes": "return mode == 1 ? (size_t)(M + 64) * (K + 64) * 16 + (N + 64) * (K + 64) * 16 + 4 * M * N * 8 : 0;",
 }
 
@@ -107,7 +109,7 @@ def main():
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     out = ['// generated by gen_nulldev.py -- host-memory stand-in for ASan runs of the host runtime',
            "#include <aby3gpu.h>", "#include <cstdlib>", "#include <cstring>", PREAMBLE, 'extern "C" {']
-    for m in re.finditer(r"(const char\*|int|size_t)\s+(aby3g_\w+)\s*\(([^;]*?)\)\s*;", text, flags=re.S):
+    for m in re.finditer(r"(const char\*|int|size_t|uint64_t)\s+(aby3g_\w+)\s*\(([^;]*?)\)\s*;", text, flags=re.S):
         ret, name, args = m.group(1), m.group(2), " ".join(m.group(3).split())
         body = OVERRIDES.get(name, "return 0;")
         out.append(f"{ret} {name}({args}) {{ {body} }}")

@@ -333,6 +333,7 @@ i64 ABY3PosMap::access(const boolIndex& index, const boolShare& fake) {
         bool_cipher_selector(pIdx, mainFlag, fetched, inStash, r, *eval, *runtime);
         physical = boolIndex(r.shareToHost(0)[0], r.shareToHost(1)[0]);
     }
+    last_physical_index = physical;
     return back2plain(pIdx, physical, *runtime);
 }
 

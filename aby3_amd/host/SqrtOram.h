@@ -74,18 +74,22 @@ public:
     i64 access(const boolIndex& index, const boolShare& fake);
     bool linear() const { return mLinear; }
 
+    // the state is public, as the reference's members are (read by the
+    // share-level parity test, tests/cpp/test_oram.cpp)
+    u64 n, pack, S, t = 0, map_len;
+    std::vector<boolIndex> permutation;      // linear map
+    std::vector<boolShare> usage_map;        // linear map
+    std::vector<ABY3PackedIndex> packed_index, stash;
+    std::unique_ptr<ABY3PosMap> subPosMap;
+    boolIndex last_physical_index;  // the last access's physical index, before back2plain opens it
+
 private:
     void linear_ram(const std::vector<sbMatrix>& data, const boolIndex& index, sbMatrix& res);
-    u64 n, pack, S, t = 0, map_len;
     bool mLinear;
     int pIdx;
     Sh3Encryptor* enc;
     Sh3Evaluator* eval;
     Sh3Runtime* runtime;
-    std::vector<boolIndex> permutation;      // linear map
-    std::vector<boolShare> usage_map;        // linear map
-    std::vector<ABY3PackedIndex> packed_index, stash;
-    std::unique_ptr<ABY3PosMap> subPosMap;
 };
 
 // SqrtOram.h:389-450 (SqrtOram, oram.h:203-275)

@@ -329,3 +329,85 @@ Shared shuffleRows(std::array<Party, 3>& enc, const Shared& T);     // efficient
 Shared shuffleWithPermutation(std::array<Party, 3>& enc, const Shared& T, Shared& Pi);
 
 }  // namespace orc
+
+#include <functional>
+#include <memory>
+
+namespace orc {
+
+// --------------------------------------------------------------------------
+// Square-root ORAM (aby3-Basic/SqrtOram.h over Oram/include/oram.h;
+// orc_oram.cpp). boolShare / boolIndex values of the three parties: s[p] =
+// party p's (share 0, share 1).
+// --------------------------------------------------------------------------
+struct Index3 {
+    std::array<std::array<i64, 2>, 3> s{};
+    static Index3 pub(i64 plain);  // boolIndex(plain, pIdx)
+};
+struct Bool3 {
+    std::array<std::array<bool, 2>, 3> s{};
+    static Bool3 pub(bool plain);  // boolShare(plain, pIdx)
+    static Bool3 initFalse();      // bool_init_false
+};
+// the circuits the BoolBasic helpers evaluate, supplied by the caller (the
+// product's circuit library; cryptoTools' BetaLibrary is not vendored)
+struct OramCircuits {
+    Circuit eq64;   // int_eq(64)
+    Circuit and64;  // int_int_bitwiseAnd(64)
+    Circuit or1;    // int_int_bitwiseOr(1)
+};
+// BoolBasic.cpp helpers over the evaluators (each call = one fresh evaluator)
+struct OramOps {
+    std::array<Party, 3>* ev;
+    const OramCircuits* cir;
+    Shared eq(const Shared& A, const Shared& B);                   // :42-62
+    Shared eqPlain(const Shared& A, const std::vector<i64>& b);    // :64-100
+    Shared and64(const Shared& A, const Shared& B);                // :187-209
+    Shared or1(const Shared& A, const Shared& B);                  // :102-122
+    Bool3 orBool(const Bool3& a, const Bool3& b);                  // :124-141
+    Bool3 notBool(const Bool3& a);                                 // :373-391
+    Shared dotRows(const Shared& A, const Shared& B);              // :393-423
+    Shared dotUnits(const std::vector<Shared>& A, Shared B, bool bOneBit);  // :463-515
+    Shared selector(const Bool3& flag, const Shared& t, const Shared& f);   // :425-461
+    Shared firstZeroMask(const std::vector<Bool3>& A);             // :596-640
+    i64 back2plain(const Index3& x);                               // :895-904
+};
+struct PackedIndex3 {  // ABY3PackedIndex (SqrtOram.h:17-61)
+    std::vector<Index3> packed;
+    Index3 logical;
+};
+// ABY3PosMap (SqrtOram.h:63-369); enc drives the shuffles of the packed maps
+class PosMap3 {
+public:
+    PosMap3(std::array<Party, 3>& enc, OramOps& ops, u64 n, u64 pack, u64 S, const std::vector<Index3>& perm);
+    i64 access(const Index3& index, const Bool3& fake);
+    std::vector<i64> dump(int p) const;  // party p's state, this level then the sub-map's
+    u64 n, pack, S, t = 0, map_len;
+    bool linear;
+    std::vector<Index3> permutation;
+    std::vector<Bool3> usage_map;
+    std::vector<PackedIndex3> packed_index, stash;
+    std::unique_ptr<PosMap3> subPosMap;
+    Index3 last_physical;  // shares of the last access's physical index, before it is opened
+
+private:
+    Shared linearRam(const std::vector<Shared>& data, const Index3& index);
+    std::array<Party, 3>* enc;
+    OramOps* ops;
+};
+// ABY3SqrtOram (SqrtOram.h:371-450)
+class SqrtOram3 {
+public:
+    SqrtOram3(std::array<Party, 3>& enc, OramOps& ops, u64 n, u64 S, u64 pack);
+    void initiate(const std::vector<Shared>& data);
+    Shared access(const Index3& index);
+    u64 n, S, pack;
+    std::vector<Shared> shuffle_mem;
+    std::unique_ptr<PosMap3> posMap;
+
+private:
+    std::array<Party, 3>* enc;
+    OramOps* ops;
+};
+
+}  // namespace orc

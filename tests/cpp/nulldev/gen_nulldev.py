@@ -14,14 +14,16 @@ HDR = os.path.join(HERE, "..", "..", "..", "include", "aby3gpu.h")
 OVERRIDES = {
     "aby3g_last_error": 'return "";',
     "aby3g_version": "return 1;",
-    "aby3g_device_count": "*n = 1; return 0;",
-    "aby3g_get_device": "*device = 0; return 0;",
+    "aby3g_device_count": "*n = ND_DEVICES; return 0;",
+    "aby3g_set_device": "if (device < 0 || device >= ND_DEVICES) return 1; t_device = device; return 0;",
+    "aby3g_get_device": "*device = t_device; return 0;",
+    "aby3g_enable_peer_access": "return nd_peer(device, peer);",
     "aby3g_api_time": "*us = 0; *calls = 0; return 0;",
     "aby3g_malloc": "*ptr = nd_alloc(bytes); return *ptr ? 0 : 1;",
     "aby3g_free": "nd_free(ptr); return 0;",
     "aby3g_host_malloc": "*ptr = calloc(1, bytes ? bytes : 1); return *ptr ? 0 : 1;",
     "aby3g_host_free": "free(ptr); return 0;",
-    "aby3g_memcpy": "if (bytes) memmove(dst, src, bytes); return 0;",
+    "aby3g_memcpy": "if (kind == 3) g_kind3.fetch_add(1); if (bytes) memmove(dst, src, bytes); return 0;",
     "aby3g_memset": "if (bytes) memset(dst, value, bytes); return 0;",
     "aby3g_stream_create": "*stream = new int(0); return 0;",
     "aby3g_stream_destroy": "delete (int*)stream; return 0;",
@@ -58,6 +60,22 @@ PREAMBLE = r"""
 #include <sys/mman.h>
 #include <thread>
 #include <unistd.h>
+// three "devices" with distinct ordinals, so the host runtime's cross-device
+// branches (peer access between parties' devices, peer copies of staged
+// messages) run here too; the current device is per thread, as in HIP
+constexpr int ND_DEVICES = 3;
+static thread_local int t_device = 0;
+static std::atomic<unsigned> g_peer{0};       // bit 3 * device + peer: access enabled
+static std::atomic<unsigned long> g_kind3{0}; // copies between devices (kind 3)
+static int nd_peer(int device, int peer) {
+    if (device < 0 || peer < 0 || device >= ND_DEVICES || peer >= ND_DEVICES || device == peer) return 1;
+    g_peer.fetch_or(1u << (3 * device + peer));
+    return 0;
+}
+extern "C" void nulldev_stats(unsigned* peer_bits, unsigned long* kind3_copies) {
+    *peer_bits = g_peer.load();
+    *kind3_copies = g_kind3.load();
+}
 static char* g_arena = nullptr;
 static std::atomic<size_t>* g_off = nullptr;
 static size_t g_cap = 0;

@@ -13,8 +13,11 @@
 #include <vector>
 
 extern "C" int nulldev_shared_arena(size_t bytes);
+extern "C" void nulldev_stats(unsigned* peer_bits, unsigned long* kind3_copies);
 
-static int party_main(int party, const std::string& tag) {
+// ownDevice: party p on device p (the north-star layout, three GPUs): the
+// receiver's copy out of the sender's staging slot is then a peer copy
+static int party_main(int party, const std::string& tag, bool ownDevice) {
     struct J {
         int job;
         std::vector<uint64_t> p;
@@ -28,7 +31,8 @@ static int party_main(int party, const std::string& tag) {
     int k = 0;
     for (auto& j : jobs) {
         const std::string link = tag + "." + std::to_string(k++);
-        aby3h_session* s = aby3h_party_create(j.job, j.p.data(), (int)j.p.size(), party, 0, link.c_str(), 1, 0);
+        aby3h_session* s = aby3h_party_create(j.job, j.p.data(), (int)j.p.size(), party, ownDevice ? party : 0,
+                                              link.c_str(), ownDevice ? 0 : 1, 0);
         if (!s) {
             std::printf("FAIL party %d create job %d: %s\n", party, j.job, aby3h_last_error());
             return 1;
@@ -41,6 +45,15 @@ static int party_main(int party, const std::string& tag) {
         aby3h_session_info(s, info, ABY3H_INFO_COUNT);
         aby3h_session_destroy(s);
     }
+    if (ownDevice) {
+        unsigned peers = 0;
+        unsigned long kind3 = 0;
+        nulldev_stats(&peers, &kind3);
+        if (!kind3) {
+            std::printf("FAIL party %d: no peer copy on its own device\n", party);
+            return 1;
+        }
+    }
     return 0;
 }
 
@@ -49,20 +62,22 @@ int main(int argc, char** argv) {
     // `party_procs <party> <tag>`: one party only, started by a launcher
     // (tests/test_dist.py: three gloo ranks, one party each, sharing the
     // named arena ND_ARENA)
-    if (argc == 3) return party_main(atoi(argv[1]), argv[2]);
-    const std::string tag = "t" + std::to_string(getpid());
-    pid_t kids[3];
-    for (int p = 0; p < 3; ++p) {
-        kids[p] = fork();
-        if (kids[p] == 0) _exit(party_main(p, tag));
-    }
+    if (argc == 3) return party_main(atoi(argv[1]), argv[2], false);
     int bad = 0;
-    for (int p = 0; p < 3; ++p) {
-        int st = 0;
-        waitpid(kids[p], &st, 0);
-        if (!WIFEXITED(st) || WEXITSTATUS(st) != 0) {
-            std::printf("party %d exited with status %d\n", p, st);
-            bad = 1;
+    for (int own = 0; own < 2 && !bad; ++own) {  // one device, then a device per party
+        const std::string tag = "t" + std::to_string(getpid()) + "d" + std::to_string(own);
+        pid_t kids[3];
+        for (int p = 0; p < 3; ++p) {
+            kids[p] = fork();
+            if (kids[p] == 0) _exit(party_main(p, tag, own != 0));
+        }
+        for (int p = 0; p < 3; ++p) {
+            int st = 0;
+            waitpid(kids[p], &st, 0);
+            if (!WIFEXITED(st) || WEXITSTATUS(st) != 0) {
+                std::printf("party %d exited with status %d (%s)\n", p, st, own ? "own devices" : "one device");
+                bad = 1;
+            }
         }
     }
     if (!bad) std::printf("party_procs: ok\n");

@@ -7,6 +7,8 @@
 #include <cstdio>
 #include <vector>
 
+extern "C" void nulldev_stats(unsigned* peer_bits, unsigned long* kind3_copies);
+
 static int fail(const char* what) {
     std::printf("FAIL %s: %s\n", what, aby3h_last_error());
     return 1;
@@ -24,9 +26,14 @@ int main() {
         {ABY3H_JOB_MSB, {3000}, 2},                    {ABY3H_JOB_LR, {2048, 16, 64, 16, 11}, 3},
         {ABY3H_JOB_SORT, {4096}, 1},                  {ABY3H_JOB_MUL_TRUNC, {64, 48, 80, 16, 1}, 2},
     };
-    for (int round = 0; round < 2; ++round)
+    // rounds 0 / 1: the three parties on one device, without and with probes;
+    // round 2: each on its own device (the north-star layout inside one
+    // process): peer access both ways and peer copies of staged messages
+    const int dev3[3] = {0, 1, 2};
+    for (int round = 0; round < 3; ++round)
         for (auto& j : jobs) {
-            aby3h_session* s = aby3h_session_create(j.job, j.p.data(), (int)j.p.size(), dev, round);
+            aby3h_session* s =
+                aby3h_session_create(j.job, j.p.data(), (int)j.p.size(), round == 2 ? dev3 : dev, round == 1);
             if (!s) return fail("create");
             if (aby3h_session_run(s, j.steps)) return fail("run");
             if (aby3h_session_check(s) == 2) return fail("check");
@@ -35,6 +42,18 @@ int main() {
             aby3h_session_probe(s, 0, &ms, &n);
             aby3h_session_destroy(s);
         }
+    unsigned peers = 0;
+    unsigned long kind3 = 0;
+    nulldev_stats(&peers, &kind3);
+    if (peers != 0xEEu) {  // every ordered pair of distinct devices
+        std::printf("FAIL peer access enabled for pairs 0x%x, expected 0xee\n", peers);
+        return 1;
+    }
+    if (!kind3) {
+        std::printf("FAIL no copy between devices on three devices\n");
+        return 1;
+    }
+    std::printf("cross-device: peer pairs 0x%x, %lu copies between devices\n", peers, kind3);
     std::vector<int64_t> a(64 * 48, 3), b(48 * 80, 5), sh(6 * 64 * 80), pl(64 * 80);
     if (aby3h_sim_mul(0, 1, 1, 16, a.data(), b.data(), 64, 48, 80, sh.data(), pl.data())) return fail("sim_mul");
     std::vector<int64_t> x(300, 1), y(300, 2), o(300), osh(6 * 300);

@@ -618,8 +618,9 @@ int aby3g_bin_level_hs(const aby3g_gate* gates, const uint32_t* recv_rows, const
         ABY3G_REQUIRE(!(post && post->flags) || sendbuf, "a hand-off post without a send buffer");
         if ((!nbatches && !nunpack) || !words) return;
         // one workgroup per chunk; in-kernel hand-offs are used only for
-        // launches of at most 64 chunks (Channel::handoffPost), so the spinning
-        // workgroups of two parties' launches never fill the device
+        // launches of at most 64 chunks, or 512 from a light producer
+        // (Channel::handoffPost), so the spinning workgroups of two parties'
+        // launches never fill the device (4 of the 5 wave slots per SIMD)
         const u32 wgs = (u32)(words / kLevelWords);
         const HsWait hw = hs_wait_arg(wait);
         const HsPost hp = hs_post_arg(post);

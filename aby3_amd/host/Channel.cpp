@@ -61,9 +61,21 @@ struct LinkSlot {
 };
 }  // namespace
 
-// in-kernel hand-offs: messages of at most kHandoffMaxChunks chunks (128 Ki rows)
+// in-kernel hand-offs: messages of at most kHandoffMaxChunks chunks (128 Ki
+// rows), or of at most kHandoffChunks chunks (1 Mi rows) from a light
+// producer. Residency bound: the level kernel (94 VGPRs, 5 waves per SIMD)
+// takes one wave per SIMD per 2048-row workgroup, so two parties' consumer
+// launches of 512 workgroups spinning on 256 CUs hold 4 of the 5 slots of
+// every SIMD and the producer always finds one (binary.hip, k_bin_level).
 constexpr u64 kHandoffMaxChunks = 64;
-constexpr u64 kHandoffChunks = kHandoffMaxChunks;  // flags per direction
+constexpr u64 kHandoffChunks = 512;  // flags per direction
+// A producing launch of at most this many HBM bytes is light: its consumer's
+// workgroups spin only briefly. On C3 / C5 (2^20 / 2^19 rows, 512 / 256
+// chunks) in one A/B (scripts/gpu_ab_env.sh): stream hand-offs for every
+// large message 0.386-0.399 ms / 80.3-80.8 ms; in-kernel from producers of
+// <= 2 MiB the same; <= 8 MiB 0.376-0.382 / 75.6-76.6; <= 32 MiB
+// 0.363-0.368 / 72.1-73.6; every level in-kernel 0.376-0.384 / 75.7-75.9.
+constexpr u64 kHandoffLightBytes = (u64)32 << 20;
 
 // how long a receive polls before it sleeps on the condition variable
 constexpr int kSpinUs = 500;
@@ -435,7 +447,7 @@ void Channel::asyncSendShared(std::shared_ptr<DeviceBuffer> buf, size_t bytes, G
     mOut->push(std::move(m));
 }
 
-aby3g_handoff Channel::handoffPost(Gpu& gpu, u64 rows) {
+aby3g_handoff Channel::handoffPost(Gpu& gpu, u64 rows, u64 producerBytes) {
     if (!mOut) throw std::runtime_error("channel not connected");
     Pipe& p = *mOut;
     if (!p.kernelHandoff || p.link || p.signalDevice != gpu.device() || kernelsSerialized())
@@ -455,10 +467,12 @@ aby3g_handoff Channel::handoffPost(Gpu& gpu, u64 rows) {
         return aby3g_handoff{nullptr, 0, nullptr};
     }
     const u64 chunks = std::max<u64>(1, (rows + ABY3G_HANDOFF_ROWS - 1) / ABY3G_HANDOFF_ROWS);
-    // Large messages keep the stream hand-off: a consumer launch of many
-    // workgroups would hold its CUs spinning while the producer still runs
-    // (measured slower on C3 / C5 at 512 chunks); small ones are latency-bound
-    if (chunks > kHandoffMaxChunks) return aby3g_handoff{nullptr, 0, nullptr};
+    // Large messages from a heavy producer keep the stream hand-off: a
+    // consumer launch of many workgroups would hold its CUs spinning while the
+    // producer still runs (measured slower on C3 / C5 at 512 chunks with every
+    // level handed over in-kernel); small ones are latency-bound
+    if (chunks > kHandoffChunks || (chunks > kHandoffMaxChunks && producerBytes > kHandoffLightBytes))
+        return aby3g_handoff{nullptr, 0, nullptr};
     return aby3g_handoff{p.hsFlags, ++p.hsSeq, nullptr};
 }
 

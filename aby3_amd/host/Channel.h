@@ -82,7 +82,9 @@ public:
     // rows (aby3g_handoff); flags null when this channel cannot do it. The
     // producer is enqueued with it, then the message is sent with
     // asyncSendShared(buf, bytes, gpu, posted): no stream operation.
-    aby3g_handoff handoffPost(Gpu& gpu, u64 rows);
+    // producerBytes: HBM bytes of the producing launch (large messages go
+    // in-kernel only from light producers)
+    aby3g_handoff handoffPost(Gpu& gpu, u64 rows, u64 producerBytes = 0);
     // Both directions join parties on `gpu`'s device in this process whose
     // ring allows kernel hand-offs (a fused launch may then address the
     // peer's device memory and poll it).

@@ -386,7 +386,8 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
         send = DeviceBuffer::view(mSendAll, mAndDone * rowBytes, nAnd * rowBytes);
     }
     mAndDone += nAnd;
-    if (nAnd) hp = comm.mNext.handoffPost(g, mRows);
+    // this level's bytes (about 72 per gate and 64-row word)
+    if (nAnd) hp = comm.mNext.handoffPost(g, mRows, (u64)mCir->mLevelCounts[mLevel] * mWords * 72);
     if (nb && mZPending) waitZ();
     if (nb || nUnpack) {
         const aby3g_gate* gl = nb ? mCur->gates + mCur->levelFirstGate[mLevel] : nullptr;

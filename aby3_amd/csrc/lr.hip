@@ -43,7 +43,21 @@ constexpr u32 kLrMaxD = 4096;
 constexpr u64 kLrDynLdsMax = 88 << 10;
 
 // mailbox flags (one u64 each; value = epoch of the last message published)
-enum : u32 { F_Z1 = 0, F_V = 1, F_OT1 = 2, F_OT2 = 3, F_PM = 4, F_Z2 = 5, F_LVL = 8 };
+// F_H1 / F_H2: the helper workgroups' arrival counters (own mailbox only;
+// epoch * helpers once every helper published); F_ERR = F_LVL + nlevels:
+// workgroup 0's err vector published to its helpers
+enum : u32 { F_Z1 = 0, F_V = 1, F_OT1 = 2, F_OT2 = 3, F_PM = 4, F_Z2 = 5, F_H1 = 6, F_H2 = 7, F_LVL = 8 };
+
+// Helper workgroups (blocks 1..G of the launch): the two dataset products
+// gather the batch rows from all over the dataset, which one CU does at a few
+// tens of GB/s; G CUs split the rows instead (kLrHelperRows each). Block 0
+// runs the protocol as before and meets them through its own mailbox.
+constexpr u32 kLrHelperRows = 16;
+constexpr u32 kLrMaxHelpers = 32;
+__host__ __device__ inline u32 lr_helpers(u32 B) {
+    const u32 g = (B + kLrHelperRows - 1) / kLrHelperRows;
+    return g > kLrMaxHelpers ? kLrMaxHelpers : g;
+}
 
 // The expanded AES keys of an iteration (kernel argument).
 struct LrKeys {
@@ -60,11 +74,11 @@ struct Layout {
     u64 flags, region;
     u64 z1, v, lvl, ots, oth, otc, pma, pmb, z2;
     // scratch
-    u64 xw, a, fr, f2, yy, err, z1own, z2own, upd, reg, zmask, mem, prod, total;
+    u64 xw, a, fr, f2, yy, err, z1own, z2own, upd, reg, zmask, mem, prod, hprod, hy, hpart, total;
     __host__ __device__ Layout(u32 B, u32 d, const aby3g_lr_circuit& c) {
         W = (B + 63) / 64;
         Wpad = 32 * (((u64)B + 2047) / 2048);
-        flags = ((F_LVL + (u64)c.nlevels + 31) / 32) * 32;
+        flags = ((F_LVL + (u64)c.nlevels + 1 + 31) / 32) * 32;
         u64 o = 0;
         z1 = o, o += B;
         v = o, o += B;
@@ -90,10 +104,28 @@ struct Layout {
         zmask = o, o += (u64)c.nand * W;
         mem = o, o += 2 * (u64)c.wires * W;
         prod = o, o += (B > d ? B : d);
+        hprod = o, o += B;                          // helpers: XX w products, one per batch row
+        hy = o, o += 2 * (u64)B;                    // helpers: YY (both shares)
+        hpart = o, o += (u64)lr_helpers(B) * d;     // helpers: partial XX^T err, one d-vector each
         total = o;
     }
     __host__ __device__ u64 mailboxWords() const { return flags + 2 * region; }
 };
+
+static_assert(kLrThreads == 512, "the XtE reduction adds eight waves' partial sums in two halves of part[]");
+
+struct u64x2 {
+    u64 x, y;
+};
+// p[0], p[1] (p[1] only when `pair`): one 16-byte load when p is 16-byte aligned
+__device__ __forceinline__ u64x2 load_pair(const u64* p, bool pair) {
+    if (pair && !((uintptr_t)p & 15)) {
+        typedef u64 v2u64 __attribute__((ext_vector_type(2)));
+        const v2u64 v = *reinterpret_cast<const v2u64*>(p);
+        return u64x2{v.x, v.y};
+    }
+    return u64x2{p[0], pair ? p[1] : 0};
+}
 
 // word j of PRNG(k): half (j & 1) of AES(k, j >> 1)
 __device__ __forceinline__ u64 stream_word(const u32* T, const AesKey& k, u64 j) {
@@ -137,9 +169,149 @@ __device__ __forceinline__ void lr_trunc_finalize(const u64* zn, const u64* zp, 
     }
 }
 
+// An agent-scope acquire for the whole workgroup (cdna_hip_programming.md
+// Guideline 16): one lane's fence drops this CU's stale L1 lines, its wait and
+// the barrier put every wave's later plain loads behind it.
+__device__ __forceinline__ void lr_acquire() {
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
+// Every storing wave drains its write-through stores, then one lane adds 1 to
+// counter f of the own mailbox (the arrival of one helper).
+__device__ __forceinline__ void lr_arrive(u64* box, u32 f) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add((gu64*)box + f, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Helper workgroup h = blockIdx.x - 1 of the launch: batch rows
+// [h R, min(B, (h + 1) R)), R = ceil(B / G).
+//   phase 1: hprod[i] = XX0[i] (w0 + w1) + XX1[i] w0 and hy = YY of its rows,
+//            then arrives on F_H1 (block 0 waits for epoch * G);
+//   phase 4: after block 0's err (F_ERR), hpart[h] = sum over its rows of
+//            XX0[i] (e0 + e1)[i] + XX1[i] e0[i], then arrives on F_H2.
+// A wave per row (rows wave, wave + 8, ...), lanes over k pairs (16-byte
+// loads), kLrHelperUnroll rows of a wave in flight.
+constexpr u32 kLrHelperUnroll = 4;
+__device__ __noinline__ void lr_helper(const aby3g_lr_iter& it, u32* status, u64* part) {
+    const u32 B = it.B, d = it.d, G = lr_helpers(B), h = blockIdx.x - 1;
+    const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const Layout L(B, d, it.cir);
+    u64* sc = (u64*)it.scratch;
+    u64* box = (u64*)it.mailbox;
+    const u64 ep = it.epoch, n = it.n;
+    const u64* X0 = (const u64*)it.X;
+    const u64* X1 = X0 + n * d;
+    const u64* Y0 = (const u64*)it.Y;
+    const u64* Y1 = Y0 + n;
+    const u64* w0 = (const u64*)it.w;
+    const u64* w1 = w0 + d;
+    const u32 R = (B + G - 1) / G, r0 = h * R, r1 = min(B, r0 + R);
+
+    // ---- phase 1 ----
+    for (u32 i0 = r0 + wave; i0 < r1; i0 += kLrWaves * kLrHelperUnroll) {
+        u64 acc[kLrHelperUnroll], row[kLrHelperUnroll];
+#pragma unroll
+        for (u32 u = 0; u < kLrHelperUnroll; ++u) {
+            acc[u] = 0;
+            const u32 i = i0 + u * kLrWaves;
+            row[u] = it.batch[i < r1 ? i : r0];
+        }
+        for (u32 k = 2 * lane; k < d; k += 128) {
+            const bool pair = k + 1 < d;
+            const u64 ws0 = w0[k] + w1[k], wa0 = w0[k];
+            const u64 ws1 = pair ? w0[k + 1] + w1[k + 1] : 0, wa1 = pair ? w0[k + 1] : 0;
+            u64x2 a0[kLrHelperUnroll], a1[kLrHelperUnroll];
+#pragma unroll
+            for (u32 u = 0; u < kLrHelperUnroll; ++u) {
+                a0[u] = load_pair(X0 + row[u] * d + k, pair);
+                a1[u] = load_pair(X1 + row[u] * d + k, pair);
+            }
+#pragma unroll
+            for (u32 u = 0; u < kLrHelperUnroll; ++u)
+                acc[u] += a0[u].x * ws0 + a0[u].y * ws1 + a1[u].x * wa0 + a1[u].y * wa1;
+        }
+#pragma unroll
+        for (u32 u = 0; u < kLrHelperUnroll; ++u) {
+            u64 a = acc[u];
+#pragma unroll
+            for (int o = 32; o; o >>= 1) a += __shfl_xor(a, o, 64);
+            const u32 i = i0 + u * kLrWaves;
+            if (i < r1) {
+                if (lane == 0) hs_store(sc + L.hprod + i, a);
+                if (lane == 1) hs_store(sc + L.hy + i, Y0[row[u]]);
+                if (lane == 2) hs_store(sc + L.hy + B + i, Y1[row[u]]);
+            }
+        }
+    }
+    lr_arrive(box, F_H1);
+
+    // ---- phase 4 ----
+    // block 0's err comes only after its circuit and products (~80 us): until
+    // its F_PM flag (phase 3) poll rarely, so that the helpers' polls do not
+    // load the memory path of the parties' hand-offs; then poll closely
+    if (threadIdx.x == 0) {
+        const u64 t0 = wall_clock64();
+        for (u32 spins = 0; __hip_atomic_load((const gu64*)box + F_PM, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ep;) {
+            __builtin_amdgcn_s_sleep(32);
+            if ((++spins & 15) == 0 && (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+                                        wall_clock64() - t0 > kHandoffTimeoutTicks))
+                break;  // the close wait below gives up too
+        }
+    }
+    __syncthreads();
+    if (!hs_wait(HsWait{box, ep, nullptr, status}, F_LVL + it.cir.nlevels, F_LVL + it.cir.nlevels + 1)) return;
+    const u64* e0 = sc + L.err;
+    const u64* e1 = e0 + B;
+    for (u32 k0 = 0; k0 < d; k0 += 128) {
+        const u32 k = k0 + 2 * lane;
+        const bool kin = k < d, pair = k + 1 < d;
+        u64 acc0 = 0, acc1 = 0;
+        for (u32 i0 = r0 + wave; i0 < r1; i0 += kLrWaves * kLrHelperUnroll) {
+            u64x2 a0[kLrHelperUnroll], a1[kLrHelperUnroll];
+            u64 ev0[kLrHelperUnroll], evs[kLrHelperUnroll];
+#pragma unroll
+            for (u32 u = 0; u < kLrHelperUnroll; ++u) {
+                const u32 i = i0 + u * kLrWaves;
+                const bool in = i < r1;
+                const u64 rw = it.batch[in ? i : r0];
+                a0[u] = kin && in ? load_pair(X0 + rw * d + k, pair) : u64x2{0, 0};
+                a1[u] = kin && in ? load_pair(X1 + rw * d + k, pair) : u64x2{0, 0};
+                ev0[u] = in ? hs_load(e0 + i) : 0;  // written by block 0 on another CU
+                evs[u] = in ? ev0[u] + hs_load(e1 + i) : 0;
+            }
+#pragma unroll
+            for (u32 u = 0; u < kLrHelperUnroll; ++u) {
+                acc0 += a0[u].x * evs[u] + a1[u].x * ev0[u];
+                acc1 += a0[u].y * evs[u] + a1[u].y * ev0[u];
+            }
+        }
+        // waves 0-3 store, waves 4-7 add, then one sum of four per k
+        if (wave < 4) {
+            part[wave * 128 + 2 * lane] = acc0;
+            part[wave * 128 + 2 * lane + 1] = acc1;
+        }
+        __syncthreads();
+        if (wave >= 4) {
+            part[(wave - 4) * 128 + 2 * lane] += acc0;
+            part[(wave - 4) * 128 + 2 * lane + 1] += acc1;
+        }
+        __syncthreads();
+        if (tid < 128 && k0 + tid < d)
+            hs_store(sc + L.hpart + (u64)h * d + k0 + tid, part[tid] + part[128 + tid] + part[256 + tid] + part[384 + tid]);
+        __syncthreads();
+    }
+    lr_arrive(box, F_H2);
+}
+
 // phase stamps for profiling (aby3g_lr_iter.phase_ticks): wall clock of slot s
 __device__ __forceinline__ void lr_stamp(u64* ticks, u32 s) {
     if (ticks && threadIdx.x == 0) ticks[s] = wall_clock64();
+    // shader-clock counter beside the first and last stamps (slots 13, 14):
+    // the clock the iteration actually ran at
+    if (ticks && threadIdx.x == 0 && (s == 0 || s == 11)) ticks[s == 0 ? 13 : 14] = clock64();
 }
 
 __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict__ T0g, aby3g_lr_iter it, LrKeys K,
@@ -147,14 +319,18 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
     __shared__ u32 lds[kAesLdsWords];
     __shared__ u64 part[kLrThreads];
     extern __shared__ __attribute__((aligned(16))) u64 dyn[];  // [2][wires][W] engine memory, then [nand][W] masks
+    if (blockIdx.x > 0) {
+        lr_helper(it, status, part);
+        return;
+    }
     u64* const PT = it.phase_ticks;
     lr_stamp(PT, 0);
     aes_fill_lds(lds, T0g);
+    lr_stamp(PT, 12);
     const u32* T = lds;
     const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int p = it.party;
     const u32 B = it.B, d = it.d;
-    const u64 n = it.n;
     const aby3g_lr_circuit& cir = it.cir;
     const Layout L(B, d, cir);
     const u64 W = L.W;
@@ -168,10 +344,6 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
     const u64* pv = pbox + L.flags + par;            // prev party's
     const u64 ep = it.epoch;
     u64* ticks = it.wait_ticks;
-    const u64* X0 = (const u64*)it.X;
-    const u64* X1 = X0 + n * d;
-    const u64* Y0 = (const u64*)it.Y;
-    const u64* Y1 = Y0 + n;
     u64* w0 = (u64*)it.w;
     u64* w1 = w0 + d;
     u64* xw0 = sc + L.xw;
@@ -197,37 +369,11 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
 
     lr_stamp(PT, 1);
     // ---- phase 1: xw = mul(XX, w) with truncation (shift D) ----
-    // a wave per row, lanes over k; 8 rows of a wave at a time, so that every
-    // lane has 16 independent row loads in flight (the rows are scattered
-    // over the dataset: HBM latency, not bandwidth)
-    constexpr u32 kRowsAtOnce = 8;
-    for (u32 r0 = wave * kRowsAtOnce; r0 < B; r0 += kLrWaves * kRowsAtOnce) {
-        u64 acc[kRowsAtOnce];
-        u64 rowOf[kRowsAtOnce];
-#pragma unroll
-        for (u32 j = 0; j < kRowsAtOnce; ++j) {
-            acc[j] = 0;
-            rowOf[j] = r0 + j < B ? it.batch[r0 + j] : 0;
-        }
-        for (u32 k = lane; k < d; k += 64) {
-            const u64 ws = w0[k] + w1[k], wa = w0[k];
-            u64 a0[kRowsAtOnce], a1[kRowsAtOnce];
-#pragma unroll
-            for (u32 j = 0; j < kRowsAtOnce; ++j) {
-                a0[j] = r0 + j < B ? X0[rowOf[j] * d + k] : 0;
-                a1[j] = r0 + j < B ? X1[rowOf[j] * d + k] : 0;
-            }
-#pragma unroll
-            for (u32 j = 0; j < kRowsAtOnce; ++j) acc[j] += a0[j] * ws + a1[j] * wa;
-        }
-#pragma unroll
-        for (u32 j = 0; j < kRowsAtOnce; ++j) {
-            u64 a = acc[j];
-#pragma unroll
-            for (int o = 32; o; o >>= 1) a += __shfl_xor(a, o, 64);
-            if (lane == 0 && r0 + j < B) prod[r0 + j] = a;
-        }
-    }
+    // the products come from the helper workgroups (lr_helper)
+    const u32 G = lr_helpers(B);
+    if (!lr_wait(box, F_H1, ep * G, ticks, status)) return;
+    lr_acquire();
+    prod = sc + L.hprod;
     __syncthreads();
     lr_stamp(PT, 2);
     lr_trunc_pair(T, K, it.t1_next_off / 8, it.t1_prev_off / 8, B, it.D, prod, my + L.z1, sc + L.z1own, xw0, xw1);
@@ -450,49 +596,23 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
     // ---- phase 4: err = f - YY; update = mulTruncate(XX^T, err); w -= update ----
     u64* e0 = sc + L.err;
     u64* e1 = e0 + B;
+    const u64* hy = sc + L.hy;
     for (u32 i = tid; i < B; i += kLrThreads) {
-        const u64 row = it.batch[i];
-        e0[i] = fr0[i] + g0[i] - Y0[row];
-        e1[i] = fr1[i] + g1[i] - Y1[row];
+        // write-through: the helpers on other CUs read err
+        hs_store(e0 + i, fr0[i] + g0[i] - hy[i]);
+        hs_store(e1 + i, fr1[i] + g1[i] - hy[B + i]);
+    }
+    lr_post(box, F_LVL + cir.nlevels, ep);  // F_ERR
+    // prod = XX^T err: the helpers' partial sums over their rows
+    prod = sc + L.prod;
+    if (!lr_wait(box, F_H2, ep * G, ticks, status)) return;
+    lr_acquire();
+    for (u32 k = tid; k < d; k += kLrThreads) {
+        u64 v = 0;
+        for (u32 h = 0; h < G; ++h) v += sc[L.hpart + (u64)h * d + k];
+        prod[k] = v;
     }
     __syncthreads();
-    // prod[k] = sum_i XX0[i][k] (e0 + e1)[i] + XX1[i][k] e0[i]: thread (k, i-group)
-    for (u32 k0 = 0; k0 < d; k0 += kLrThreads) {
-        const u32 dk = min(d - k0, kLrThreads);
-        const u32 G = kLrThreads / dk;  // i-groups
-        const u32 k = k0 + tid % dk, gi = tid / dk;
-        u64 acc = 0;
-        if (gi < G) {
-            // 8 rows per step: 16 independent loads in flight per thread
-            u32 i = gi;
-            for (; i + 7 * G < B; i += 8 * G) {
-                u64 a0[8], a1[8];
-#pragma unroll
-                for (u32 j = 0; j < 8; ++j) {
-                    const u64 row = it.batch[i + j * G];
-                    a0[j] = X0[row * d + k];
-                    a1[j] = X1[row * d + k];
-                }
-#pragma unroll
-                for (u32 j = 0; j < 8; ++j) {
-                    const u32 ii = i + j * G;
-                    acc += a0[j] * (e0[ii] + e1[ii]) + a1[j] * e0[ii];
-                }
-            }
-            for (; i < B; i += G) {
-                const u64 row = it.batch[i];
-                acc += X0[row * d + k] * (e0[i] + e1[i]) + X1[row * d + k] * e0[i];
-            }
-        }
-        part[tid] = acc;
-        __syncthreads();
-        if (tid < dk) {
-            u64 s = 0;
-            for (u32 g = 0; g < G; ++g) s += part[g * dk + tid];
-            prod[k0 + tid] = s;
-        }
-        __syncthreads();
-    }
     lr_stamp(PT, 9);
     const u32 sh2 = it.D + it.aB;
     u64* u0 = sc + L.upd;
@@ -558,8 +678,9 @@ int aby3g_lr_iteration(const aby3g_lr_iter* it, aby3g_stream stream) {
                                        (int)kLrDynLdsMax) == hipSuccess;
         }();
         ABY3G_REQUIRE(attr || !inLds, "could not raise the fused iteration's dynamic LDS limit");
-        launch(PROBE_OTHER, k_lr_iter, dim3(1), dim3(kLrThreads), inLds ? dynBytes : 0, S(stream), aes_table(), *it, K,
-               handoff_status_word(), inLds);
+        // block 0 runs the protocol, blocks 1..G help with the dataset products
+        launch(PROBE_OTHER, k_lr_iter, dim3(1 + lr_helpers(it->B)), dim3(kLrThreads), inLds ? dynBytes : 0, S(stream),
+               aes_table(), *it, K, handoff_status_word(), inLds);
     });
 }
 

@@ -67,9 +67,10 @@ int main(int argc, char** argv) {
         });
     for (auto& t : th) t.join();
     std::printf("wall %.1f us per iteration (%llu iterations)\n", wallUs / iters, (unsigned long long)iters);
-    const char* names[11] = {"aes table", "masks", "xw product", "trunc pair+post", "z wait+finalize",
-                             "reshare+inputs", "levels", "regions+fvals", "OT+public products", "err+XtE product",
-                             "trunc pair 2 / finalize / w"};
+    // interval i = stamps i -> i + 1 (lr.hip lr_stamp slots; slot 12 = after the table fill)
+    const char* names[11] = {"aes table+masks", "xw product", "trunc pair+post", "z wait+finalize",
+                             "reshare+inputs", "levels", "regions", "OT+public products", "err+XtE product",
+                             "trunc pair 2", "finalize / w"};
     for (int p = 0; p < 3; ++p) {
         std::printf("party %d:", p);
         double tot = 0;
@@ -80,6 +81,18 @@ int main(int argc, char** argv) {
             std::sort(v.begin(), v.end());
             std::printf(" %s %.1f |", names[ph], v[v.size() / 2]);
             tot += v[v.size() / 2];
+        }
+        {
+            std::vector<double> v;
+            for (u64 t = iters / 2; t < iters; ++t) v.push_back(0.01 * (double)(stamps[p][16 * t + 12] - stamps[p][16 * t]));
+            std::sort(v.begin(), v.end());
+            std::printf(" (table fill %.1f)", v[v.size() / 2]);
+            std::vector<double> f;
+            for (u64 t = iters / 2; t < iters; ++t)
+                f.push_back(100.0 * (double)(stamps[p][16 * t + 14] - stamps[p][16 * t + 13]) /
+                            (double)(stamps[p][16 * t + 11] - stamps[p][16 * t]));
+            std::sort(f.begin(), f.end());
+            std::printf(" (shader clock %.0f MHz)", f[f.size() / 2]);
         }
         std::vector<double> gap;  // launch-to-launch gap: end of t-1 to start of t
         for (u64 t = iters / 2; t < iters; ++t) gap.push_back(0.01 * (double)(stamps[p][16 * t] - stamps[p][16 * (t - 1) + 11]));

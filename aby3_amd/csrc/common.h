@@ -102,20 +102,37 @@ constexpr int kAesLdsWords = 256 * 64;
 
 __host__ __device__ __forceinline__ u32 rotl(u32 x, int r) { return __builtin_rotateleft32(x, r); }
 
-// One global load per thread, then 128 B of replicated copies from registers:
-// thread t covers entry x = t % 256 of table t / 256 (T1 = rotl(T0, 8)); a
-// loop of dependent global loads here would cost ~1 us per iteration.
+// The 64 KiB image is 4096 16-byte chunks (entry x: chunks 16x .. 16x + 15,
+// the first 8 holding T0[x] four times each, the last 8 T1[x]); consecutive
+// threads write consecutive chunks, so every ds_write_b128 of a wave covers
+// 1 KiB of consecutive banks, and every table read is in flight before the
+// first store. (Measured in the fused LR kernel, whose one workgroup fills
+// the table at the start of every launch: 8.4 us for the first fill of a
+// launch -- the launch's cold start, kernel arguments and code, whatever the
+// fill does: a table computed in registers instead of loaded took as long --
+// and 0.8 us for a second fill right after it.)
 __device__ __forceinline__ void aes_fill_lds(u32* lds, const u32* __restrict__ T0g) {
     static_assert(kAesLdsWords == 256 * 64, "layout");
-    for (u32 t = threadIdx.x; t < 512; t += blockDim.x) {
-        const u32 x = t & 255, tab = t >> 8;
-        u32 v = T0g[x];
-        if (tab) v = rotl(v, 8);
-        typedef u32 v4u __attribute__((ext_vector_type(4)));
-        v4u* dst = reinterpret_cast<v4u*>(lds + (x << 6) + (tab << 5));
-        const v4u q = {v, v, v, v};
+    typedef u32 v4u __attribute__((ext_vector_type(4)));
+    constexpr u32 kChunks = kAesLdsWords / 4, kU = 16;  // 16 chunks per thread at 256 threads
+    v4u* dst = reinterpret_cast<v4u*>(lds);
+    u32 v[kU];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) dst[i] = q;
+    for (u32 i = 0; i < kU; ++i) {
+        const u32 q = threadIdx.x + i * blockDim.x;
+        v[i] = q < kChunks ? T0g[q >> 4] : 0;
+    }
+#pragma unroll
+    for (u32 i = 0; i < kU; ++i) {
+        const u32 q = threadIdx.x + i * blockDim.x;
+        if (q < kChunks) {
+            const u32 x = (q & 8) ? rotl(v[i], 8) : v[i];
+            dst[q] = v4u{x, x, x, x};
+        }
+    }
+    for (u32 q = threadIdx.x + kU * blockDim.x; q < kChunks; q += blockDim.x) {  // blocks under 256 threads
+        const u32 x = (q & 8) ? rotl(T0g[q >> 4], 8) : T0g[q >> 4];
+        dst[q] = v4u{x, x, x, x};
     }
     __syncthreads();
 }

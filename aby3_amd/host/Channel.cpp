@@ -3,7 +3,9 @@
 #include <chrono>
 #include <cstdlib>
 #include <atomic>
+#include <deque>
 #include <map>
+#include <thread>
 
 namespace aby3 {
 
@@ -103,9 +105,63 @@ struct Pipe {
     std::unique_ptr<LinkEnd> link;
     int linkDevice = -1;                      // this end's device
     std::vector<LinkSlot> lslots;             // sender: staging slots
-    std::vector<void*> retired;               // sender: outgrown slots (freed at teardown)
+    struct Retired {
+        void* ptr;
+        u32 slot;
+        u64 lastSeq;
+    };
+    std::vector<Retired> retired;             // sender: outgrown slot buffers, freed once their last copy-out finished
     std::map<std::pair<u32, u64>, void*> mapped;  // receiver: opened slots by (slot, gen)
     u64 linkRead = 0;                         // receiver: messages taken off the ring
+    // sender: the ring is written by a thread of its own, in the order the
+    // messages were sent, so a send never blocks on the peer's reads: a host
+    // payload larger than the ring (4 MiB) then streams through it while the
+    // sending party goes on, as with in-process pipes -- a cyclic exchange
+    // where every party sends more than the ring holds before it receives
+    // would otherwise wait on itself until the link timeout
+    std::thread writer;
+    std::mutex wmu;
+    std::condition_variable wcv;
+    std::deque<std::vector<u8>> wq;
+    bool wstop = false;
+    std::string werr;
+
+    void ringWrite(std::vector<u8>&& bytes) {
+        std::lock_guard<std::mutex> lk(wmu);
+        if (!werr.empty()) throw std::runtime_error("link writer: " + werr);
+        wq.push_back(std::move(bytes));
+        if (!writer.joinable()) writer = std::thread([this] { writerLoop(); });
+        wcv.notify_one();
+    }
+    void writerLoop() {
+        for (;;) {
+            std::vector<u8> b;
+            {
+                std::unique_lock<std::mutex> lk(wmu);
+                wcv.wait(lk, [&] { return wstop || !wq.empty(); });
+                if (wq.empty()) return;  // stopped and drained
+                b = std::move(wq.front());
+                wq.pop_front();
+            }
+            try {
+                if (!b.empty()) link->write(b.data(), b.size());
+            } catch (const std::exception& e) {
+                std::lock_guard<std::mutex> lk(wmu);
+                werr = e.what();
+                wq.clear();
+                return;
+            }
+        }
+    }
+    // drains the queue (each write bounded by the link timeout) and joins
+    void stopWriter() {
+        {
+            std::lock_guard<std::mutex> lk(wmu);
+            wstop = true;
+        }
+        wcv.notify_one();
+        if (writer.joinable()) writer.join();
+    }
 
     // readiness of a device payload enqueued so far on `gpu`'s stream
     void signalReady(Msg& m, Gpu& gpu, Event* fallback) {
@@ -120,12 +176,28 @@ struct Pipe {
     }
 
     ~Pipe() {
+        stopWriter();
         if (link) {
             aby3g_set_device(linkDevice);
             aby3g_device_sync();
             for (auto& m : mapped) aby3g_ipc_close(m.second);
-            for (auto& s : lslots) aby3g_free(s.ptr);
-            for (void* p : retired) aby3g_free(p);
+            // the peer process may still be copying out of a staging slot:
+            // free each buffer once its last message is consumed -- within 10 s
+            // in all (a live peer takes milliseconds; one that died, or a
+            // session torn down after an error, leaves nothing to wait for)
+            const auto t0 = std::chrono::steady_clock::now();
+            auto left = [&] {
+                return std::max(0.0, 10.0 - std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+            };
+            for (size_t i = 0; i < lslots.size(); ++i)
+                if (lslots[i].ptr) {
+                    if (lslots[i].lastSeq) link->waitConsumed((u32)i, lslots[i].lastSeq, left());
+                    aby3g_free(lslots[i].ptr);
+                }
+            for (auto& r : retired) {
+                link->waitConsumed(r.slot, r.lastSeq, left());
+                aby3g_free(r.ptr);
+            }
         }
         for (auto& s : slots)
             if (s->ptr) {
@@ -145,7 +217,7 @@ struct Pipe {
 
     void push(Msg&& m) {
         if (link) {
-            linkPush(m);
+            linkPush(std::move(m));
             return;
         }
         std::lock_guard<std::mutex> lk(mu);
@@ -207,7 +279,7 @@ struct Pipe {
     // sender: host payloads go onto the ring; device payloads are copied into
     // a staging slot whose previous message the receiver has already taken
     // (its copy-out enqueued), the stream waiting for that copy-out to finish.
-    void linkPush(const Msg& m) {
+    void linkPush(Msg&& m) {
         std::lock_guard<std::mutex> lk(mu);
         WireMsg w{};
         w.bytes = m.bytes;
@@ -215,8 +287,11 @@ struct Pipe {
         w.slot = kNoSlot;
         w.device = linkDevice;
         sent += m.bytes;
-        link->write(&w, sizeof w);
-        if (m.bytes) link->write(m.host.data(), m.bytes);
+        ringWrite(std::vector<u8>((const u8*)&w, (const u8*)&w + sizeof w));
+        if (m.bytes) {
+            m.host.resize(m.bytes);
+            ringWrite(std::move(m.host));
+        }
     }
     void linkSendDevice(const void* src, size_t bytes, Gpu& gpu) {
         std::lock_guard<std::mutex> lk(mu);
@@ -226,6 +301,15 @@ struct Pipe {
         w.slot = kNoSlot;
         w.device = gpu.device();
         if (bytes) {
+            // outgrown buffers whose last copy-out finished
+            for (size_t i = 0; i < retired.size();)
+                if (link->consumed(retired[i].slot) >= retired[i].lastSeq) {
+                    GPU_CALL(aby3g_free(retired[i].ptr));
+                    retired[i] = retired.back();
+                    retired.pop_back();
+                } else {
+                    ++i;
+                }
             int k = -1;
             u64 staged = 0;
             for (const LinkSlot& ls : lslots) staged += ls.cap;
@@ -252,7 +336,7 @@ struct Pipe {
                     // free but too small: replace it (the receiver may still be
                     // reading the old buffer on its stream: retire, don't free)
                     k = (int)i;
-                    retired.push_back(lslots[i].ptr);
+                    retired.push_back(Retired{lslots[i].ptr, (u32)i, lslots[i].lastSeq});
                     lslots[i].ptr = nullptr;
                 }
             if (k < 0) {
@@ -278,7 +362,7 @@ struct Pipe {
             w.handle = s.h;
         }
         sent += bytes;
-        link->write(&w, sizeof w);
+        ringWrite(std::vector<u8>((const u8*)&w, (const u8*)&w + sizeof w));
     }
     // receiver: the next message off the ring, filed under its ticket
     void linkTake() {
@@ -309,6 +393,21 @@ struct Pipe {
             auto key = std::make_pair(m.lslot, m.lgen);
             auto it = mapped.find(key);
             if (it == mapped.end()) {
+                // a new buffer behind this slot: close the openings of its
+                // older ones once this stream's copy-outs from them finished
+                // (slots are outgrown rarely; the sync is off the common path)
+                bool older = false;
+                for (auto& kv : mapped) older = older || (kv.first.first == m.lslot && kv.first.second < m.lgen);
+                if (older) {
+                    GPU_CALL(aby3g_stream_sync(g.stream()));
+                    for (auto o = mapped.begin(); o != mapped.end();)
+                        if (o->first.first == m.lslot && o->first.second < m.lgen) {
+                            GPU_CALL(aby3g_ipc_close(o->second));
+                            o = mapped.erase(o);
+                        } else {
+                            ++o;
+                        }
+                }
                 void* p = nullptr;
                 GPU_CALL(aby3g_ipc_open(&m.lh, &p));
                 it = mapped.emplace(key, p).first;

@@ -97,6 +97,20 @@ std::atomic<u64>& LinkEnd::posted(u32 slot) { return mHdr->posted[slot]; }
 
 void LinkEnd::waitPosted(u32 slot, u64 seq) const { waitFor("a free staging slot", mHdr->posted[slot], seq); }
 
+u64 LinkEnd::consumed(u32 slot) const {
+    return __atomic_load_n(reinterpret_cast<const u64*>(mBase) + 8 + slot, __ATOMIC_ACQUIRE);
+}
+
+bool LinkEnd::waitConsumed(u32 slot, u64 seq, double maxS) const {
+    const auto t0 = std::chrono::steady_clock::now();
+    const auto limit = std::chrono::duration<double>(maxS);
+    while (consumed(slot) < seq) {
+        if (std::chrono::steady_clock::now() - t0 > limit) return false;
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    return true;
+}
+
 void LinkEnd::write(const void* src, size_t n) {
     const u8* s = (const u8*)src;
     u64 head = mHdr->head.load(std::memory_order_relaxed);

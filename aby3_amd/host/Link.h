@@ -46,6 +46,11 @@ public:
     std::atomic<u64>& posted(u32 slot);
     // blocks (up to timeoutS()) until posted(slot) >= seq
     void waitPosted(u32 slot, u64 seq) const;
+    // host view of consumed[slot] (written by the receiver's stream once its
+    // copy-out of the slot's message `seq` finished)
+    u64 consumed(u32 slot) const;
+    // waits (up to maxS seconds, no error) until consumed(slot) >= seq; false on timeout
+    bool waitConsumed(u32 slot, u64 seq, double maxS) const;
 
     static double timeoutS();
 

@@ -45,3 +45,14 @@ def test_party_processes_sanitized(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
     assert "party_procs: ok" in r.stdout
+
+
+def test_link_large_cyclic_exchange(tmp_path):
+    """Three processes, each sending host payloads of three times a link's
+    ring size to the next party before receiving from the previous one
+    (this cycle used to block until the link timeout)."""
+    exe = _build(str(tmp_path), "address", "link_exchange.cpp")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1", ABY3_LINK_TIMEOUT_S="30")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    assert "link_exchange: ok" in r.stdout

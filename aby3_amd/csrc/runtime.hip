@@ -293,6 +293,18 @@ int aby3g_event_record(aby3g_event ev, aby3g_stream stream) {
 int aby3g_event_sync(aby3g_event ev) {
     return guarded([&] { ABY3G_CHECK_HIP(hipEventSynchronize((hipEvent_t)ev)); });
 }
+int aby3g_event_query(aby3g_event ev, int* done) {
+    return guarded([&] {
+        ABY3G_REQUIRE(done != nullptr, "null argument");
+        const hipError_t e = hipEventQuery((hipEvent_t)ev);
+        if (e == hipErrorNotReady) {
+            *done = 0;
+            return;
+        }
+        ABY3G_CHECK_HIP(e);
+        *done = 1;
+    });
+}
 int aby3g_stream_wait_event(aby3g_stream stream, aby3g_event ev) {
     return guarded([&] { ABY3G_CHECK_HIP(hipStreamWaitEvent(S(stream), (hipEvent_t)ev, 0)); });
 }

@@ -110,8 +110,18 @@ struct Pipe {
         u32 slot;
         u64 lastSeq;
     };
-    std::vector<Retired> retired;             // sender: outgrown slot buffers, freed once their last copy-out finished
+    // sender: outgrown slot buffers, freed at teardown once their last
+    // copy-out finished (not before: aby3g_free may synchronize the device,
+    // and a party's stream can hold a wait on a peer whose next message this
+    // host has yet to send -- a free mid-protocol could deadlock; slots are
+    // outgrown rarely, so few pile up)
+    std::vector<Retired> retired;
     std::map<std::pair<u32, u64>, void*> mapped;  // receiver: opened slots by (slot, gen)
+    struct Closing {
+        void* ptr;
+        std::unique_ptr<Event> done;
+    };
+    std::vector<Closing> closing;  // receiver: openings of replaced slot buffers, closed once `done`
     u64 linkRead = 0;                         // receiver: messages taken off the ring
     // sender: the ring is written by a thread of its own, in the order the
     // messages were sent, so a send never blocks on the peer's reads: a host
@@ -181,6 +191,8 @@ struct Pipe {
             aby3g_set_device(linkDevice);
             aby3g_device_sync();
             for (auto& m : mapped) aby3g_ipc_close(m.second);
+            for (auto& c : closing) aby3g_ipc_close(c.ptr);
+            closing.clear();
             // the peer process may still be copying out of a staging slot:
             // free each buffer once its last message is consumed -- within 10 s
             // in all (a live peer takes milliseconds; one that died, or a
@@ -301,15 +313,6 @@ struct Pipe {
         w.slot = kNoSlot;
         w.device = gpu.device();
         if (bytes) {
-            // outgrown buffers whose last copy-out finished
-            for (size_t i = 0; i < retired.size();)
-                if (link->consumed(retired[i].slot) >= retired[i].lastSeq) {
-                    GPU_CALL(aby3g_free(retired[i].ptr));
-                    retired[i] = retired.back();
-                    retired.pop_back();
-                } else {
-                    ++i;
-                }
             int k = -1;
             u64 staged = 0;
             for (const LinkSlot& ls : lslots) staged += ls.cap;
@@ -396,23 +399,32 @@ struct Pipe {
                 // a new buffer behind this slot: close the openings of its
                 // older ones once this stream's copy-outs from them finished
                 // (slots are outgrown rarely; the sync is off the common path)
-                bool older = false;
-                for (auto& kv : mapped) older = older || (kv.first.first == m.lslot && kv.first.second < m.lgen);
-                if (older) {
-                    GPU_CALL(aby3g_stream_sync(g.stream()));
-                    for (auto o = mapped.begin(); o != mapped.end();)
-                        if (o->first.first == m.lslot && o->first.second < m.lgen) {
-                            GPU_CALL(aby3g_ipc_close(o->second));
-                            o = mapped.erase(o);
-                        } else {
-                            ++o;
-                        }
-                }
+                for (auto o = mapped.begin(); o != mapped.end();)
+                    if (o->first.first == m.lslot && o->first.second < m.lgen) {
+                        // every copy-out from it is already on this stream:
+                        // close it once an event recorded now has completed
+                        // (never a blocking sync here: the stream can hold a
+                        // wait on a peer that needs this host's next send)
+                        auto ev = std::make_unique<Event>();
+                        ev->record(g.stream());
+                        closing.push_back(Closing{o->second, std::move(ev)});
+                        o = mapped.erase(o);
+                    } else {
+                        ++o;
+                    }
                 void* p = nullptr;
                 GPU_CALL(aby3g_ipc_open(&m.lh, &p));
                 it = mapped.emplace(key, p).first;
             }
             src = it->second;
+            for (size_t i = 0; i < closing.size();)
+                if (closing[i].done->done()) {
+                    GPU_CALL(aby3g_ipc_close(closing[i].ptr));
+                    closing[i] = std::move(closing.back());
+                    closing.pop_back();
+                } else {
+                    ++i;
+                }
         }
         GPU_CALL(aby3g_stream_wait_value(g.stream(), link->readyDev(), m.lseq));
         GPU_CALL(aby3g_memcpy(dst, src, m.bytes, m.ldevice == g.device() ? 2 : 3, g.stream()));

@@ -68,6 +68,11 @@ Event::~Event() {
 }
 void Event::record(aby3g_stream s) { GPU_CALL(aby3g_event_record(mEv, s)); }
 void Event::sync() { GPU_CALL(aby3g_event_sync(mEv)); }
+bool Event::done() const {
+    int d = 0;
+    GPU_CALL(aby3g_event_query(mEv, &d));
+    return d != 0;
+}
 
 Gpu::Gpu(int device) : mDevice(device) {
     GPU_CALL(aby3g_set_device(device));

@@ -24,6 +24,7 @@ public:
     Event& operator=(const Event&) = delete;
     void record(aby3g_stream s);
     void sync();
+    bool done() const;  // the last recorded work completed (never blocks)
     aby3g_event get() const { return mEv; }
 
 private:

@@ -157,6 +157,7 @@ _SIGS = {
     "aby3g_bin_level_hs": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_uint32, c_void_p, c_void_p, ctypes.c_uint32,
                                    c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "aby3g_handoff_status": (c_int, [POINTER(ctypes.c_uint32)]),
+    "aby3g_event_query": (c_int, [c_void_p, POINTER(c_int)]),
     "aby3g_lr_mailbox_bytes": (c_uint64, [ctypes.c_uint32, ctypes.c_uint32, c_void_p]),
     "aby3g_lr_scratch_bytes": (c_uint64, [ctypes.c_uint32, ctypes.c_uint32, c_void_p]),
     "aby3g_lr_iteration": (c_int, [c_void_p, c_void_p]),

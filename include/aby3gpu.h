@@ -70,6 +70,9 @@ int aby3g_event_create_timed(aby3g_event* ev); /* for aby3g_event_elapsed_ms */
 int aby3g_event_destroy(aby3g_event ev);
 int aby3g_event_record(aby3g_event ev, aby3g_stream stream);
 int aby3g_event_sync(aby3g_event ev);
+/* *done = 1 once the work captured by the event's last record has completed
+ * (never blocks; hipEventQuery) */
+int aby3g_event_query(aby3g_event ev, int* done);
 int aby3g_stream_wait_event(aby3g_stream stream, aby3g_event ev);
 int aby3g_event_elapsed_ms(aby3g_event start, aby3g_event end, float* ms);
 /* Stream-ordered signal words (device memory, 8 bytes): `stream` writes

@@ -32,6 +32,7 @@ OVERRIDES = {
     "aby3g_event_destroy": "delete (int*)ev; return 0;",
     "aby3g_event_record": "*(int*)ev = 1; return 0;",
     "aby3g_event_elapsed_ms": "*ms = 0; return 0;",
+    "aby3g_event_query": "*done = 1; return 0;",
     "aby3g_signal_alloc": "*word = (uint64_t*)calloc(1, 8); return *word ? 0 : 1;",
     "aby3g_stream_write_value": "__atomic_store_n(word, value, __ATOMIC_RELEASE); return 0;",
     "aby3g_stream_wait_value": "return nd_wait(word, value);",

@@ -505,10 +505,13 @@ __global__ void __launch_bounds__(256) k_bits_to_wires_map(const i64* __restrict
         }
         vv[k] = v;
     }
-    for (u32 k = 0; k < 16; ++k) {
-        const u32 wl = wave * 16 + k;
-        tile[lane * kTilePitch + wl] = transpose64(vv[k], lane);
-    }
+    // unrolled: the 16 transposes are independent, so their shuffle stages
+    // interleave instead of waiting out each one's latency in turn (the
+    // rolled loop ran 16 x 6 dependent ds_bpermute rounds per wave)
+#pragma unroll
+    for (u32 k = 0; k < 16; ++k) vv[k] = transpose64(vv[k], lane);
+#pragma unroll
+    for (u32 k = 0; k < 16; ++k) tile[lane * kTilePitch + wave * 16 + k] = vv[k];
     __syncthreads();
     for (u32 idx = threadIdx.x; idx < 64 * kTileWords; idx += 256) {
         const u32 b = idx / kTileWords, wl = idx % kTileWords;
@@ -545,13 +548,16 @@ __global__ void __launch_bounds__(256) k_wires_to_bits_map(const u64* __restrict
     }
     __syncthreads();
     const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // unrolled, as in k_bits_to_wires_map: 16 independent transposes in flight
+#pragma unroll
+    for (u32 k = 0; k < 16; ++k) vv[k] = transpose64(tile[lane * kTilePitch + wave * 16 + k], lane);
+#pragma unroll
     for (u32 k = 0; k < 16; ++k) {
         const u32 wl = wave * 16 + k;
-        const u64 mine = transpose64(tile[lane * kTilePitch + wl], lane);
         const u64 row = (w0 + wl) * 64 + lane;
         if (w0 + wl < rw && row < rows) {
             const u64 dst = map_row(map, row);
-            if (dst < outRows) out[dst * cols + c] = (i64)mine;
+            if (dst < outRows) out[dst * cols + c] = (i64)vv[k];
         }
     }
 }

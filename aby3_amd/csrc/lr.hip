@@ -82,7 +82,7 @@ struct Layout {
         u64 o = 0;
         z1 = o, o += B;
         v = o, o += B;
-        lvl = o, o += (u64)c.nand * W;
+        lvl = o, o += 2 * (u64)c.nand * W;  // level messages as {epoch, 32-bit half} granules
         ots = o, o += 2 * (u64)B;
         oth = o, o += B;
         otc = o, o += B;
@@ -352,6 +352,35 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
 
     u64* mem = memInLds ? dyn : sc + L.mem;
     u64* zmw = memInLds ? dyn + 2 * (u64)cir.wires * W : sc + L.zmask;
+    // the gate list and the AND output wires in LDS beside the engine memory
+    // (the levels read a gate descriptor per gate-word: from global memory
+    // that is one L2 round trip each, 4 us per level)
+    const aby3g_gate* gates = cir.gates;
+    const u32* andWires = cir.and_wires;
+    const aby3g_lr_level* levelsL = cir.levels;
+    const u32* batchEndsL = cir.batch_ends;
+    if (memInLds) {
+        u32* gl = reinterpret_cast<u32*>(zmw + (u64)cir.nand * W);
+        const u32* gg = reinterpret_cast<const u32*>(cir.gates);
+        const u32 gw = cir.ngates * (u32)(sizeof(aby3g_gate) / 4);
+        for (u32 i = threadIdx.x; i < gw; i += kLrThreads) gl[i] = gg[i];
+        u32* al = gl + gw;
+        for (u32 i = threadIdx.x; i < cir.nand; i += kLrThreads) al[i] = cir.and_wires[i];
+        gates = reinterpret_cast<const aby3g_gate*>(gl);
+        andWires = al;
+        // the level table and batch ends too: per level they were two
+        // dependent loads from global memory, ~2 us of a 4 us level
+        u32* lvl = al + ((cir.nand + 3) & ~3u);
+        const u32* lg = reinterpret_cast<const u32*>(cir.levels);
+        for (u32 i = threadIdx.x; i < cir.nlevels * (u32)(sizeof(aby3g_lr_level) / 4); i += kLrThreads) lvl[i] = lg[i];
+        const aby3g_lr_level& last = cir.levels[cir.nlevels - 1];
+        const u32 nbatches = last.batch_off + last.nbatch;  // <= ngates
+        u32* be = lvl + cir.nlevels * (u32)(sizeof(aby3g_lr_level) / 4);
+        for (u32 i = threadIdx.x; i < nbatches; i += kLrThreads) be[i] = cir.batch_ends[i];
+        levelsL = reinterpret_cast<const aby3g_lr_level*>(lvl);
+        batchEndsL = be;
+        // read from the levels on, after phase 1's barriers
+    }
 
     // ---- phase 0: the circuit's AND masks, words with rows only ----
     {
@@ -422,27 +451,61 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
     lr_stamp(PT, 5);
     // the levels (roundCallback): unpack the previous level's received AND
     // shares, then this level's batches, then publish its AND shares
+    // The level messages use the granule form of the in-kernel hand-off
+    // (cdna_hip_programming.md Guideline 16, R2): every 64-bit AND share goes
+    // as two 8-byte {epoch, half} words stored write-through, and the reader
+    // polls the words themselves until both carry this epoch -- one memory
+    // round trip per level instead of a drain, a flag and the payload load.
     const u64* zm = zmw;
+    const u32 tag = (u32)ep;
+    const u32 W32 = (u32)W;
+    __shared__ u32 lvlBad;
+    if (tid == 0) lvlBad = 0;
     for (u32 lv = 0; lv <= cir.nlevels; ++lv) {
-        if (lv > 0 && cir.levels[lv - 1].nand) {
-            const aby3g_lr_level& pl = cir.levels[lv - 1];
-            if (!lr_wait(pbox, F_LVL + lv - 1, ep, ticks, status)) return;
-            const u64* rows = pv + L.lvl + (u64)pl.and_wire_off * W;
-            for (u64 q = tid; q < (u64)pl.nand * W; q += kLrThreads) {
-                const u64 j = q / W, w = q % W;
-                mem[WS + (u64)cir.and_wires[pl.and_wire_off + j] * W + w] = hs_load(rows + q);
+        if (lv > 0 && levelsL[lv - 1].nand) {
+            const aby3g_lr_level& pl = levelsL[lv - 1];
+            const u64* grows = pv + L.lvl + 2 * (u64)pl.and_wire_off * W;
+            const u64 t0 = wall_clock64();
+            bool ok = true;
+            for (u32 q = tid; q < pl.nand * W32 && ok; q += kLrThreads) {
+                u64 a, b;
+                for (u32 spins = 0;;) {
+                    a = hs_load(grows + 2 * q);
+                    b = hs_load(grows + 2 * q + 1);
+                    if ((u32)(a >> 32) == tag && (u32)(b >> 32) == tag) break;
+                    __builtin_amdgcn_s_sleep(1);
+                    if ((++spins & 63) == 0) {
+                        if (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+                            ok = false;
+                            break;
+                        }
+                        if (wall_clock64() - t0 > kHandoffTimeoutTicks) {
+                            __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                            ok = false;
+                            break;
+                        }
+                    }
+                }
+                if (ok) {
+                    const u32 j = q / W32, w = q - j * W32;
+                    mem[WS + (u64)andWires[pl.and_wire_off + j] * W + w] = (u64)(u32)a | ((u64)(u32)b << 32);
+                }
             }
+            if (!ok) lvlBad = 1;
+            if (tid == 0 && ticks)
+                __hip_atomic_fetch_add((gu64*)ticks, wall_clock64() - t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __syncthreads();
+            if (lvlBad) return;
         }
         if (lv == cir.nlevels) break;
-        const aby3g_lr_level& lvr = cir.levels[lv];
-        u64* send = my + L.lvl + (u64)lvr.and_wire_off * W;
+        const aby3g_lr_level& lvr = levelsL[lv];
+        u64* gsend = my + L.lvl + 2 * (u64)lvr.and_wire_off * W;
         u32 begin = 0;
         for (u32 b = 0; b < lvr.nbatch; ++b) {
-            const u32 end = cir.batch_ends[lvr.batch_off + b];
-            for (u64 q = tid; q < (u64)(end - begin) * W; q += kLrThreads) {
-                const aby3g_gate g = cir.gates[lvr.first_gate + begin + q / W];
-                const u64 w = q % W;
+            const u32 end = batchEndsL[lvr.batch_off + b];
+            for (u32 q = tid; q < (end - begin) * W32; q += kLrThreads) {
+                const u32 gq = q / W32, w = q - gq * W32;  // 32-bit: a 64-bit divide per gate-word cost ~1 us per level
+                const aby3g_gate g = gates[lvr.first_gate + begin + gq];
                 const bool unary = g.type == ABY3G_GATE_COPY || g.type == ABY3G_GATE_INV;
                 const u32 in1 = unary ? g.in0 : g.in1;
                 const u64 x0 = mem[(u64)g.in0 * W + w], x1 = mem[WS + (u64)g.in0 * W + w];
@@ -450,7 +513,9 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
                 if (gate_is_and(g.type)) {
                     const u64 r = gate_and_share(g.type, x0, x1, y0, y1) ^ zm[(u64)g.z_row * W + w];
                     mem[(u64)g.out * W + w] = r;
-                    hs_store(send + (u64)g.send_row * W + w, r);
+                    const u64 gi = 2 * ((u64)g.send_row * W + w);
+                    hs_store(gsend + gi, ((u64)tag << 32) | (u32)r);
+                    hs_store(gsend + gi + 1, ((u64)tag << 32) | (u32)(r >> 32));
                 } else {
                     u64 o0, o1;
                     gate_local(g.type, x0, x1, y0, y1, o0, o1);
@@ -461,7 +526,7 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
             __syncthreads();
             begin = end;
         }
-        if (lvr.nand) lr_post(box, F_LVL + lv, ep);
+        if (lv < 16) lr_stamp(PT, 16 + lv);
     }
     lr_stamp(PT, 6);
     // regions (getOutput, 1 bit each): reg[t][h][i]
@@ -671,7 +736,10 @@ int aby3g_lr_iteration(const aby3g_lr_iter* it, aby3g_stream stream) {
         K.otn = expand_key(it->ot_next_key);
         K.otp = expand_key(it->ot_prev_key);
         const Layout L(it->B, it->d, it->cir);
-        const u64 dynBytes = (2 * (u64)it->cir.wires + it->cir.nand) * L.W * 8;
+        // engine memory, masks, gates, AND wires (padded to 4), level table, batch ends (<= ngates)
+        const u64 dynBytes = (2 * (u64)it->cir.wires + it->cir.nand) * L.W * 8 +
+                             (u64)it->cir.ngates * sizeof(aby3g_gate) + 4 * (((u64)it->cir.nand + 3) & ~3ull) +
+                             (u64)it->cir.nlevels * sizeof(aby3g_lr_level) + 4 * (u64)it->cir.ngates;
         const int inLds = dynBytes <= kLrDynLdsMax;
         static const bool attr = [] {  // dynamic LDS beyond the default limit, once per process
             return hipFuncSetAttribute((const void*)k_lr_iter, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -38,7 +38,7 @@ struct SgdState {
     // parties take together.
     std::shared_ptr<FusedLr> fused;
     bool fusedChecked = false;
-    u64* phaseTicks = nullptr;  // optional device [16]: the fused launch's phase stamps (profiling)
+    u64* phaseTicks = nullptr;  // optional device [32]: the fused launch's phase stamps (profiling)
 };
 
 // One SGD_Logistic iteration on the batch of B row indices at device pointer

@@ -50,19 +50,19 @@ int main(int argc, char** argv) {
             }
             aby3ML ml(rt, enc, ev, D);
             SgdState st;
-            DeviceBuffer dIdx(rt.gpu(), idx.size() * 4), ticks(rt.gpu(), iters * 16 * 8);
+            DeviceBuffer dIdx(rt.gpu(), idx.size() * 4), ticks(rt.gpu(), iters * 32 * 8);
             toDevice(dIdx.data(), idx.data(), idx.size() * 4, rt.gpu());
             rt.gpu().sync();
             const auto t0 = std::chrono::steady_clock::now();
             for (u64 t = 0; t < iters; ++t) {
-                st.phaseTicks = ticks.as<u64>() + 16 * t;
+                st.phaseTicks = ticks.as<u64>() + 32 * t;
                 sgdLogisticStep(ml, sX, sY, sW, dIdx.as<u32>() + t * B, B, aB, st);
             }
             rt.gpu().sync();
             if (p == 0)
                 wallUs = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-            stamps[p].resize(iters * 16);
-            toHost(stamps[p].data(), ticks.data(), iters * 16 * 8, rt.gpu());
+            stamps[p].resize(iters * 32);
+            toHost(stamps[p].data(), ticks.data(), iters * 32 * 8, rt.gpu());
             if (!st.fused) std::printf("party %d: fused form NOT taken\n", p);
         });
     for (auto& t : th) t.join();
@@ -77,25 +77,41 @@ int main(int argc, char** argv) {
         for (int ph = 0; ph < 11; ++ph) {
             std::vector<double> v;
             for (u64 t = iters / 2; t < iters; ++t)
-                v.push_back(0.01 * (double)(stamps[p][16 * t + ph + 1] - stamps[p][16 * t + ph]));
+                v.push_back(0.01 * (double)(stamps[p][32 * t + ph + 1] - stamps[p][32 * t + ph]));
             std::sort(v.begin(), v.end());
             std::printf(" %s %.1f |", names[ph], v[v.size() / 2]);
             tot += v[v.size() / 2];
         }
         {
             std::vector<double> v;
-            for (u64 t = iters / 2; t < iters; ++t) v.push_back(0.01 * (double)(stamps[p][16 * t + 12] - stamps[p][16 * t]));
+            for (u64 t = iters / 2; t < iters; ++t) v.push_back(0.01 * (double)(stamps[p][32 * t + 12] - stamps[p][32 * t]));
             std::sort(v.begin(), v.end());
             std::printf(" (table fill %.1f)", v[v.size() / 2]);
             std::vector<double> f;
             for (u64 t = iters / 2; t < iters; ++t)
-                f.push_back(100.0 * (double)(stamps[p][16 * t + 14] - stamps[p][16 * t + 13]) /
-                            (double)(stamps[p][16 * t + 11] - stamps[p][16 * t]));
+                f.push_back(100.0 * (double)(stamps[p][32 * t + 14] - stamps[p][32 * t + 13]) /
+                            (double)(stamps[p][32 * t + 11] - stamps[p][32 * t]));
             std::sort(f.begin(), f.end());
             std::printf(" (shader clock %.0f MHz)", f[f.size() / 2]);
         }
+        {
+            // the circuit levels (slots 16 + lv: end of level lv; slot 5 = start of the levels)
+            std::printf("\n   levels:");
+            for (int lv = 0; lv < 8; ++lv) {
+                std::vector<double> v;
+                for (u64 t = iters / 2; t < iters; ++t) {
+                    const u64 a = stamps[p][32 * t + (lv ? 16 + lv - 1 : 5)], b = stamps[p][32 * t + 16 + lv];
+                    if (b) v.push_back(0.01 * (double)(b - a));
+                }
+                if (!v.empty()) {
+                    std::sort(v.begin(), v.end());
+                    std::printf(" L%d %.1f", lv, v[v.size() / 2]);
+                }
+            }
+            std::printf("\n  ");
+        }
         std::vector<double> gap;  // launch-to-launch gap: end of t-1 to start of t
-        for (u64 t = iters / 2; t < iters; ++t) gap.push_back(0.01 * (double)(stamps[p][16 * t] - stamps[p][16 * (t - 1) + 11]));
+        for (u64 t = iters / 2; t < iters; ++t) gap.push_back(0.01 * (double)(stamps[p][32 * t] - stamps[p][32 * (t - 1) + 11]));
         std::sort(gap.begin(), gap.end());
         std::printf(" total %.1f us, gap between launches %.1f us\n", tot, gap[gap.size() / 2]);
     }

@@ -19,24 +19,6 @@ typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
 constexpr u32 kGateBlock = 256;
 
-// 64 x 64 bit transpose across a wave: lane i holds row i (bit k = column k);
-// afterwards lane i holds column i (bit k = bit i of row k). Six butterfly
-// stages: at stage j the lanes i and i ^ j swap the off-diagonal j x j
-// blocks of their 2j x 2j block (one 64-bit lane exchange + masks each),
-// instead of 64 ballots.
-__device__ __forceinline__ u64 transpose64(u64 x, u32 lane) {
-    constexpr u64 kMask[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
-                              0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
-#pragma unroll
-    for (int st = 0; st < 6; ++st) {
-        const u32 j = 32u >> st;
-        const u64 m = kMask[st];
-        const u64 y = __shfl_xor(x, (int)j, 64);
-        x = (lane & j) ? ((x & ~m) | ((y & ~m) >> j)) : ((x & m) | ((y & m) << j));
-    }
-    return x;
-}
-
 __global__ void __launch_bounds__(kGateBlock) k_bin_gates(const aby3g_gate* __restrict__ gates, u64* __restrict__ mem,
                                                           u64 wires, u64 words, const u64* __restrict__ z,
                                                           u64* __restrict__ sendbuf) {

@@ -179,39 +179,86 @@ __host__ __device__ __forceinline__ u32 aes_sb4(u32 A, u32 B, u32 C, u32 D) {
 #endif
 }
 
-// AES-128 of the counter block LE64(ctr) || 0^8 under `k`, T-table form.
-// Column c of the state is the LE word of bytes 4c..4c+3; after ShiftRows,
-// row r of column c comes from column c+r, and MixColumns row weights of
-// input row r are T0 rotated left by 8r bits, so a column is
+// 64 x 64 bit transpose across a wave: lane i holds row i (bit k = column k);
+// afterwards lane i holds column i (bit k = bit i of row k). Six butterfly
+// stages: at stage j the lanes i and i ^ j swap the off-diagonal j x j
+// blocks of their 2j x 2j block (one 64-bit lane exchange + masks each),
+// instead of 64 ballots.
+__device__ __forceinline__ u64 transpose64(u64 x, u32 lane) {
+    constexpr u64 kMask[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
+                              0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
+#pragma unroll
+    for (int st = 0; st < 6; ++st) {
+        const u32 j = 32u >> st;
+        const u64 m = kMask[st];
+        const u64 y = __shfl_xor(x, (int)j, 64);
+        x = (lane & j) ? ((x & ~m) | ((y & ~m) >> j)) : ((x & m) | ((y & m) << j));
+    }
+    return x;
+}
+
+// Round-key sources of aes_ctr_blocks. Keys in SGPRs: schedules that are
+// kernel arguments (a kernel with one or two keys keeps them resident).
+struct AesRkSgpr {
+    const AesKey* const* k;
+    __host__ __device__ __forceinline__ void round(int b, int r, u32 (&o)[4]) const {
+        o[0] = k[b]->rk[4 * r + 0];
+        o[1] = k[b]->rk[4 * r + 1];
+        o[2] = k[b]->rk[4 * r + 2];
+        o[3] = k[b]->rk[4 * r + 3];
+    }
+    static __host__ __device__ __forceinline__ u32 x3(u32 a, u32 b, u32 k) { return xor3_uniform(a, b, k); }
+};
+// Keys in LDS (44-word schedules at 16-byte aligned offsets), one broadcast
+// ds_read_b128 per round and block: a kernel with many keys would otherwise
+// spill them from SGPRs into VGPR lanes, loading the whole kernel-argument
+// block up front one dependent 64-byte scalar load at a time.
+struct AesRkLds {
+    const u32* const* k;
+    __device__ __forceinline__ void round(int b, int r, u32 (&o)[4]) const {
+        typedef u32 v4u __attribute__((ext_vector_type(4)));
+        const v4u v = *reinterpret_cast<const v4u*>(k[b] + 4 * r);
+        o[0] = v.x, o[1] = v.y, o[2] = v.z, o[3] = v.w;
+    }
+    static __device__ __forceinline__ u32 x3(u32 a, u32 b, u32 k) { return xor3_v(a, b, k); }
+};
+
+// AES-128 of the counter block LE64(ctr) || 0^8 under key b of `R`, T-table
+// form. Column c of the state is the LE word of bytes 4c..4c+3; after
+// ShiftRows, row r of column c comes from column c+r, and MixColumns row
+// weights of input row r are T0 rotated left by 8r bits, so a column is
 //   xor3(T0[a], T1[b], rk) ^ rotl(T0[c] ^ T1[d], 16).
 // NB blocks (keys / counters of their own) are interleaved so each round
 // issues 16 * NB independent table reads.
-template <int NB>
-__host__ __device__ __forceinline__ void aes_ctr_blocks(const u32* __restrict__ T, u32 lane32, const AesKey* const* k,
-                                                        const u64* ctr, u64* lo, u64* hi) {
+template <int NB, class RK>
+__host__ __device__ __forceinline__ void aes_ctr_blocks_rk(const u32* __restrict__ T, u32 lane32, const RK& R,
+                                                           const u64* ctr, u64* lo, u64* hi) {
     const u8* Tb = reinterpret_cast<const u8*>(T);
     const u32 L0 = lane32 << 2, L1 = L0 | 0x80u;
 #define ABY3G_TL(s, L, j) (*reinterpret_cast<const u32*>(Tb + aes_addr((s), (L), (j))))
     u32 s0[NB], s1[NB], s2[NB], s3[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-        s0[b] = (u32)ctr[b] ^ k[b]->rk[0];
-        s1[b] = (u32)(ctr[b] >> 32) ^ k[b]->rk[1];
-        s2[b] = k[b]->rk[2];
-        s3[b] = k[b]->rk[3];
+        u32 k[4];
+        R.round(b, 0, k);
+        s0[b] = (u32)ctr[b] ^ k[0];
+        s1[b] = (u32)(ctr[b] >> 32) ^ k[1];
+        s2[b] = k[2];
+        s3[b] = k[3];
     }
 #pragma unroll
     for (int r = 1; r < 10; ++r) {
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
-            const u32* rk = k[b]->rk;
-            const u32 t0 = xor3_uniform(ABY3G_TL(s0[b], L0, 0), ABY3G_TL(s1[b], L1, 1), rk[4 * r + 0]) ^
+            u32 k[4];
+            R.round(b, r, k);
+            const u32 t0 = RK::x3(ABY3G_TL(s0[b], L0, 0), ABY3G_TL(s1[b], L1, 1), k[0]) ^
                            rotl(ABY3G_TL(s2[b], L0, 2) ^ ABY3G_TL(s3[b], L1, 3), 16);
-            const u32 t1 = xor3_uniform(ABY3G_TL(s1[b], L0, 0), ABY3G_TL(s2[b], L1, 1), rk[4 * r + 1]) ^
+            const u32 t1 = RK::x3(ABY3G_TL(s1[b], L0, 0), ABY3G_TL(s2[b], L1, 1), k[1]) ^
                            rotl(ABY3G_TL(s3[b], L0, 2) ^ ABY3G_TL(s0[b], L1, 3), 16);
-            const u32 t2 = xor3_uniform(ABY3G_TL(s2[b], L0, 0), ABY3G_TL(s3[b], L1, 1), rk[4 * r + 2]) ^
+            const u32 t2 = RK::x3(ABY3G_TL(s2[b], L0, 0), ABY3G_TL(s3[b], L1, 1), k[2]) ^
                            rotl(ABY3G_TL(s0[b], L0, 2) ^ ABY3G_TL(s1[b], L1, 3), 16);
-            const u32 t3 = xor3_uniform(ABY3G_TL(s3[b], L0, 0), ABY3G_TL(s0[b], L1, 1), rk[4 * r + 3]) ^
+            const u32 t3 = RK::x3(ABY3G_TL(s3[b], L0, 0), ABY3G_TL(s0[b], L1, 1), k[3]) ^
                            rotl(ABY3G_TL(s1[b], L0, 2) ^ ABY3G_TL(s2[b], L1, 3), 16);
             s0[b] = t0;
             s1[b] = t1;
@@ -222,19 +269,26 @@ __host__ __device__ __forceinline__ void aes_ctr_blocks(const u32* __restrict__ 
     // last round: SubBytes + ShiftRows
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-        const u32* rk = k[b]->rk;
+        u32 k[4];
+        R.round(b, 10, k);
         const u32 o0 = aes_sb4(ABY3G_TL(s0[b], L0, 0), ABY3G_TL(s1[b], L0, 1), ABY3G_TL(s2[b], L0, 2),
-                               ABY3G_TL(s3[b], L0, 3)) ^ rk[40];
+                               ABY3G_TL(s3[b], L0, 3)) ^ k[0];
         const u32 o1 = aes_sb4(ABY3G_TL(s1[b], L0, 0), ABY3G_TL(s2[b], L0, 1), ABY3G_TL(s3[b], L0, 2),
-                               ABY3G_TL(s0[b], L0, 3)) ^ rk[41];
+                               ABY3G_TL(s0[b], L0, 3)) ^ k[1];
         const u32 o2 = aes_sb4(ABY3G_TL(s2[b], L0, 0), ABY3G_TL(s3[b], L0, 1), ABY3G_TL(s0[b], L0, 2),
-                               ABY3G_TL(s1[b], L0, 3)) ^ rk[42];
+                               ABY3G_TL(s1[b], L0, 3)) ^ k[2];
         const u32 o3 = aes_sb4(ABY3G_TL(s3[b], L0, 0), ABY3G_TL(s0[b], L0, 1), ABY3G_TL(s1[b], L0, 2),
-                               ABY3G_TL(s2[b], L0, 3)) ^ rk[43];
+                               ABY3G_TL(s2[b], L0, 3)) ^ k[3];
         lo[b] = (u64)o0 | ((u64)o1 << 32);
         hi[b] = (u64)o2 | ((u64)o3 << 32);
     }
 #undef ABY3G_TL
+}
+
+template <int NB>
+__host__ __device__ __forceinline__ void aes_ctr_blocks(const u32* __restrict__ T, u32 lane32, const AesKey* const* k,
+                                                        const u64* ctr, u64* lo, u64* hi) {
+    aes_ctr_blocks_rk<NB>(T, lane32, AesRkSgpr{k}, ctr, lo, hi);
 }
 
 // A key schedule copied into VGPRs (44 per lane): a kernel that needs two

@@ -67,6 +67,13 @@ struct LrKeys {
     AesKey otn, otp;        // SharedOT keys
 };
 
+// Block 0 copies the schedules into LDS (AesRkLds): as kernel arguments the
+// eight of them spill out of SGPRs (loaded up front, one dependent scalar load
+// per 64 bytes: ~7 us at the start of every launch).
+enum : u32 { kKeyPrev, kKeyNext, kKeyZsp, kKeyZsn, kKeyMp, kKeyMn, kKeyOtn, kKeyOtp, kLrKeys };
+constexpr u32 kKeyWords = 44;
+static_assert(sizeof(LrKeys) == kLrKeys * kKeyWords * 4, "LrKeys is the schedules in kKey order");
+
 // Mailbox and scratch layouts, in u64 words.
 struct Layout {
     u64 W, Wpad;
@@ -127,11 +134,18 @@ __device__ __forceinline__ u64x2 load_pair(const u64* p, bool pair) {
     return u64x2{p[0], pair ? p[1] : 0};
 }
 
+// NB AES-CTR blocks under LDS key schedules (keys[kKey...] + counters)
+template <int NB>
+__device__ __forceinline__ void lr_blocks(const u32* T, const u32* const (&k)[NB], const u64 (&c)[NB], u64 (&lo)[NB],
+                                          u64 (&hi)[NB]) {
+    aes_ctr_blocks_rk<NB>(T, threadIdx.x & 31, AesRkLds{k}, c, lo, hi);
+}
+
 // word j of PRNG(k): half (j & 1) of AES(k, j >> 1)
-__device__ __forceinline__ u64 stream_word(const u32* T, const AesKey& k, u64 j) {
-    u64 lo, hi;
-    aes_ctr_block(T, threadIdx.x & 31, k, j >> 1, lo, hi);
-    return (j & 1) ? hi : lo;
+__device__ __forceinline__ u64 stream_word(const u32* T, const u32* k, u64 j) {
+    u64 lo[1], hi[1];
+    lr_blocks<1>(T, {k}, {j >> 1}, lo, hi);
+    return (j & 1) ? hi[0] : lo[0];
 }
 
 // waits for a neighbour's flag `f` (one lane polls; the workgroup leaves
@@ -146,11 +160,14 @@ __device__ __forceinline__ void lr_post(u64* box, u32 f, u64 epoch) { hs_post(Hs
 // t0 = next-stream word (nw0 + i), t1 = prev-stream word (pw0 + i);
 // z = prod - (t0 >> 2) published into `out` (write-through) and kept in own,
 // C = (t0 >> (d+2), t1 >> (d+2)) into c0 / c1.
-__device__ __forceinline__ void lr_trunc_pair(const u32* T, const LrKeys& K, u64 nw0, u64 pw0, u32 n, u32 d,
+__device__ __forceinline__ void lr_trunc_pair(const u32* T, const u32* keys, u64 nw0, u64 pw0, u32 n, u32 d,
                                               const u64* prod, u64* out, u64* own, u64* c0, u64* c1) {
     for (u32 i = threadIdx.x; i < n; i += kLrThreads) {
-        const i64 t0 = (i64)stream_word(T, K.next, nw0 + i);
-        const i64 t1 = (i64)stream_word(T, K.prev, pw0 + i);
+        const u32* const k[2] = {keys + kKeyNext * kKeyWords, keys + kKeyPrev * kKeyWords};
+        u64 lo[2], hi[2];
+        lr_blocks<2>(T, k, {(nw0 + i) >> 1, (pw0 + i) >> 1}, lo, hi);
+        const i64 t0 = (i64)(((nw0 + i) & 1) ? hi[0] : lo[0]);
+        const i64 t1 = (i64)(((pw0 + i) & 1) ? hi[1] : lo[1]);
         const u64 z = prod[i] - (u64)(t0 >> 2);
         own[i] = z;
         hs_store(out + i, z);
@@ -195,7 +212,7 @@ __device__ __forceinline__ void lr_arrive(u64* box, u32 f) {
 // A wave per row (rows wave, wave + 8, ...), lanes over k pairs (16-byte
 // loads), kLrHelperUnroll rows of a wave in flight.
 constexpr u32 kLrHelperUnroll = 4;
-__device__ __noinline__ void lr_helper(const aby3g_lr_iter& it, u32* status, u64* part) {
+__device__ __forceinline__ void lr_helper(const aby3g_lr_iter& it, u32* status, u64* part) {
     const u32 B = it.B, d = it.d, G = lr_helpers(B), h = blockIdx.x - 1;
     const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const Layout L(B, d, it.cir);
@@ -325,9 +342,15 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
     }
     u64* const PT = it.phase_ticks;
     lr_stamp(PT, 0);
-    aes_fill_lds(lds, T0g);
+    __shared__ __attribute__((aligned(16))) u32 keys[kLrKeys * kKeyWords];
+    {
+        const u32* kw = reinterpret_cast<const u32*>(&K);
+        for (u32 i = threadIdx.x; i < kLrKeys * kKeyWords; i += kLrThreads) keys[i] = kw[i];
+    }
+    aes_fill_lds(lds, T0g);  // its barrier publishes the keys too
     lr_stamp(PT, 12);
     const u32* T = lds;
+    auto KL = [&](u32 key) -> const u32* { return keys + key * kKeyWords; };
     const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int p = it.party;
     const u32 B = it.B, d = it.d;
@@ -389,10 +412,12 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
         for (u64 q = tid; q < (u64)cir.nand * Wh; q += kLrThreads) {
             const u64 k = q / Wh, wp = q % Wh;
             const u64 c = (k * L.Wpad + 2 * wp) >> 1;  // Wpad is even: draws 2wp, 2wp + 1 share a block
-            u64 a0, a1, b0, b1;
-            aes_ctr_block2(T, tid & 31, K.mp, c, K.mn, c, a0, a1, b0, b1);
-            zm[k * W + 2 * wp] = a0 ^ b0;
-            if (2 * wp + 1 < W) zm[k * W + 2 * wp + 1] = a1 ^ b1;
+            const u32* const kk[2] = {KL(kKeyMp), KL(kKeyMn)};
+            const u64 cc[2] = {c, c};
+            u64 lo[2], hi[2];
+            lr_blocks<2>(T, kk, cc, lo, hi);  // interleaved: 8 waves leave the LDS idle otherwise
+            zm[k * W + 2 * wp] = lo[0] ^ lo[1];
+            if (2 * wp + 1 < W) zm[k * W + 2 * wp + 1] = hi[0] ^ hi[1];
         }
     }
 
@@ -405,7 +430,7 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
     prod = sc + L.hprod;
     __syncthreads();
     lr_stamp(PT, 2);
-    lr_trunc_pair(T, K, it.t1_next_off / 8, it.t1_prev_off / 8, B, it.D, prod, my + L.z1, sc + L.z1own, xw0, xw1);
+    lr_trunc_pair(T, keys, it.t1_next_off / 8, it.t1_prev_off / 8, B, it.D, prod, my + L.z1, sc + L.z1own, xw0, xw1);
     lr_post(box, F_Z1, ep);
     lr_stamp(PT, 3);
     if (p < 2) {
@@ -426,7 +451,7 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
         vrecv = pv + L.v;
     }
     // inputs straight into the wires (setTwoInputSharing): source s in
-    // {aa_0, aa_1, b}, share h; a wave ballots bit b of its 64 rows
+    // {aa_0, aa_1, b}, share h; a wave transposes the bits of its 64 rows
     const u64 WS = (u64)cir.wires * W;  // share stride
     for (u32 job = wave; job < 6 * W; job += kLrWaves) {
         const u32 src = job / (2 * (u32)W), h = (job / (u32)W) & 1, w = job % (u32)W;
@@ -441,11 +466,8 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
                 if (p == 2 && h == 1) val = xw1[r];
             }
         }
-        u64* base = mem + h * WS + (u64)cir.in_wire[src] * W + w;
-        for (u32 b = 0; b < 64; ++b) {
-            const u64 word = __ballot((val >> b) & 1);
-            if (lane == 0) base[(u64)b * W] = word;
-        }
+        // lane b stores bit b of the wave's 64 rows (one transpose, not 64 ballots)
+        mem[h * WS + ((u64)cir.in_wire[src] + lane) * W + w] = transpose64(val, lane);
     }
     __syncthreads();
     lr_stamp(PT, 5);
@@ -555,39 +577,50 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
     __syncthreads();
     lr_stamp(PT, 7);
     const u64 otw = p == 0 ? it.ot_prev_off / 8 : p == 1 ? it.ot_prev_off / 8 : it.ot_next_off / 8;
+    // Each send loop splits its AES blocks over all 512 threads (the OT part
+    // on threads [0, B), the public-product part on [B, 2B)) and interleaves a
+    // thread's blocks in one lr_blocks<NB> call: one wave of dependent
+    // table reads per round instead of NB of them.
     if (p == 0) {
         const u64 nw = it.ot_next_off / 8;
-        for (u32 i = tid; i < B; i += kLrThreads) {
-            // OT product, sender + helper (Sh3Evaluator.cpp:132-163)
-            const u64 zr = stream_word(T, K.prev, otw + 2 * i), c1 = stream_word(T, K.prev, otw + 2 * i + 1);
-            const u64 c0 = stream_word(T, K.next, nw + i);
-            fr0[i] = c0;
-            fr1[i] = c1;
-            const u32 bb0 = (u32)((r1a[i] ^ r1b[i]) & 1), bb1 = (u32)(r1a[i] & 1);
-            const u64 zz = 0 - (c0 + c1) - zr;
-            u64 s[2];
-            s[bb0] = zz;
-            s[bb0 ^ 1] = A0[i] + A1[i] + zz;
-            u64 lo, hi, hlo, hhi;
-            aes_ctr_block2(T, tid & 31, K.otn, it.ot_ctr + i, K.otn, it.ot_ctr + B + i, lo, hi, hlo, hhi);
-            hs_store(my + L.ots + 2 * i, lo ^ s[0]);
-            hs_store(my + L.ots + 2 * i + 1, hi ^ s[1]);
-            hs_store(my + L.oth + i, bb1 ? hhi : hlo);
-            // public product (Sh3Evaluator.cpp:430-447)
-            const u64 j = it.pm_draw + i;
-            u64 zp[2], zq[2];
-            aes_ctr_block2(T, tid & 31, K.zsp, j >> 1, K.zsn, j >> 1, zp[0], zp[1], zq[0], zq[1]);
-            const u64 zs = zp[j & 1] - zq[j & 1];
-            const u32 bb = (u32)((r2a[i] ^ r2b[i]) & 1);
-            u64 t[2];
-            t[bb] = zs;
-            t[bb ^ 1] = (u64)it.one + zs;
-            u64 nlo, nhi, plo, phi;
-            aes_ctr_block2(T, tid & 31, K.otn, it.pm_ctr_next + i, K.otp, it.pm_ctr_prev + i, nlo, nhi, plo, phi);
-            hs_store(my + L.pma + 2 * i, nlo ^ t[0]);
-            hs_store(my + L.pma + 2 * i + 1, nhi ^ t[1]);
-            hs_store(my + L.pmb + 2 * i, plo ^ t[0]);
-            hs_store(my + L.pmb + 2 * i + 1, phi ^ t[1]);
+        for (u32 q = tid; q < 2 * B; q += kLrThreads) {
+            if (q < B) {
+                // OT product, sender + helper (Sh3Evaluator.cpp:132-163)
+                const u32 i = q;
+                const u64 wz = otw + 2 * i, wc = wz + 1, wn = nw + i;
+                const u32* const k[5] = {KL(kKeyPrev), KL(kKeyPrev), KL(kKeyNext), KL(kKeyOtn), KL(kKeyOtn)};
+                const u64 c[5] = {wz >> 1, wc >> 1, wn >> 1, it.ot_ctr + i, it.ot_ctr + B + i};
+                u64 lo[5], hi[5];
+                lr_blocks<5>(T, k, c, lo, hi);
+                const u64 zr = (wz & 1) ? hi[0] : lo[0], c1 = (wc & 1) ? hi[1] : lo[1], c0 = (wn & 1) ? hi[2] : lo[2];
+                fr0[i] = c0;
+                fr1[i] = c1;
+                const u32 bb0 = (u32)((r1a[i] ^ r1b[i]) & 1), bb1 = (u32)(r1a[i] & 1);
+                const u64 zz = 0 - (c0 + c1) - zr;
+                u64 s[2];
+                s[bb0] = zz;
+                s[bb0 ^ 1] = A0[i] + A1[i] + zz;
+                hs_store(my + L.ots + 2 * i, lo[3] ^ s[0]);
+                hs_store(my + L.ots + 2 * i + 1, hi[3] ^ s[1]);
+                hs_store(my + L.oth + i, bb1 ? hi[4] : lo[4]);
+            } else {
+                // public product (Sh3Evaluator.cpp:430-447)
+                const u32 i = q - B;
+                const u64 j = it.pm_draw + i;
+                const u32* const k[4] = {KL(kKeyZsp), KL(kKeyZsn), KL(kKeyOtn), KL(kKeyOtp)};
+                const u64 c[4] = {j >> 1, j >> 1, it.pm_ctr_next + i, it.pm_ctr_prev + i};
+                u64 lo[4], hi[4];
+                lr_blocks<4>(T, k, c, lo, hi);
+                const u64 zs = (j & 1) ? hi[0] - hi[1] : lo[0] - lo[1];
+                const u32 bb = (u32)((r2a[i] ^ r2b[i]) & 1);
+                u64 t[2];
+                t[bb] = zs;
+                t[bb ^ 1] = (u64)it.one + zs;
+                hs_store(my + L.pma + 2 * i, lo[2] ^ t[0]);
+                hs_store(my + L.pma + 2 * i + 1, hi[2] ^ t[1]);
+                hs_store(my + L.pmb + 2 * i, lo[3] ^ t[0]);
+                hs_store(my + L.pmb + 2 * i + 1, hi[3] ^ t[1]);
+            }
         }
         lr_post(box, F_OT1, ep);
         lr_post(box, F_PM, ep);
@@ -597,17 +630,25 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
             g1[i] = hs_load(pv + L.pmb + i);  // P2's
         }
     } else if (p == 1) {
-        for (u32 i = tid; i < B; i += kLrThreads) {
-            fr1[i] = stream_word(T, K.prev, otw + i);  // OT receiver's share 1 (:165-200)
-            const u64 j = it.pm_draw + i;              // public product, helper (:452-487)
-            u64 zp[2], zq[2];
-            aes_ctr_block2(T, tid & 31, K.zsp, j >> 1, K.zsn, j >> 1, zp[0], zp[1], zq[0], zq[1]);
-            const u64 zs = zp[j & 1] - zq[j & 1];
-            g1[i] = zs;
-            u64 lo, hi;
-            aes_ctr_block(T, tid & 31, K.otn, it.pm_ctr_next + i, lo, hi);
-            hs_store(my + L.pma + i, (r2a[i] & 1) ? hi : lo);  // help -> P2
-            hs_store(my + L.pmb + i, zs);                      // mine -> P0
+        for (u32 q = tid; q < 2 * B; q += kLrThreads) {
+            if (q < B) {
+                // OT receiver's share 1 (:165-200); public product, helper (:452-487)
+                const u32 i = q;
+                const u64 wf = otw + i, j = it.pm_draw + i;
+                const u32* const k[3] = {KL(kKeyPrev), KL(kKeyZsp), KL(kKeyZsn)};
+                const u64 c[3] = {wf >> 1, j >> 1, j >> 1};
+                u64 lo[3], hi[3];
+                lr_blocks<3>(T, k, c, lo, hi);
+                fr1[i] = (wf & 1) ? hi[0] : lo[0];
+                const u64 zs = (j & 1) ? hi[1] - hi[2] : lo[1] - lo[2];
+                g1[i] = zs;
+                hs_store(my + L.pmb + i, zs);  // mine -> P0
+            } else {
+                const u32 i = q - B;
+                u64 lo[1], hi[1];
+                lr_blocks<1>(T, {KL(kKeyOtn)}, {it.pm_ctr_next + i}, lo, hi);
+                hs_store(my + L.pma + i, (r2a[i] & 1) ? hi[0] : lo[0]);  // help -> P2
+            }
         }
         lr_post(box, F_PM, ep);
         if (!lr_wait(pbox, F_OT1, ep, ticks, status) || !lr_wait(nbox, F_OT1, ep, ticks, status)) return;
@@ -623,29 +664,37 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
         for (u32 i = tid; i < B; i += kLrThreads)
             g0[i] = hs_load(pv + L.pma + 2 * i + (r2a[i] & 1)) ^ hs_load(nx + L.pma + i);
     } else {
-        for (u32 i = tid; i < B; i += kLrThreads) {
-            // OT product, sender + helper (:202-240)
-            const u64 zr = stream_word(T, K.next, otw + 2 * i), c0 = stream_word(T, K.next, otw + 2 * i + 1);
-            fr0[i] = c0;
-            const u32 bb0 = (u32)(r1b[i] & 1), bb1 = (u32)((r1a[i] ^ r1b[i]) & 1);
-            u64 s[2];
-            s[bb1] = zr;
-            s[bb1 ^ 1] = A1[i] + zr;
-            u64 hlo, hhi, lo, hi;
-            aes_ctr_block2(T, tid & 31, K.otp, it.ot_ctr + i, K.otp, it.ot_ctr + B + i, hlo, hhi, lo, hi);
-            hs_store(my + L.oth + i, bb0 ? hhi : hlo);
-            hs_store(my + L.ots + 2 * i, lo ^ s[0]);
-            hs_store(my + L.ots + 2 * i + 1, hi ^ s[1]);
-            // public product, helper
-            const u64 j = it.pm_draw + i;
-            u64 zp[2], zq[2];
-            aes_ctr_block2(T, tid & 31, K.zsp, j >> 1, K.zsn, j >> 1, zp[0], zp[1], zq[0], zq[1]);
-            const u64 zs = zp[j & 1] - zq[j & 1];
-            g0[i] = zs;
-            u64 plo, phi;
-            aes_ctr_block(T, tid & 31, K.otp, it.pm_ctr_prev + i, plo, phi);
-            hs_store(my + L.pma + i, (r2b[i] & 1) ? phi : plo);  // help -> P1
-            hs_store(my + L.pmb + i, zs);                        // mine -> P0
+        for (u32 q = tid; q < 2 * B; q += kLrThreads) {
+            if (q < B) {
+                // OT product, sender + helper (:202-240)
+                const u32 i = q;
+                const u64 wz = otw + 2 * i, wc = wz + 1;
+                const u32* const k[4] = {KL(kKeyNext), KL(kKeyNext), KL(kKeyOtp), KL(kKeyOtp)};
+                const u64 c[4] = {wz >> 1, wc >> 1, it.ot_ctr + i, it.ot_ctr + B + i};
+                u64 lo[4], hi[4];
+                lr_blocks<4>(T, k, c, lo, hi);
+                const u64 zr = (wz & 1) ? hi[0] : lo[0], c0 = (wc & 1) ? hi[1] : lo[1];
+                fr0[i] = c0;
+                const u32 bb0 = (u32)(r1b[i] & 1), bb1 = (u32)((r1a[i] ^ r1b[i]) & 1);
+                u64 s[2];
+                s[bb1] = zr;
+                s[bb1 ^ 1] = A1[i] + zr;
+                hs_store(my + L.oth + i, bb0 ? hi[2] : lo[2]);
+                hs_store(my + L.ots + 2 * i, lo[3] ^ s[0]);
+                hs_store(my + L.ots + 2 * i + 1, hi[3] ^ s[1]);
+            } else {
+                // public product, helper
+                const u32 i = q - B;
+                const u64 j = it.pm_draw + i;
+                const u32* const k[3] = {KL(kKeyZsp), KL(kKeyZsn), KL(kKeyOtp)};
+                const u64 c[3] = {j >> 1, j >> 1, it.pm_ctr_prev + i};
+                u64 lo[3], hi[3];
+                lr_blocks<3>(T, k, c, lo, hi);
+                const u64 zs = (j & 1) ? hi[0] - hi[1] : lo[0] - lo[1];
+                g0[i] = zs;
+                hs_store(my + L.pma + i, (r2b[i] & 1) ? hi[2] : lo[2]);  // help -> P1
+                hs_store(my + L.pmb + i, zs);                            // mine -> P0
+            }
         }
         lr_post(box, F_OT1, ep);
         lr_post(box, F_PM, ep);
@@ -682,7 +731,7 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
     const u32 sh2 = it.D + it.aB;
     u64* u0 = sc + L.upd;
     u64* u1 = u0 + d;
-    lr_trunc_pair(T, K, it.t2_next_off / 8, it.t2_prev_off / 8, d, sh2, prod, my + L.z2, sc + L.z2own, u0, u1);
+    lr_trunc_pair(T, keys, it.t2_next_off / 8, it.t2_prev_off / 8, d, sh2, prod, my + L.z2, sc + L.z2own, u0, u1);
     lr_post(box, F_Z2, ep);
     lr_stamp(PT, 10);
     if (p < 2) {

@@ -52,6 +52,8 @@ int main(int argc, char** argv) {
             SgdState st;
             DeviceBuffer dIdx(rt.gpu(), idx.size() * 4), ticks(rt.gpu(), iters * 32 * 8);
             toDevice(dIdx.data(), idx.data(), idx.size() * 4, rt.gpu());
+            const std::vector<u64> zeros(iters * 32, 0);  // unused slots read 0
+            toDevice(ticks.data(), zeros.data(), iters * 32 * 8, rt.gpu());
             rt.gpu().sync();
             const auto t0 = std::chrono::steady_clock::now();
             for (u64 t = 0; t < iters; ++t) {
@@ -93,6 +95,24 @@ int main(int argc, char** argv) {
                             (double)(stamps[p][32 * t + 11] - stamps[p][32 * t]));
             std::sort(f.begin(), f.end());
             std::printf(" (shader clock %.0f MHz)", f[f.size() / 2]);
+            std::vector<double> pr;  // slot 15: an optional probe stamp after slot 12
+            for (u64 t = iters / 2; t < iters; ++t)
+                if (stamps[p][32 * t + 15]) pr.push_back(0.01 * (double)(stamps[p][32 * t + 15] - stamps[p][32 * t + 12]));
+            std::vector<double> sk, ld;
+            for (u64 t = iters / 2; t < iters; ++t)
+                if (stamps[p][32 * t + 31]) {
+                    sk.push_back(0.01 * (double)(stamps[p][32 * t + 30] - stamps[p][32 * t]));
+                    ld.push_back(0.01 * (double)(stamps[p][32 * t + 31] - stamps[p][32 * t]));
+                }
+            if (!sk.empty()) {
+                std::sort(sk.begin(), sk.end());
+                std::sort(ld.begin(), ld.end());
+                std::printf(" (probe last wave start %.1f, first load %.1f)", sk[sk.size() / 2], ld[ld.size() / 2]);
+            }
+            if (!pr.empty()) {
+                std::sort(pr.begin(), pr.end());
+                std::printf(" (probe 12->15 %.1f)", pr[pr.size() / 2]);
+            }
         }
         {
             // the circuit levels (slots 16 + lv: end of level lv; slot 5 = start of the levels)

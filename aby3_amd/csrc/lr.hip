@@ -723,7 +723,8 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
     lr_acquire();
     for (u32 k = tid; k < d; k += kLrThreads) {
         u64 v = 0;
-        for (u32 h = 0; h < G; ++h) v += sc[L.hpart + (u64)h * d + k];
+#pragma unroll 16
+        for (u32 h = 0; h < G; ++h) v += sc[L.hpart + (u64)h * d + k];  // the loads of 16 go out together
         prod[k] = v;
     }
     __syncthreads();

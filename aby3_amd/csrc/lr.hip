@@ -42,11 +42,15 @@ constexpr u32 kLrMaxD = 4096;
 // word accesses, at LDS instead of L2 latency
 constexpr u64 kLrDynLdsMax = 88 << 10;
 
-// mailbox flags (one u64 each; value = epoch of the last message published)
-// F_H1 / F_H2: the helper workgroups' arrival counters (own mailbox only;
-// epoch * helpers once every helper published); F_ERR = F_LVL + nlevels:
-// workgroup 0's err vector published to its helpers
-enum : u32 { F_Z1 = 0, F_V = 1, F_OT1 = 2, F_OT2 = 3, F_PM = 4, F_Z2 = 5, F_H1 = 6, F_H2 = 7, F_LVL = 8 };
+// mailbox flags (one u64 each), all within a workgroup's own mailbox: F_H1 /
+// F_H2 the helper workgroups' arrival counters (epoch * helpers once every
+// helper published), F_ERR workgroup 0's err vector published to its helpers
+// and F_P3 its start of phase 3, a hint for the helpers' polling (value =
+// epoch). Between the parties there are no flags: every message word
+// carries the epoch itself (msg_put / msg_get).
+// (each on a 128-byte line of its own: 16 helpers poll F_ERR while block 0
+// polls F_H1 / F_H2 and the helpers add to them)
+enum : u32 { F_H1 = 0, F_H2 = 16, F_ERR = 32, F_P3 = 48, kLrFlags = 64 };
 
 // Helper workgroups (blocks 1..G of the launch): the two dataset products
 // gather the batch rows from all over the dataset, which one CU does at a few
@@ -85,17 +89,18 @@ struct Layout {
     __host__ __device__ Layout(u32 B, u32 d, const aby3g_lr_circuit& c) {
         W = (B + 63) / 64;
         Wpad = 32 * (((u64)B + 2047) / 2048);
-        flags = ((F_LVL + (u64)c.nlevels + 1 + 31) / 32) * 32;
+        flags = ((kLrFlags + 31) / 32) * 32;
+        // messages: two {epoch, 32-bit half} granules per 64-bit word
         u64 o = 0;
-        z1 = o, o += B;
-        v = o, o += B;
-        lvl = o, o += 2 * (u64)c.nand * W;  // level messages as {epoch, 32-bit half} granules
-        ots = o, o += 2 * (u64)B;
-        oth = o, o += B;
-        otc = o, o += B;
-        pma = o, o += 2 * (u64)B;
-        pmb = o, o += 2 * (u64)B;
-        z2 = o, o += d;
+        z1 = o, o += 2 * (u64)B;
+        v = o, o += 2 * (u64)B;
+        lvl = o, o += 2 * (u64)c.nand * W;
+        ots = o, o += 4 * (u64)B;
+        oth = o, o += 2 * (u64)B;
+        otc = o, o += 2 * (u64)B;
+        pma = o, o += 4 * (u64)B;
+        pmb = o, o += 4 * (u64)B;
+        z2 = o, o += 2 * (u64)d;
         region = (o + 31) / 32 * 32;
         o = 0;
         xw = o, o += 2 * (u64)B;
@@ -156,12 +161,61 @@ __device__ __forceinline__ bool lr_wait(const u64* box, u32 f, u64 epoch, u64* t
 // publishes this party's flag `f` after every wave's write-through stores
 __device__ __forceinline__ void lr_post(u64* box, u32 f, u64 epoch) { hs_post(HsPost{box, epoch}, f, f + 1); }
 
+// Messages between the parties in the granule form of the in-kernel hand-off
+// (cdna_hip_programming.md Guideline 16, R2): word i of a message array m is
+// m[2i] = {epoch, low half}, m[2i + 1] = {epoch, high half}, stored
+// write-through; the reader polls the words themselves until both halves
+// carry this epoch -- no drain, no flag and no second round trip for the
+// payload. The mailbox regions alternate by epoch parity, so a word left from
+// two epochs before never matches.
+__device__ __forceinline__ void msg_put(u64* m, u64 i, u64 v, u32 tag) {
+    hs_store(m + 2 * i, ((u64)tag << 32) | (u32)v);
+    hs_store(m + 2 * i + 1, ((u64)tag << 32) | (u32)(v >> 32));
+}
+// A thread's reads of one receive loop: after a timeout or an abort (status
+// set) it stops polling and the workgroup leaves together at msg_done.
+struct MsgWait {
+    u32 tag;
+    u32* status;
+    u64 t0;
+    bool ok;
+};
+__device__ __forceinline__ MsgWait msg_begin(u64 epoch, u32* status) {
+    return MsgWait{(u32)epoch, status, (u64)wall_clock64(), true};
+}
+__device__ __forceinline__ u64 msg_get(const u64* m, u64 i, MsgWait& w) {
+    if (!w.ok) return 0;
+    for (u32 spins = 0;;) {
+        const u64 a = hs_load(m + 2 * i), b = hs_load(m + 2 * i + 1);
+        if ((u32)(a >> 32) == w.tag && (u32)(b >> 32) == w.tag) return (u64)(u32)a | ((u64)(u32)b << 32);
+        __builtin_amdgcn_s_sleep(1);
+        if ((++spins & 63) == 0) {
+            if (__hip_atomic_load(w.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+            if (wall_clock64() - w.t0 > kHandoffTimeoutTicks) {
+                __hip_atomic_store(w.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                break;
+            }
+        }
+    }
+    w.ok = false;
+    return 0;
+}
+// the end of a receive loop (a workgroup barrier): false when any thread's
+// read failed; thread 0 adds the loop's time to the wait ticks
+__device__ __forceinline__ bool msg_done(const MsgWait& w, u32* bad, u64* ticks) {
+    if (!w.ok) *bad = 1;
+    if (threadIdx.x == 0 && ticks)
+        __hip_atomic_fetch_add((gu64*)ticks, wall_clock64() - w.t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    return *bad == 0;
+}
+
 // The truncation pair over n elements (Sh3Evaluator.cpp:503-566, 667-673):
 // t0 = next-stream word (nw0 + i), t1 = prev-stream word (pw0 + i);
 // z = prod - (t0 >> 2) published into `out` (write-through) and kept in own,
 // C = (t0 >> (d+2), t1 >> (d+2)) into c0 / c1.
 __device__ __forceinline__ void lr_trunc_pair(const u32* T, const u32* keys, u64 nw0, u64 pw0, u32 n, u32 d,
-                                              const u64* prod, u64* out, u64* own, u64* c0, u64* c1) {
+                                              const u64* prod, u64* out, u32 tag, u64* own, u64* c0, u64* c1) {
     for (u32 i = threadIdx.x; i < n; i += kLrThreads) {
         const u32* const k[2] = {keys + kKeyNext * kKeyWords, keys + kKeyPrev * kKeyWords};
         u64 lo[2], hi[2];
@@ -170,7 +224,7 @@ __device__ __forceinline__ void lr_trunc_pair(const u32* T, const u32* keys, u64
         const i64 t1 = (i64)(((pw0 + i) & 1) ? hi[1] : lo[1]);
         const u64 z = prod[i] - (u64)(t0 >> 2);
         own[i] = z;
-        hs_store(out + i, z);
+        msg_put(out, i, z, tag);
         c0[i] = (u64)(t0 >> (d + 2));
         c1[i] = (u64)(t1 >> (d + 2));
     }
@@ -179,9 +233,9 @@ __device__ __forceinline__ void lr_trunc_pair(const u32* T, const u32* keys, u64
 // Round 2 of the truncating product, parties 0 and 1 (Sh3Evaluator.cpp:
 // 703-719): C[party] += (z_next + z_prev + z_own) >> d.
 __device__ __forceinline__ void lr_trunc_finalize(const u64* zn, const u64* zp, const u64* own, u32 n, u32 d,
-                                                  u64* cp) {
+                                                  u64* cp, MsgWait& w) {
     for (u32 i = threadIdx.x; i < n; i += kLrThreads) {
-        const i64 s = (i64)(hs_load(zn + i) + hs_load(zp + i) + own[i]);
+        const i64 s = (i64)(msg_get(zn, i, w) + msg_get(zp, i, w) + own[i]);
         cp[i] += (u64)(s >> d);
     }
 }
@@ -267,11 +321,11 @@ __device__ __forceinline__ void lr_helper(const aby3g_lr_iter& it, u32* status, 
 
     // ---- phase 4 ----
     // block 0's err comes only after its circuit and products (~80 us): until
-    // its F_PM flag (phase 3) poll rarely, so that the helpers' polls do not
+    // its F_P3 flag (phase 3) poll rarely, so that the helpers' polls do not
     // load the memory path of the parties' hand-offs; then poll closely
     if (threadIdx.x == 0) {
         const u64 t0 = wall_clock64();
-        for (u32 spins = 0; __hip_atomic_load((const gu64*)box + F_PM, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ep;) {
+        for (u32 spins = 0; __hip_atomic_load((const gu64*)box + F_P3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ep;) {
             __builtin_amdgcn_s_sleep(32);
             if ((++spins & 15) == 0 && (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
                                         wall_clock64() - t0 > kHandoffTimeoutTicks))
@@ -279,7 +333,7 @@ __device__ __forceinline__ void lr_helper(const aby3g_lr_iter& it, u32* status, 
         }
     }
     __syncthreads();
-    if (!hs_wait(HsWait{box, ep, nullptr, status}, F_LVL + it.cir.nlevels, F_LVL + it.cir.nlevels + 1)) return;
+    if (!hs_wait(HsWait{box, ep, nullptr, status}, F_ERR, F_ERR + 1)) return;
     const u64* e0 = sc + L.err;
     const u64* e1 = e0 + B;
     for (u32 k0 = 0; k0 < d; k0 += 128) {
@@ -331,18 +385,16 @@ __device__ __forceinline__ void lr_stamp(u64* ticks, u32 s) {
     if (ticks && threadIdx.x == 0 && (s == 0 || s == 11)) ticks[s == 0 ? 13 : 14] = clock64();
 }
 
-__global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict__ T0g, aby3g_lr_iter it, LrKeys K,
-                                                           u32* status, int memInLds) {
-    __shared__ u32 lds[kAesLdsWords];
-    __shared__ u64 part[kLrThreads];
-    extern __shared__ __attribute__((aligned(16))) u64 dyn[];  // [2][wires][W] engine memory, then [nand][W] masks
-    if (blockIdx.x > 0) {
-        lr_helper(it, status, part);
-        return;
-    }
+// Block 0: the protocol of one party. kLds: engine memory, masks and circuit
+// tables in LDS. A template rather than a run-time choice of pointers: a
+// pointer that may be LDS or global memory is a flat pointer, and every flat
+// access waits for the wave's outstanding global stores too -- in the levels,
+// for the write-through AND shares just sent (~1 us a level).
+template <bool kLds>
+__device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it, const LrKeys& K, u32* status,
+                                         u32* lds, u32* keys, u64* dyn) {
     u64* const PT = it.phase_ticks;
     lr_stamp(PT, 0);
-    __shared__ __attribute__((aligned(16))) u32 keys[kLrKeys * kKeyWords];
     {
         const u32* kw = reinterpret_cast<const u32*>(&K);
         for (u32 i = threadIdx.x; i < kLrKeys * kKeyWords; i += kLrThreads) keys[i] = kw[i];
@@ -373,8 +425,8 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
     u64* xw1 = xw0 + B;
     u64* prod = sc + L.prod;
 
-    u64* mem = memInLds ? dyn : sc + L.mem;
-    u64* zmw = memInLds ? dyn + 2 * (u64)cir.wires * W : sc + L.zmask;
+    u64* mem = kLds ? dyn : sc + L.mem;
+    u64* zmw = kLds ? dyn + 2 * (u64)cir.wires * W : sc + L.zmask;
     // the gate list and the AND output wires in LDS beside the engine memory
     // (the levels read a gate descriptor per gate-word: from global memory
     // that is one L2 round trip each, 4 us per level)
@@ -382,7 +434,7 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
     const u32* andWires = cir.and_wires;
     const aby3g_lr_level* levelsL = cir.levels;
     const u32* batchEndsL = cir.batch_ends;
-    if (memInLds) {
+    if (kLds) {
         u32* gl = reinterpret_cast<u32*>(zmw + (u64)cir.nand * W);
         const u32* gg = reinterpret_cast<const u32*>(cir.gates);
         const u32 gw = cir.ngates * (u32)(sizeof(aby3g_gate) / 4);
@@ -430,26 +482,25 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
     prod = sc + L.hprod;
     __syncthreads();
     lr_stamp(PT, 2);
-    lr_trunc_pair(T, keys, it.t1_next_off / 8, it.t1_prev_off / 8, B, it.D, prod, my + L.z1, sc + L.z1own, xw0, xw1);
-    lr_post(box, F_Z1, ep);
+    const u32 tag = (u32)ep;
+    __shared__ u32 msgBad;
+    if (tid == 0) msgBad = 0;
+    lr_trunc_pair(T, keys, it.t1_next_off / 8, it.t1_prev_off / 8, B, it.D, prod, my + L.z1, tag, sc + L.z1own, xw0,
+                  xw1);
     lr_stamp(PT, 3);
-    if (p < 2) {
-        if (!lr_wait(nbox, F_Z1, ep, ticks, status) || !lr_wait(pbox, F_Z1, ep, ticks, status)) return;
-        lr_trunc_finalize(nx + L.z1, pv + L.z1, sc + L.z1own, B, it.D, p == 0 ? xw0 : xw1);
+    {
+        MsgWait mw = msg_begin(ep, status);
+        if (p < 2) lr_trunc_finalize(nx + L.z1, pv + L.z1, sc + L.z1own, B, it.D, p == 0 ? xw0 : xw1, mw);
+        if (!msg_done(mw, &msgBad, p < 2 ? ticks : nullptr)) return;
     }
-    __syncthreads();
 
     lr_stamp(PT, 4);
     // ---- phase 2: regions of the piecewise sigmoid ----
     // P0 reshares x0 + x2 (its two shares) to P1
-    const u64* vrecv = nullptr;
-    if (p == 0) {
-        for (u32 i = tid; i < B; i += kLrThreads) hs_store(my + L.v + i, xw0[i] + xw1[i]);
-        lr_post(box, F_V, ep);
-    } else if (p == 1) {
-        if (!lr_wait(pbox, F_V, ep, ticks, status)) return;
-        vrecv = pv + L.v;
-    }
+    if (p == 0)
+        for (u32 i = tid; i < B; i += kLrThreads) msg_put(my + L.v, i, xw0[i] + xw1[i], tag);
+    const u64* vrecv = pv + L.v;  // P1
+    MsgWait vw = msg_begin(ep, status);
     // inputs straight into the wires (setTwoInputSharing): source s in
     // {aa_0, aa_1, b}, share h; a wave transposes the bits of its 64 rows
     const u64 WS = (u64)cir.wires * W;  // share stride
@@ -460,7 +511,7 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
         if (r < B) {
             if (src < 2) {
                 if (p == 0 && h == 0) val = xw0[r] + xw1[r] + (u64)it.thr_off[src];
-                if (p == 1 && h == 1) val = hs_load(vrecv + r) + (u64)it.thr_off[src];
+                if (p == 1 && h == 1) val = msg_get(vrecv, r, vw) + (u64)it.thr_off[src];
             } else {
                 if (p == 1 && h == 0) val = xw0[r];
                 if (p == 2 && h == 1) val = xw1[r];
@@ -469,55 +520,24 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
         // lane b stores bit b of the wave's 64 rows (one transpose, not 64 ballots)
         mem[h * WS + ((u64)cir.in_wire[src] + lane) * W + w] = transpose64(val, lane);
     }
-    __syncthreads();
+    if (!msg_done(vw, &msgBad, p == 1 ? ticks : nullptr)) return;
     lr_stamp(PT, 5);
     // the levels (roundCallback): unpack the previous level's received AND
-    // shares, then this level's batches, then publish its AND shares
-    // The level messages use the granule form of the in-kernel hand-off
-    // (cdna_hip_programming.md Guideline 16, R2): every 64-bit AND share goes
-    // as two 8-byte {epoch, half} words stored write-through, and the reader
-    // polls the words themselves until both carry this epoch -- one memory
-    // round trip per level instead of a drain, a flag and the payload load.
+    // shares (a message word per AND gate and row word), then this level's
+    // batches, then publish its AND shares
     const u64* zm = zmw;
-    const u32 tag = (u32)ep;
     const u32 W32 = (u32)W;
-    __shared__ u32 lvlBad;
-    if (tid == 0) lvlBad = 0;
     for (u32 lv = 0; lv <= cir.nlevels; ++lv) {
         if (lv > 0 && levelsL[lv - 1].nand) {
             const aby3g_lr_level& pl = levelsL[lv - 1];
             const u64* grows = pv + L.lvl + 2 * (u64)pl.and_wire_off * W;
-            const u64 t0 = wall_clock64();
-            bool ok = true;
-            for (u32 q = tid; q < pl.nand * W32 && ok; q += kLrThreads) {
-                u64 a, b;
-                for (u32 spins = 0;;) {
-                    a = hs_load(grows + 2 * q);
-                    b = hs_load(grows + 2 * q + 1);
-                    if ((u32)(a >> 32) == tag && (u32)(b >> 32) == tag) break;
-                    __builtin_amdgcn_s_sleep(1);
-                    if ((++spins & 63) == 0) {
-                        if (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
-                            ok = false;
-                            break;
-                        }
-                        if (wall_clock64() - t0 > kHandoffTimeoutTicks) {
-                            __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                            ok = false;
-                            break;
-                        }
-                    }
-                }
-                if (ok) {
-                    const u32 j = q / W32, w = q - j * W32;
-                    mem[WS + (u64)andWires[pl.and_wire_off + j] * W + w] = (u64)(u32)a | ((u64)(u32)b << 32);
-                }
+            MsgWait mw = msg_begin(ep, status);
+            for (u32 q = tid; q < pl.nand * W32 && mw.ok; q += kLrThreads) {
+                const u64 v = msg_get(grows, q, mw);
+                const u32 j = q / W32, w = q - j * W32;
+                if (mw.ok) mem[WS + (u64)andWires[pl.and_wire_off + j] * W + w] = v;
             }
-            if (!ok) lvlBad = 1;
-            if (tid == 0 && ticks)
-                __hip_atomic_fetch_add((gu64*)ticks, wall_clock64() - t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __syncthreads();
-            if (lvlBad) return;
+            if (!msg_done(mw, &msgBad, ticks)) return;
         }
         if (lv == cir.nlevels) break;
         const aby3g_lr_level& lvr = levelsL[lv];
@@ -535,9 +555,7 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
                 if (gate_is_and(g.type)) {
                     const u64 r = gate_and_share(g.type, x0, x1, y0, y1) ^ zm[(u64)g.z_row * W + w];
                     mem[(u64)g.out * W + w] = r;
-                    const u64 gi = 2 * ((u64)g.send_row * W + w);
-                    hs_store(gsend + gi, ((u64)tag << 32) | (u32)r);
-                    hs_store(gsend + gi + 1, ((u64)tag << 32) | (u32)(r >> 32));
+                    msg_put(gsend, (u64)g.send_row * W + w, r, tag);
                 } else {
                     u64 o0, o1;
                     gate_local(g.type, x0, x1, y0, y1, o0, o1);
@@ -600,9 +618,9 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
                 u64 s[2];
                 s[bb0] = zz;
                 s[bb0 ^ 1] = A0[i] + A1[i] + zz;
-                hs_store(my + L.ots + 2 * i, lo[3] ^ s[0]);
-                hs_store(my + L.ots + 2 * i + 1, hi[3] ^ s[1]);
-                hs_store(my + L.oth + i, bb1 ? hi[4] : lo[4]);
+                msg_put(my + L.ots, 2 * i, lo[3] ^ s[0], tag);
+                msg_put(my + L.ots, 2 * i + 1, hi[3] ^ s[1], tag);
+                msg_put(my + L.oth, i, bb1 ? hi[4] : lo[4], tag);
             } else {
                 // public product (Sh3Evaluator.cpp:430-447)
                 const u32 i = q - B;
@@ -616,19 +634,19 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
                 u64 t[2];
                 t[bb] = zs;
                 t[bb ^ 1] = (u64)it.one + zs;
-                hs_store(my + L.pma + 2 * i, lo[2] ^ t[0]);
-                hs_store(my + L.pma + 2 * i + 1, hi[2] ^ t[1]);
-                hs_store(my + L.pmb + 2 * i, lo[3] ^ t[0]);
-                hs_store(my + L.pmb + 2 * i + 1, hi[3] ^ t[1]);
+                msg_put(my + L.pma, 2 * i, lo[2] ^ t[0], tag);
+                msg_put(my + L.pma, 2 * i + 1, hi[2] ^ t[1], tag);
+                msg_put(my + L.pmb, 2 * i, lo[3] ^ t[0], tag);
+                msg_put(my + L.pmb, 2 * i + 1, hi[3] ^ t[1], tag);
             }
         }
-        lr_post(box, F_OT1, ep);
-        lr_post(box, F_PM, ep);
-        if (!lr_wait(nbox, F_PM, ep, ticks, status) || !lr_wait(pbox, F_PM, ep, ticks, status)) return;
+        if (tid == 0) hs_store(box + F_P3, ep);  // sends done: the helpers poll for err closely from here
+        MsgWait mw = msg_begin(ep, status);
         for (u32 i = tid; i < B; i += kLrThreads) {
-            g0[i] = hs_load(nx + L.pmb + i);  // P1's share of the product
-            g1[i] = hs_load(pv + L.pmb + i);  // P2's
+            g0[i] = msg_get(nx + L.pmb, i, mw);  // P1's share of the product
+            g1[i] = msg_get(pv + L.pmb, i, mw);  // P2's
         }
+        if (!msg_done(mw, &msgBad, ticks)) return;
     } else if (p == 1) {
         for (u32 q = tid; q < 2 * B; q += kLrThreads) {
             if (q < B) {
@@ -642,27 +660,26 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
                 fr1[i] = (wf & 1) ? hi[0] : lo[0];
                 const u64 zs = (j & 1) ? hi[1] - hi[2] : lo[1] - lo[2];
                 g1[i] = zs;
-                hs_store(my + L.pmb + i, zs);  // mine -> P0
+                msg_put(my + L.pmb, i, zs, tag);  // mine -> P0
             } else {
                 const u32 i = q - B;
                 u64 lo[1], hi[1];
                 lr_blocks<1>(T, {KL(kKeyOtn)}, {it.pm_ctr_next + i}, lo, hi);
-                hs_store(my + L.pma + i, (r2a[i] & 1) ? hi[0] : lo[0]);  // help -> P2
+                msg_put(my + L.pma, i, (r2a[i] & 1) ? hi[0] : lo[0], tag);  // help -> P2
             }
         }
-        lr_post(box, F_PM, ep);
-        if (!lr_wait(pbox, F_OT1, ep, ticks, status) || !lr_wait(nbox, F_OT1, ep, ticks, status)) return;
+        if (tid == 0) hs_store(box + F_P3, ep);  // sends done: the helpers poll for err closely from here
+        MsgWait mw = msg_begin(ep, status);
         for (u32 i = tid; i < B; i += kLrThreads) {
             // c0 = recv(P2's send, P0's help; choice b1) + recv(P0's send, P2's help; choice b0)
-            const u64 m1 = hs_load(nx + L.ots + 2 * i + (r1b[i] & 1)) ^ hs_load(pv + L.oth + i);
-            const u64 m0 = hs_load(pv + L.ots + 2 * i + (r1a[i] & 1)) ^ hs_load(nx + L.oth + i);
+            const u64 m1 = msg_get(nx + L.ots, 2 * i + (r1b[i] & 1), mw) ^ msg_get(pv + L.oth, i, mw);
+            const u64 m0 = msg_get(pv + L.ots, 2 * i + (r1a[i] & 1), mw) ^ msg_get(nx + L.oth, i, mw);
             fr0[i] = m1 + m0;
-            hs_store(my + L.otc + i, m1 + m0);  // -> P2
+            msg_put(my + L.otc, i, m1 + m0, tag);  // -> P2
         }
-        lr_post(box, F_OT2, ep);
-        if (!lr_wait(pbox, F_PM, ep, ticks, status) || !lr_wait(nbox, F_PM, ep, ticks, status)) return;
         for (u32 i = tid; i < B; i += kLrThreads)
-            g0[i] = hs_load(pv + L.pma + 2 * i + (r2a[i] & 1)) ^ hs_load(nx + L.pma + i);
+            g0[i] = msg_get(pv + L.pma, 2 * i + (r2a[i] & 1), mw) ^ msg_get(nx + L.pma, i, mw);
+        if (!msg_done(mw, &msgBad, ticks)) return;
     } else {
         for (u32 q = tid; q < 2 * B; q += kLrThreads) {
             if (q < B) {
@@ -679,9 +696,9 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
                 u64 s[2];
                 s[bb1] = zr;
                 s[bb1 ^ 1] = A1[i] + zr;
-                hs_store(my + L.oth + i, bb0 ? hi[2] : lo[2]);
-                hs_store(my + L.ots + 2 * i, lo[3] ^ s[0]);
-                hs_store(my + L.ots + 2 * i + 1, hi[3] ^ s[1]);
+                msg_put(my + L.oth, i, bb0 ? hi[2] : lo[2], tag);
+                msg_put(my + L.ots, 2 * i, lo[3] ^ s[0], tag);
+                msg_put(my + L.ots, 2 * i + 1, hi[3] ^ s[1], tag);
             } else {
                 // public product, helper
                 const u32 i = q - B;
@@ -692,17 +709,17 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
                 lr_blocks<3>(T, k, c, lo, hi);
                 const u64 zs = (j & 1) ? hi[0] - hi[1] : lo[0] - lo[1];
                 g0[i] = zs;
-                hs_store(my + L.pma + i, (r2b[i] & 1) ? hi[2] : lo[2]);  // help -> P1
-                hs_store(my + L.pmb + i, zs);                            // mine -> P0
+                msg_put(my + L.pma, i, (r2b[i] & 1) ? hi[2] : lo[2], tag);  // help -> P1
+                msg_put(my + L.pmb, i, zs, tag);                            // mine -> P0
             }
         }
-        lr_post(box, F_OT1, ep);
-        lr_post(box, F_PM, ep);
-        if (!lr_wait(pbox, F_OT2, ep, ticks, status)) return;
-        for (u32 i = tid; i < B; i += kLrThreads) fr1[i] = hs_load(pv + L.otc + i);
-        if (!lr_wait(nbox, F_PM, ep, ticks, status) || !lr_wait(pbox, F_PM, ep, ticks, status)) return;
-        for (u32 i = tid; i < B; i += kLrThreads)
-            g1[i] = hs_load(nx + L.pmb + 2 * i + (r2b[i] & 1)) ^ hs_load(pv + L.pma + i);
+        if (tid == 0) hs_store(box + F_P3, ep);  // sends done: the helpers poll for err closely from here
+        MsgWait mw = msg_begin(ep, status);
+        for (u32 i = tid; i < B; i += kLrThreads) {
+            fr1[i] = msg_get(pv + L.otc, i, mw);
+            g1[i] = msg_get(nx + L.pmb, 2 * i + (r2b[i] & 1), mw) ^ msg_get(pv + L.pma, i, mw);
+        }
+        if (!msg_done(mw, &msgBad, ticks)) return;
     }
     __syncthreads();
 
@@ -716,7 +733,7 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
         hs_store(e0 + i, fr0[i] + g0[i] - hy[i]);
         hs_store(e1 + i, fr1[i] + g1[i] - hy[B + i]);
     }
-    lr_post(box, F_LVL + cir.nlevels, ep);  // F_ERR
+    lr_post(box, F_ERR, ep);
     // prod = XX^T err: the helpers' partial sums over their rows
     prod = sc + L.prod;
     if (!lr_wait(box, F_H2, ep * G, ticks, status)) return;
@@ -732,19 +749,32 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
     const u32 sh2 = it.D + it.aB;
     u64* u0 = sc + L.upd;
     u64* u1 = u0 + d;
-    lr_trunc_pair(T, keys, it.t2_next_off / 8, it.t2_prev_off / 8, d, sh2, prod, my + L.z2, sc + L.z2own, u0, u1);
-    lr_post(box, F_Z2, ep);
+    lr_trunc_pair(T, keys, it.t2_next_off / 8, it.t2_prev_off / 8, d, sh2, prod, my + L.z2, tag, sc + L.z2own, u0, u1);
     lr_stamp(PT, 10);
-    if (p < 2) {
-        if (!lr_wait(nbox, F_Z2, ep, ticks, status) || !lr_wait(pbox, F_Z2, ep, ticks, status)) return;
-        lr_trunc_finalize(nx + L.z2, pv + L.z2, sc + L.z2own, d, sh2, p == 0 ? u0 : u1);
+    {
+        MsgWait mw = msg_begin(ep, status);
+        if (p < 2) lr_trunc_finalize(nx + L.z2, pv + L.z2, sc + L.z2own, d, sh2, p == 0 ? u0 : u1, mw);
+        if (!msg_done(mw, &msgBad, p < 2 ? ticks : nullptr)) return;
     }
-    __syncthreads();
     for (u32 k = tid; k < d; k += kLrThreads) {
         w0[k] -= u0[k];
         w1[k] -= u1[k];
     }
     lr_stamp(PT, 11);
+}
+
+__global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict__ T0g, aby3g_lr_iter it, LrKeys K,
+                                                           u32* status, int memInLds) {
+    __shared__ u32 lds[kAesLdsWords];
+    __shared__ u64 part[kLrThreads];
+    __shared__ __attribute__((aligned(16))) u32 keys[kLrKeys * kKeyWords];
+    extern __shared__ __attribute__((aligned(16))) u64 dyn[];  // [2][wires][W] engine memory, then [nand][W] masks
+    if (blockIdx.x > 0)
+        lr_helper(it, status, part);
+    else if (memInLds)
+        lr_party<true>(T0g, it, K, status, lds, keys, dyn);
+    else
+        lr_party<false>(T0g, it, K, status, lds, keys, dyn);
 }
 
 }  // namespace

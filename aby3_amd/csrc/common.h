@@ -182,18 +182,42 @@ __host__ __device__ __forceinline__ u32 aes_sb4(u32 A, u32 B, u32 C, u32 D) {
 // 64 x 64 bit transpose across a wave: lane i holds row i (bit k = column k);
 // afterwards lane i holds column i (bit k = bit i of row k). Six butterfly
 // stages: at stage j the lanes i and i ^ j swap the off-diagonal j x j
-// blocks of their 2j x 2j block (one 64-bit lane exchange + masks each),
-// instead of 64 ballots.
+// blocks of their 2j x 2j block. The exchanges stay off the LDS pipe
+// (ds_bpermute, twelve per transpose, made the C5 mapped transposes ~40 %
+// slower): gfx950's v_permlane32_swap does stage 32 in one instruction (lanes
+// below 32 keep their low words and take the partner's, lanes above keep
+// their high words), v_permlane16_swap stage 16 on 16-bit pieces packed into
+// whole words (E: pieces 0 and 2, O: pieces 1 and 3), and DPP row / quad
+// permutations the stages within a row of 16 lanes.
+template <int kCtrl>
+__device__ __forceinline__ u32 dpp_mov(u32 v) {
+    return __builtin_amdgcn_update_dpp(0u, v, kCtrl, 0xf, 0xf, false);
+}
+template <int kCtrl>
+__device__ __forceinline__ u64 dpp_mov64(u64 v) {
+    return (u64)dpp_mov<kCtrl>((u32)v) | ((u64)dpp_mov<kCtrl>((u32)(v >> 32)) << 32);
+}
+__device__ __forceinline__ u64 transpose_stage(u64 x, u64 y, u32 lane, u32 j, u64 m) {
+    return (lane & j) ? ((x & ~m) | ((y & ~m) >> j)) : ((x & m) | ((y & m) << j));
+}
 __device__ __forceinline__ u64 transpose64(u64 x, u32 lane) {
-    constexpr u64 kMask[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
-                              0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
-#pragma unroll
-    for (int st = 0; st < 6; ++st) {
-        const u32 j = 32u >> st;
-        const u64 m = kMask[st];
-        const u64 y = __shfl_xor(x, (int)j, 64);
-        x = (lane & j) ? ((x & ~m) | ((y & ~m) >> j)) : ((x & m) | ((y & m) << j));
+    u32 lo = (u32)x, hi = (u32)(x >> 32);
+    {  // j = 32
+        const auto r = __builtin_amdgcn_permlane32_swap(lo, hi, false, false);
+        lo = r[0];
+        hi = r[1];
     }
+    {  // j = 16
+        const u32 e = (lo & 0xffffu) | (hi << 16), o = (lo >> 16) | (hi & 0xffff0000u);
+        const auto r = __builtin_amdgcn_permlane16_swap(e, o, false, false);
+        lo = (r[0] & 0xffffu) | (r[1] << 16);
+        hi = (r[0] >> 16) | (r[1] & 0xffff0000u);
+    }
+    x = (u64)lo | ((u64)hi << 32);
+    x = transpose_stage(x, dpp_mov64<0x128>(x), lane, 8, 0x00FF00FF00FF00FFull);                     // row_ror:8 = i ^ 8
+    x = transpose_stage(x, dpp_mov64<0x141>(dpp_mov64<0x1B>(x)), lane, 4, 0x0F0F0F0F0F0F0F0Full);   // (i ^ 3) ^ 7
+    x = transpose_stage(x, dpp_mov64<0x4E>(x), lane, 2, 0x3333333333333333ull);                     // quad_perm 2,3,0,1
+    x = transpose_stage(x, dpp_mov64<0xB1>(x), lane, 1, 0x5555555555555555ull);                     // quad_perm 1,0,3,2
     return x;
 }
 

@@ -476,8 +476,9 @@ int aby3g_bits_to_wires_lin(const aby3g_wire_src* srcs, uint32_t nsrc, uint64_t 
  * resharing, the int_Sh3Piecewise_helper circuit level by level, the OT
  * product and the public-constant product, Sh3Evaluator.cpp:119-263,
  * 418-501), err = f - YY, mulTruncate(XX^T, err, aB) and w -= update.
- * Every message goes through the parties' mailboxes with in-kernel hand-offs
- * (aby3g_handoff's write-through payload + flag form); the randomness is the
+ * Every message goes through the parties' mailboxes as in-kernel hand-offs:
+ * each 64-bit word as two write-through {epoch, 32-bit half} words that the
+ * reader polls until both carry its epoch (no flags); the randomness is the
  * op-by-op path's, at the stream positions, draw indices and OT counters the
  * host passes, so the shares are bit-identical to that path's.
  *

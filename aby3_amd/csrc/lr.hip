@@ -214,19 +214,36 @@ __device__ __forceinline__ bool msg_done(const MsgWait& w, u32* bad, u64* ticks)
 // t0 = next-stream word (nw0 + i), t1 = prev-stream word (pw0 + i);
 // z = prod - (t0 >> 2) published into `out` (write-through) and kept in own,
 // C = (t0 >> (d+2), t1 >> (d+2)) into c0 / c1.
+// Tiles of 256 elements: an AES block holds two consecutive stream words, so
+// a tile needs at most 129 blocks of each stream -- threads [0, 256) draw the
+// next stream's, [256, 512) the prev stream's, one block each, into tw (512
+// u64 of LDS), then the tile's elements are formed from it.
 __device__ __forceinline__ void lr_trunc_pair(const u32* T, const u32* keys, u64 nw0, u64 pw0, u32 n, u32 d,
-                                              const u64* prod, u64* out, u32 tag, u64* own, u64* c0, u64* c1) {
-    for (u32 i = threadIdx.x; i < n; i += kLrThreads) {
-        const u32* const k[2] = {keys + kKeyNext * kKeyWords, keys + kKeyPrev * kKeyWords};
-        u64 lo[2], hi[2];
-        lr_blocks<2>(T, k, {(nw0 + i) >> 1, (pw0 + i) >> 1}, lo, hi);
-        const i64 t0 = (i64)(((nw0 + i) & 1) ? hi[0] : lo[0]);
-        const i64 t1 = (i64)(((pw0 + i) & 1) ? hi[1] : lo[1]);
-        const u64 z = prod[i] - (u64)(t0 >> 2);
-        own[i] = z;
-        msg_put(out, i, z, tag);
-        c0[i] = (u64)(t0 >> (d + 2));
-        c1[i] = (u64)(t1 >> (d + 2));
+                                              const u64* prod, u64* out, u32 tag, u64* own, u64* c0, u64* c1,
+                                              u64* tw) {
+    const u32 tid = threadIdx.x, half = tid >> 8, t = tid & 255;
+    for (u32 i0 = 0; i0 < n; i0 += 256) {
+        const u32 nt = min(256u, n - i0);
+        const u64 w0 = (half ? pw0 : nw0) + i0;  // this half's first stream word of the tile
+        const u64 b = (w0 >> 1) + t;              // block t of it
+        if (b <= ((w0 + nt - 1) >> 1)) {
+            u64 lo[1], hi[1];
+            lr_blocks<1>(T, {keys + (half ? kKeyPrev : kKeyNext) * kKeyWords}, {b}, lo, hi);
+            const u64 j = 2 * b - w0;  // tile position of the block's low word (-1: before the tile)
+            if (2 * b >= w0) tw[half * 256 + j] = lo[0];
+            if (j + 1 < nt) tw[half * 256 + j + 1] = hi[0];
+        }
+        __syncthreads();
+        if (tid < nt) {
+            const u32 i = i0 + tid;
+            const i64 t0 = (i64)tw[tid], t1 = (i64)tw[256 + tid];
+            const u64 z = prod[i] - (u64)(t0 >> 2);
+            own[i] = z;
+            msg_put(out, i, z, tag);
+            c0[i] = (u64)(t0 >> (d + 2));
+            c1[i] = (u64)(t1 >> (d + 2));
+        }
+        __syncthreads();
     }
 }
 
@@ -392,7 +409,7 @@ __device__ __forceinline__ void lr_stamp(u64* ticks, u32 s) {
 // for the write-through AND shares just sent (~1 us a level).
 template <bool kLds>
 __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it, const LrKeys& K, u32* status,
-                                         u32* lds, u32* keys, u64* dyn) {
+                                         u32* lds, u32* keys, u64* dyn, u64* tw) {
     u64* const PT = it.phase_ticks;
     lr_stamp(PT, 0);
     {
@@ -461,15 +478,21 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
     {
         u64* zm = zmw;
         const u64 Wh = (W + 1) / 2;
-        for (u64 q = tid; q < (u64)cir.nand * Wh; q += kLrThreads) {
-            const u64 k = q / Wh, wp = q % Wh;
+        // two items per thread (q, q + 512), their four blocks interleaved:
+        // one chain of table reads per thread (8 waves leave the LDS idle otherwise)
+        const u64 items = (u64)cir.nand * Wh;
+        for (u64 q = tid; q < items; q += 2 * kLrThreads) {
+            const u64 q2 = q + kLrThreads < items ? q + kLrThreads : q;  // a duplicate of q when none is left
+            const u64 k = q / Wh, wp = q % Wh, k2 = q2 / Wh, wp2 = q2 % Wh;
             const u64 c = (k * L.Wpad + 2 * wp) >> 1;  // Wpad is even: draws 2wp, 2wp + 1 share a block
-            const u32* const kk[2] = {KL(kKeyMp), KL(kKeyMn)};
-            const u64 cc[2] = {c, c};
-            u64 lo[2], hi[2];
-            lr_blocks<2>(T, kk, cc, lo, hi);  // interleaved: 8 waves leave the LDS idle otherwise
+            const u64 c2 = (k2 * L.Wpad + 2 * wp2) >> 1;
+            const u32* const kk[4] = {KL(kKeyMp), KL(kKeyMn), KL(kKeyMp), KL(kKeyMn)};
+            u64 lo[4], hi[4];
+            lr_blocks<4>(T, kk, {c, c, c2, c2}, lo, hi);
             zm[k * W + 2 * wp] = lo[0] ^ lo[1];
             if (2 * wp + 1 < W) zm[k * W + 2 * wp + 1] = hi[0] ^ hi[1];
+            zm[k2 * W + 2 * wp2] = lo[2] ^ lo[3];
+            if (2 * wp2 + 1 < W) zm[k2 * W + 2 * wp2 + 1] = hi[2] ^ hi[3];
         }
     }
 
@@ -486,7 +509,7 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
     __shared__ u32 msgBad;
     if (tid == 0) msgBad = 0;
     lr_trunc_pair(T, keys, it.t1_next_off / 8, it.t1_prev_off / 8, B, it.D, prod, my + L.z1, tag, sc + L.z1own, xw0,
-                  xw1);
+                  xw1, tw);
     lr_stamp(PT, 3);
     {
         MsgWait mw = msg_begin(ep, status);
@@ -749,7 +772,7 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
     const u32 sh2 = it.D + it.aB;
     u64* u0 = sc + L.upd;
     u64* u1 = u0 + d;
-    lr_trunc_pair(T, keys, it.t2_next_off / 8, it.t2_prev_off / 8, d, sh2, prod, my + L.z2, tag, sc + L.z2own, u0, u1);
+    lr_trunc_pair(T, keys, it.t2_next_off / 8, it.t2_prev_off / 8, d, sh2, prod, my + L.z2, tag, sc + L.z2own, u0, u1, tw);
     lr_stamp(PT, 10);
     {
         MsgWait mw = msg_begin(ep, status);
@@ -772,9 +795,9 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
     if (blockIdx.x > 0)
         lr_helper(it, status, part);
     else if (memInLds)
-        lr_party<true>(T0g, it, K, status, lds, keys, dyn);
+        lr_party<true>(T0g, it, K, status, lds, keys, dyn, part);
     else
-        lr_party<false>(T0g, it, K, status, lds, keys, dyn);
+        lr_party<false>(T0g, it, K, status, lds, keys, dyn, part);
 }
 
 }  // namespace

@@ -453,6 +453,45 @@ __device__ __forceinline__ u64 map_row(const aby3g_rowmap& m, u64 p) {
     return m.start + rep * m.rep_stride + k * m.step;
 }
 
+// Rows p, p + 64, p + 128, ... of an affine map without a division per row
+// (a 32- or 64-bit division is ~20-40 VALU ops, 16 of them per thread made the
+// mapped transposes VALU-bound): one division at the start, then each step
+// adds 64 / per_rep reps and 64 % per_rep positions with one carry.
+struct MapWalk {
+    u64 q, rep, k, qd, qm;
+};
+__device__ __forceinline__ MapWalk map_walk(const aby3g_rowmap& m, u64 p) {
+    MapWalk w;
+    w.q = m.first + p;
+    if (m.idx) return w;
+    if (((w.q | m.per_rep) >> 32) == 0) {
+        const u32 qq = (u32)w.q, pr = (u32)m.per_rep, r32 = qq / pr;
+        w.rep = r32;
+        w.k = qq - r32 * pr;
+        w.qd = 64u / pr;
+        w.qm = 64u - (u32)w.qd * pr;
+    } else {
+        w.rep = w.q / m.per_rep;
+        w.k = w.q - w.rep * m.per_rep;
+        w.qd = 64 / m.per_rep;
+        w.qm = 64 - w.qd * m.per_rep;
+    }
+    return w;
+}
+__device__ __forceinline__ u64 map_walk_row(const aby3g_rowmap& m, const MapWalk& w) {
+    return m.idx ? m.idx[w.q] : m.start + w.rep * m.rep_stride + w.k * m.step;
+}
+__device__ __forceinline__ void map_walk_next(const aby3g_rowmap& m, MapWalk& w) {
+    w.q += 64;
+    if (m.idx) return;
+    w.k += w.qm;
+    w.rep += w.qd;
+    if (w.k >= m.per_rep) {
+        w.k -= m.per_rep;
+        ++w.rep;
+    }
+}
+
 // LDS-tiled bits -> wires over mapped source rows (the round's gather fused
 // into setInput). Rows mapped outside the source read as zero.
 // Up to two (map, destination) pairs per launch, blockIdx.z selecting one:
@@ -476,16 +515,18 @@ __global__ void __launch_bounds__(256) k_bits_to_wires_map(const i64* __restrict
     const u64 c = blockIdx.x / tilesPerCol, w0 = (blockIdx.x % tilesPerCol) * kTileWords;
     const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     u64 vv[16];
+    MapWalk mw = map_walk(map, (w0 + wave * 16) * 64 + lane);  // the thread's rows step by 64
 #pragma unroll
     for (u32 k = 0; k < 16; ++k) {
         const u32 wl = wave * 16 + k;
         const u64 r = (w0 + wl) * 64 + lane;
         u64 v = 0;
         if (w0 + wl < words && r < rows) {
-            const u64 src = map_row(map, r);
+            const u64 src = map_walk_row(map, mw);
             if (src < inRows) v = (u64)in[src * cols64 + c];
         }
         vv[k] = v;
+        map_walk_next(map, mw);
     }
     // unrolled: the 16 transposes are independent, so their shuffle stages
     // interleave instead of waiting out each one's latency in turn (the
@@ -533,14 +574,16 @@ __global__ void __launch_bounds__(256) k_wires_to_bits_map(const u64* __restrict
     // unrolled, as in k_bits_to_wires_map: 16 independent transposes in flight
 #pragma unroll
     for (u32 k = 0; k < 16; ++k) vv[k] = transpose64(tile[lane * kTilePitch + wave * 16 + k], lane);
+    MapWalk mw = map_walk(map, (w0 + wave * 16) * 64 + lane);
 #pragma unroll
     for (u32 k = 0; k < 16; ++k) {
         const u32 wl = wave * 16 + k;
         const u64 row = (w0 + wl) * 64 + lane;
         if (w0 + wl < rw && row < rows) {
-            const u64 dst = map_row(map, row);
+            const u64 dst = map_walk_row(map, mw);
             if (dst < outRows) out[dst * cols + c] = (i64)vv[k];
         }
+        map_walk_next(map, mw);
     }
 }
 

@@ -436,25 +436,9 @@ __global__ void __launch_bounds__(64) k_b2w_lin_regs(WireSrcs ws, u64 rows, u64 
         if (c * 64 + b < src.nbits) out[(c * 64 + b) * words + w] = R[b];
 }
 
-// Row p of a merge round's compare-exchange list -> row of the merge array
-// (aby3g_rowmap). 32-bit division whenever the operands fit.
-__device__ __forceinline__ u64 map_row(const aby3g_rowmap& m, u64 p) {
-    const u64 q = m.first + p;
-    if (m.idx) return m.idx[q];
-    u64 rep, k;
-    if (((q | m.per_rep) >> 32) == 0) {
-        const u32 qq = (u32)q, pr = (u32)m.per_rep, r32 = qq / pr;
-        rep = r32;
-        k = qq - r32 * pr;
-    } else {
-        rep = q / m.per_rep;
-        k = q - rep * m.per_rep;
-    }
-    return m.start + rep * m.rep_stride + k * m.step;
-}
-
-// Rows p, p + 64, p + 128, ... of an affine map without a division per row
-// (a 32- or 64-bit division is ~20-40 VALU ops, 16 of them per thread made the
+// Rows p, p + 64, p + 128, ... of a merge round's compare-exchange list ->
+// rows of the merge array (aby3g_rowmap), without a division per row (a 32-
+// or 64-bit division is ~20-40 VALU ops, 16 of them per thread made the
 // mapped transposes VALU-bound): one division at the start, then each step
 // adds 64 / per_rep reps and 64 % per_rep positions with one carry.
 struct MapWalk {

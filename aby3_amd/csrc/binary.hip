@@ -245,7 +245,8 @@ __global__ void __launch_bounds__(256) k_wires_to_bits(const u64* __restrict__ m
 // wave bit-transposes 16 words (transpose64) into an LDS tile [bit][word], then
 // the tile leaves as 64 contiguous 512-byte wire segments. wires -> bits:
 // the reverse, reading 512-byte wire segments into the tile.
-constexpr u32 kTileWords = 64;
+constexpr u32 kTileWords = 32;                   // words of a 256-thread tile workgroup
+constexpr u32 kWaveWords = kTileWords / 4;       // words a wave transposes (64 x 64 bits each)
 constexpr u32 kTilePitch = kTileWords + 1;  // u64 per tile row (+1: bank spread)
 
 // ---- register transposes: one thread per 64-row word ----------------------
@@ -498,11 +499,11 @@ __global__ void __launch_bounds__(256) k_bits_to_wires_map(const i64* __restrict
     const u64 tilesPerCol = (words + kTileWords - 1) / kTileWords;
     const u64 c = blockIdx.x / tilesPerCol, w0 = (blockIdx.x % tilesPerCol) * kTileWords;
     const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    u64 vv[16];
-    MapWalk mw = map_walk(map, (w0 + wave * 16) * 64 + lane);  // the thread's rows step by 64
+    u64 vv[kWaveWords];
+    MapWalk mw = map_walk(map, (w0 + wave * kWaveWords) * 64 + lane);  // the thread's rows step by 64
 #pragma unroll
-    for (u32 k = 0; k < 16; ++k) {
-        const u32 wl = wave * 16 + k;
+    for (u32 k = 0; k < kWaveWords; ++k) {
+        const u32 wl = wave * kWaveWords + k;
         const u64 r = (w0 + wl) * 64 + lane;
         u64 v = 0;
         if (w0 + wl < words && r < rows) {
@@ -512,13 +513,12 @@ __global__ void __launch_bounds__(256) k_bits_to_wires_map(const i64* __restrict
         vv[k] = v;
         map_walk_next(map, mw);
     }
-    // unrolled: the 16 transposes are independent, so their shuffle stages
-    // interleave instead of waiting out each one's latency in turn (the
-    // rolled loop ran 16 x 6 dependent ds_bpermute rounds per wave)
+    // unrolled: the transposes are independent, so their exchange stages
+    // interleave instead of waiting out each one's latency in turn
 #pragma unroll
-    for (u32 k = 0; k < 16; ++k) vv[k] = transpose64(vv[k], lane);
+    for (u32 k = 0; k < kWaveWords; ++k) vv[k] = transpose64(vv[k], lane);
 #pragma unroll
-    for (u32 k = 0; k < 16; ++k) tile[lane * kTilePitch + wave * 16 + k] = vv[k];
+    for (u32 k = 0; k < kWaveWords; ++k) tile[lane * kTilePitch + wave * kWaveWords + k] = vv[k];
     __syncthreads();
     for (u32 idx = threadIdx.x; idx < 64 * kTileWords; idx += 256) {
         const u32 b = idx / kTileWords, wl = idx % kTileWords;
@@ -541,27 +541,27 @@ __global__ void __launch_bounds__(256) k_wires_to_bits_map(const u64* __restrict
     const u64 rw = (rows + 63) / 64;
     const u64 tilesPerCol = (rw + kTileWords - 1) / kTileWords;
     const u64 c = blockIdx.x / tilesPerCol, w0 = (blockIdx.x % tilesPerCol) * kTileWords;
-    u64 vv[16];
+    u64 vv[kWaveWords];  // 64 x kTileWords words over 256 threads
 #pragma unroll
-    for (u32 j = 0; j < 16; ++j) {
+    for (u32 j = 0; j < kWaveWords; ++j) {
         const u32 idx = threadIdx.x + 256 * j, b = idx / kTileWords, wl = idx % kTileWords;
         const u64 bit = c * 64 + b;
         vv[j] = (bit < nbits && w0 + wl < rw) ? mem[(u64)wires[bit] * words + w0 + wl] : 0;
     }
 #pragma unroll
-    for (u32 j = 0; j < 16; ++j) {
+    for (u32 j = 0; j < kWaveWords; ++j) {
         const u32 idx = threadIdx.x + 256 * j;
         tile[(idx / kTileWords) * kTilePitch + idx % kTileWords] = vv[j];
     }
     __syncthreads();
     const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // unrolled, as in k_bits_to_wires_map: 16 independent transposes in flight
+    // unrolled, as in k_bits_to_wires_map: independent transposes in flight
 #pragma unroll
-    for (u32 k = 0; k < 16; ++k) vv[k] = transpose64(tile[lane * kTilePitch + wave * 16 + k], lane);
-    MapWalk mw = map_walk(map, (w0 + wave * 16) * 64 + lane);
+    for (u32 k = 0; k < kWaveWords; ++k) vv[k] = transpose64(tile[lane * kTilePitch + wave * kWaveWords + k], lane);
+    MapWalk mw = map_walk(map, (w0 + wave * kWaveWords) * 64 + lane);
 #pragma unroll
-    for (u32 k = 0; k < 16; ++k) {
-        const u32 wl = wave * 16 + k;
+    for (u32 k = 0; k < kWaveWords; ++k) {
+        const u32 wl = wave * kWaveWords + k;
         const u64 row = (w0 + wl) * 64 + lane;
         if (w0 + wl < rw && row < rows) {
             const u64 dst = map_walk_row(map, mw);

@@ -15,10 +15,17 @@ def main():
     link, device = sys.argv[4], int(sys.argv[5])
     params = [int(x) for x in sys.argv[6].split(",")] if len(sys.argv) > 6 and sys.argv[6] else []
     s = native.Session.party(job, params, party, link, device=device, colocated=True)
+    # a lagging party (tests): its host sleeps between steps, so the others run ahead
+    lag = float(os.environ.get("ABY3_TEST_LAG_MS", "0")) / 1e3
     try:
         s.run(1)  # warm-up
         t0 = time.perf_counter()
-        s.run(steps)
+        if lag:
+            for _ in range(steps):
+                s.run(1)
+                time.sleep(lag)
+        else:
+            s.run(steps)
         dt = time.perf_counter() - t0
         ok = s.check()
         info = s.info()

@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def run_parties(job, params, steps, tag, timeout=150):
+def run_parties(job, params, steps, tag, timeout=150, lag_ms=0):
     link = f"gt{os.getpid()}.{tag}"
     env = dict(os.environ, ABY3_LINK_TIMEOUT_S="100")
     args = [str(job), None, str(steps), link, "0", ",".join(str(p) for p in params)]
@@ -26,8 +26,9 @@ def run_parties(job, params, steps, tag, timeout=150):
     for party in range(3):
         a = list(args)
         a[1] = str(party)
+        penv = dict(env, ABY3_TEST_LAG_MS=str(lag_ms)) if party == 0 and lag_ms else env
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "party_worker.py"), *a],
-                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=penv))
     outs = []
     try:
         for p in procs:
@@ -53,5 +54,15 @@ def run_parties(job, params, steps, tag, timeout=150):
 ])
 def test_three_party_processes(gpu, job, params, steps):
     outs = run_parties(job, params, steps, f"{job}_{params[0]}")
+    assert sorted(o["party"] for o in outs) == [0, 1, 2]
+    assert all(o["ok"] for o in outs), outs
+
+
+def test_lagging_party_many_steps(gpu):
+    """Party 0's host sleeps 5 ms between 60 steps of the C2 multiplication:
+    party 2 only sends (Sh3Evaluator.cpp:152-153) and runs ahead until its
+    staging slots are all in flight, then waits for them (Channel.cpp, the
+    sender's throttle) instead of failing or growing without bound."""
+    outs = run_parties(nt.JOB_MUL_TRUNC, [1024, 1024, 1024, 16, 1], 60, "lag", timeout=200, lag_ms=5)
     assert sorted(o["party"] for o in outs) == [0, 1, 2]
     assert all(o["ok"] for o in outs), outs

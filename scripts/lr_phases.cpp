@@ -128,18 +128,6 @@ int main(int argc, char** argv) {
                     std::printf(" L%d %.1f", lv, v[v.size() / 2]);
                 }
             }
-            std::printf("\n   unpacked after:");  // slots 24 + lv (probe): previous level's shares in
-            for (int lv = 0; lv < 8; ++lv) {
-                std::vector<double> v;
-                for (u64 t = iters / 2; t < iters; ++t) {
-                    const u64 a = stamps[p][32 * t + (lv ? 16 + lv - 1 : 5)], b = stamps[p][32 * t + 24 + lv];
-                    if (b) v.push_back(0.01 * (double)(b - a));
-                }
-                if (!v.empty()) {
-                    std::sort(v.begin(), v.end());
-                    std::printf(" L%d %.1f", lv, v[v.size() / 2]);
-                }
-            }
             std::printf("\n  ");
         }
         std::vector<double> gap;  // launch-to-launch gap: end of t-1 to start of t

@@ -88,8 +88,9 @@ void logisticModelGen(const std::vector<double>& model, u64 n, u64 D, i64Matrix&
 // getSubset (Regression.h:24-40): mini-batches without replacement from the
 // pool 0..n-1, reshuffled with std::random_shuffle (for i = 1..n-1: swap with
 // j = r(i + 1)) when exhausted, r(m) = PRNG(toBlock(234543234)).get<u64>() % m
-// (the reference's functor type is unpinned; parity rests on the committed
-// batch list tests/golden/lr.json).
+// (checked against libstdc++'s std::random_shuffle on the same stream by
+// tests/cpp/test_random_shuffle.cpp; the functor's get<u64>() % m is
+// cryptoTools' PRNG::operator()(R), not vendored in the reference).
 class BatchSampler {
 public:
     explicit BatchSampler(u64 n);

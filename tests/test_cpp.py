@@ -55,3 +55,9 @@ def test_convert_protocols_gpu():
 def test_convert_oracle_revealed():
     # the oracle's share conversions against the reference tests' revealed checks (CPU)
     _run("test_convert_oracle", 120)
+
+
+def test_random_shuffle_restatements():
+    # product and oracle batch sampling / shuffle permutations against libstdc++'s
+    # own std::random_shuffle on the same PRNG stream (CPU)
+    _run("test_random_shuffle", 120)

@@ -567,6 +567,11 @@ int orc_lr_dataset(uint64_t n, uint64_t dim, uint64_t D, int64_t* X, int64_t* Y,
     });
 }
 
+// logisticLabelMargin of the C4 dataset's first n rows (orc_ml.cpp)
+int orc_lr_label_margin(uint64_t n, uint64_t dim, double* margin) {
+    return guard([&] { *margin = logisticLabelMargin(logisticModel(dim), n); });
+}
+
 // getSubset's first `iters` mini-batches of B indices over n rows: out [iters][B]
 int orc_lr_batches(uint64_t n, uint64_t B, uint64_t iters, uint64_t* out) {
     return guard([&] {

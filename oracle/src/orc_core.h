@@ -294,6 +294,9 @@ std::vector<double> logisticModel(u64 dim);
 // row; Y = [X model + noise > 0]; both converted to fixed point D as
 // fp<i64, D>::operator=(double) (Sh3FixedPoint.h:94-97: i64(v * 2^D)).
 void logisticModelGen(const std::vector<double>& model, u64 n, u64 D, Mat& X, Mat& Y);
+// min over rows of |X m + noise| / (2 x the summation-order error bound):
+// > 1 = labels independent of the summation order (orc_ml.cpp)
+double logisticLabelMargin(const std::vector<double>& model, u64 n);
 // getSubset (Regression.h:24-40) over the pool 0..n-1, reshuffled by
 // std::random_shuffle (libstdc++: for i in 1..n-1, j = r(i + 1), swap) with
 // the cryptoTools PRNG(toBlock(234543234)) as the RNG functor r(m) =

@@ -8,6 +8,8 @@
 #include "orc_core.h"
 #include <algorithm>
 #include <random>
+#include <cmath>
+#include <limits>
 
 namespace orc {
 
@@ -40,6 +42,38 @@ void logisticModelGen(const std::vector<double>& model, u64 n, u64 D, Mat& X, Ma
         for (u64 j = 0; j < dim; ++j) X.v[i * dim + j] = (i64)(row[j] * (double)(1ull << D));
         Y.v[i] = (i64)((y > 0 ? 1.0 : 0.0) * (double)(1ull << D));
     }
+}
+
+// How far every label of logisticModelGen is from flipping under another
+// summation order of X * mModel (the reference's Eigen GEMV,
+// LinearModelGen.cpp:75, sums in its own blocked / FMA order; this
+// restatement sums left to right). Any order's sum of the dim products lies
+// within E = gamma_dim * sum_j |x_j m_j| of the exact one (gamma_n = n u /
+// (1 - n u), u = 2^-53), so two orders can disagree on the sign of
+// sum + noise only where |sum + noise| <= 2E (the final add rounds to
+// nearest and keeps the sign). Returns min over rows of |sum + noise| / 2E
+// (infinity when no row has a non-zero product): > 1 means the labels are
+// the same under every summation order.
+double logisticLabelMargin(const std::vector<double>& model, u64 n) {
+    const u64 dim = model.size();
+    std::default_random_engine generator(234345);
+    std::normal_distribution<double> distribution(1.0, 1.0);
+    const double u = std::ldexp(1.0, -53), gamma = dim * u / (1 - dim * u);
+    double worst = std::numeric_limits<double>::infinity();
+    std::vector<double> row(dim);
+    for (u64 i = 0; i < n; ++i) {
+        for (u64 j = 0; j < dim; ++j) row[j] = distribution(generator);
+        const double noise = distribution(generator);
+        double y = 0, a = 0;
+        for (u64 j = 0; j < dim; ++j) {
+            y += row[j] * model[j];
+            a += std::fabs(row[j] * model[j]);
+        }
+        // E itself is computed in floating point: inflate it by 1 %
+        const double E = 1.01 * gamma * a;
+        if (E > 0) worst = std::min(worst, std::fabs(y + noise) / (2 * E));
+    }
+    return worst;
 }
 
 BatchSampler::BatchSampler(u64 n) : pool(n), iter(n) {

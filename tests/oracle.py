@@ -197,6 +197,15 @@ def lr_dataset(n: int, dim: int = 128, D: int = 16):
     return X, Y, m
 
 
+def lr_label_margin(n: int, dim: int = 128) -> float:
+    """min over the C4 dataset's first n rows of |X m + noise| over twice the
+    summation-order error bound of X m: > 1 means every label is the same
+    under any summation order (the reference's Eigen GEMV included)."""
+    out = ctypes.c_double(0)
+    _check(dll().orc_lr_label_margin(c_uint64(n), c_uint64(dim), ctypes.byref(out)))
+    return out.value
+
+
 def lr_batches(n: int, B: int = 256, iters: int = 1):
     """The oracle's getSubset restatement: the first `iters` mini-batches [iters][B]."""
     out = np.zeros((iters, B), dtype=np.uint64)

@@ -25,6 +25,16 @@ def A(x, dt=np.int64):
     return np.asarray(x, dtype=dt)
 
 
+@pytest.mark.parametrize("n", [FX["n"], 1_000_000])
+def test_labels_independent_of_summation_order(n):
+    # The reference labels rows by Eigen's GEMV X * mModel + noise
+    # (LinearModelGen.cpp:75); the restatements sum left to right. Every row's
+    # |sum + noise| exceeds twice the error bound any summation order can
+    # reach, so the labels -- of the fixture's rows and of the whole 10^6-row
+    # C4 dataset -- are the reference's whatever order Eigen sums in.
+    assert orc.lr_label_margin(n, FX["d"]) > 1.0
+
+
 def test_dataset_product_equals_oracle_and_fixture():
     X, Y, m = nt.lr_dataset(FX["n"], FX["d"], FX["D"])
     Xo, Yo, mo = orc.lr_dataset(FX["n"], FX["d"], FX["D"])

@@ -260,7 +260,7 @@ int odd_even_merge(const sbMatrix& data1, const sbMatrix& data2, sbMatrix& res, 
 }
 
 int odd_even_multi_merge(const sbMatrix& flat, const std::vector<u64>& lensIn, sbMatrix& sorted, int pIdx,
-                         Sh3Evaluator& eval, Sh3Runtime& runtime) {
+                         Sh3Evaluator& eval, Sh3Runtime& runtime, MergeOrder order) {
     if (lensIn.empty()) throw std::invalid_argument("odd_even_multi_merge: no lists " LOCATION);
     u64 total = 0;
     for (u64 l : lensIn) total += l;
@@ -287,7 +287,10 @@ int odd_even_multi_merge(const sbMatrix& flat, const std::vector<u64>& lensIn, s
                 ms.push_back(MergeSpec{off[i], lens[i], lens[i + 1]});
                 next.push_back(lens[i] + lens[i + 1]);
             }
-            mergeBatch(cur, ms, pIdx, eval, runtime);
+            if (order == MergeOrder::Sequential)
+                for (const MergeSpec& m : ms) mergeBatch(cur, {m}, pIdx, eval, runtime);
+            else
+                mergeBatch(cur, ms, pIdx, eval, runtime);
             lens = std::move(next);
         }
     }
@@ -296,7 +299,7 @@ int odd_even_multi_merge(const sbMatrix& flat, const std::vector<u64>& lensIn, s
 }
 
 int odd_even_multi_merge(std::vector<sbMatrix>& data, sbMatrix& sorted, int pIdx, Sh3Evaluator& eval,
-                         Sh3Runtime& runtime) {
+                         Sh3Runtime& runtime, MergeOrder order) {
     std::vector<const sbMatrix*> parts;
     std::vector<u64> lens;
     for (auto& d : data) {
@@ -305,7 +308,7 @@ int odd_even_multi_merge(std::vector<sbMatrix>& data, sbMatrix& sorted, int pIdx
     }
     sbMatrix flat;
     concatRows(parts, flat, runtime.gpu());
-    return odd_even_multi_merge(flat, lens, sorted, pIdx, eval, runtime);
+    return odd_even_multi_merge(flat, lens, sorted, pIdx, eval, runtime, order);
 }
 
 int odd_even_merge_sort(const sbMatrix& keys, sbMatrix& sorted, int pIdx, Sh3Evaluator& eval, Sh3Runtime& runtime) {

@@ -56,14 +56,21 @@ void mergeBatch(sbMatrix& data, const std::vector<MergeSpec>& merges, int pIdx, 
 // Sort.cpp:327-406: merge two sorted arrays
 int odd_even_merge(const sbMatrix& data1, const sbMatrix& data2, sbMatrix& res, int pIdx, Sh3Evaluator& eval,
                    Sh3Runtime& runtime);
+// How a level of odd_even_multi_merge runs its pairwise merges: Batched
+// (default) as one batch, every round of the level one cmp_swap evaluation
+// over all of its merges; Sequential one merge after the other, as the
+// reference's loop calls odd_even_merge (Sort.cpp:423-429) -- the same
+// revealed result, and the reference's own order of randomness draws (so the
+// reference's shares), at one evaluation per merge and round.
+enum class MergeOrder { Batched, Sequential };
 // Sort.cpp:413-437: merge k sorted arrays pairwise, level by level (odd k:
-// the last two first). Every level's pairwise merges form one batch.
+// the last two first).
 int odd_even_multi_merge(std::vector<sbMatrix>& data, sbMatrix& sorted, int pIdx, Sh3Evaluator& eval,
-                         Sh3Runtime& runtime);
+                         Sh3Runtime& runtime, MergeOrder order = MergeOrder::Batched);
 // The same over one array holding the lists back to back (list k has lens[k]
 // rows): no per-list allocations, for many lists.
 int odd_even_multi_merge(const sbMatrix& flat, const std::vector<u64>& lens, sbMatrix& sorted, int pIdx,
-                         Sh3Evaluator& eval, Sh3Runtime& runtime);
+                         Sh3Evaluator& eval, Sh3Runtime& runtime, MergeOrder order = MergeOrder::Batched);
 // Odd-even merge sort of `keys` (one 64-bit key per row): multi-merge of the
 // keys as singleton lists (the C5 workload).
 int odd_even_merge_sort(const sbMatrix& keys, sbMatrix& sorted, int pIdx, Sh3Evaluator& eval, Sh3Runtime& runtime);

@@ -289,7 +289,8 @@ int orc_sim_fetch_msb(uint32_t wires, const uint32_t* gates, uint64_t ngates, co
 // supplied cmp_swap circuit. mode 0: odd_even_multi_merge, each of the nlists
 // lists shared on its own; 1: the same over all keys shared as one matrix;
 // 2: high_dimensional_odd_even_multi_merge, lists [dim][nlists / dim] shared
-// in that order; 3: high_dimensional_odd_even_merge (nlists = 2 * dim).
+// in that order; 3: high_dimensional_odd_even_merge (nlists = 2 * dim);
+// 4: mode 0 with the reference's sequential merge order.
 // out_sorted / out_shares: the merged list(s) back to back.
 int orc_sim_merge(uint32_t wires, const uint32_t* gates, uint64_t ngates, const uint32_t* levels, uint64_t nlevels,
                   const uint32_t* inWires, const uint32_t* inSizes, uint64_t nin, const uint32_t* outWires,
@@ -302,7 +303,7 @@ int orc_sim_merge(uint32_t wires, const uint32_t* gates, uint64_t ngates, const 
         u64 total = 0;
         for (u64 k = 0; k < nlists; ++k) total += lens[k];
         Shared res;
-        if (mode == 0 || mode == 1) {
+        if (mode == 0 || mode == 1 || mode == 4) {
             Shared flat;
             if (mode == 1) {
                 flat = shareBin(enc, 0, toMat(keys, total, 1));
@@ -317,7 +318,7 @@ int orc_sim_merge(uint32_t wires, const uint32_t* gates, uint64_t ngates, const 
                     off += lens[k];
                 }
             }
-            res = multiMerge(ev, c, flat, std::vector<u64>(lens, lens + nlists));
+            res = multiMerge(ev, c, flat, std::vector<u64>(lens, lens + nlists), mode == 4);
         } else if (mode == 2 || mode == 3) {
             if (!dim || nlists % dim) throw std::runtime_error("nlists must be a multiple of dim");
             const u64 k = nlists / dim;

@@ -272,7 +272,10 @@ struct MergeSpec { u64 offA, lenA, lenB; };  // lists adjacent in `data`
 std::vector<std::pair<u64, u64>> mergeRounds(u64 length);
 void mergeBatch(std::array<Party, 3>& ev, const Circuit& cmpSwap, Shared& data, const std::vector<MergeSpec>& ms);
 // odd_even_multi_merge over lists stored back to back (Sort.cpp:413-437)
-Shared multiMerge(std::array<Party, 3>& ev, const Circuit& cmpSwap, const Shared& flat, std::vector<u64> lens);
+// sequential: a level's pairwise merges one after the other (the reference's
+// loop, Sort.cpp:423-429) instead of as one batch
+Shared multiMerge(std::array<Party, 3>& ev, const Circuit& cmpSwap, const Shared& flat, std::vector<u64> lens,
+                  bool sequential = false);
 // high_dimensional_odd_even_multi_merge (Sort.cpp:585-628): data[dim][k]
 std::vector<Shared> hdMultiMerge(std::array<Party, 3>& ev, const Circuit& cmpSwap,
                                  std::vector<std::vector<Shared>> data);

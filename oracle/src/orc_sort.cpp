@@ -140,7 +140,8 @@ void mergeBatch(std::array<Party, 3>& ev, const Circuit& cir, Shared& data, cons
                     data[p].s[s].v[ms[m].offA + i] = res[p].s[s].v[base[m] + i];
 }
 
-Shared multiMerge(std::array<Party, 3>& ev, const Circuit& cir, const Shared& flat, std::vector<u64> lens) {
+Shared multiMerge(std::array<Party, 3>& ev, const Circuit& cir, const Shared& flat, std::vector<u64> lens,
+                  bool sequential) {
     Shared cur = flat;
     // Sort.cpp:413-437
     while (lens.size() != 1) {
@@ -158,7 +159,10 @@ Shared multiMerge(std::array<Party, 3>& ev, const Circuit& cir, const Shared& fl
                 ms.push_back(MergeSpec{off[i], lens[i], lens[i + 1]});
                 next.push_back(lens[i] + lens[i + 1]);
             }
-            mergeBatch(ev, cir, cur, ms);
+            if (sequential)
+                for (const MergeSpec& m : ms) mergeBatch(ev, cir, cur, {m});
+            else
+                mergeBatch(ev, cir, cur, ms);
             lens = next;
         }
     }

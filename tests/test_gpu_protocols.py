@@ -124,6 +124,9 @@ MERGE_CASES = [
     (2, 2, [4, 2, 3, 5, 1, 4]),       # 2 x 3 lists (odd k)
     (3, 4, [8] * 8),                  # high_dimensional_odd_even_merge, 4 dims
     (3, 2, [5, 9, 2, 2]),
+    (4, 0, [5, 7, 8, 3]),             # the reference's sequential merge order (MergeOrder::Sequential)
+    (4, 0, [100, 3, 17, 250, 9]),
+    (4, 0, [64] * 8),
 ]
 
 
@@ -137,7 +140,7 @@ def test_merge_vs_oracle(gpu, mode, dim, lens):
     p_o, sh_o = orc.sim_merge(nt.circuit("cmp_swap", 64), lists, mode, dim, with_shares=True)
     assert np.array_equal(sh_g, sh_o)
     assert np.array_equal(p_g, p_o)
-    if mode >= 2:
+    if mode in (2, 3):
         k = len(lists) // dim
         exp = np.concatenate([np.sort(np.concatenate(lists[i * k:(i + 1) * k])) for i in range(dim)])
     else:

@@ -70,13 +70,13 @@ def test_c5_round_count():
 
 @pytest.mark.parametrize("mode,dim,lens", [
     (0, 0, [8, 8]), (0, 0, [5, 7, 8, 3]), (0, 0, [100, 3, 17, 250, 9]), (1, 0, [1] * 300),
-    (2, 3, [6] * 9), (3, 2, [5, 9, 2, 2]),
+    (2, 3, [6] * 9), (3, 2, [5, 9, 2, 2]), (4, 0, [5, 7, 8, 3]), (4, 0, [100, 3, 17, 250, 9]),
 ])
 def test_oracle_merge_sorted(mode, dim, lens):
     rng = np.random.default_rng(len(lens))
     lists = [np.sort(rng.integers(-(2**62), 2**62, size=n, dtype=np.int64)) for n in lens]
     plain, sh = orc.sim_merge(nt.circuit("cmp_swap", 64), lists, mode, dim, with_shares=True)
-    if mode >= 2:
+    if mode in (2, 3):
         k = len(lists) // dim
         exp = np.concatenate([np.sort(np.concatenate(lists[i * k:(i + 1) * k])) for i in range(dim)])
     else:
@@ -84,3 +84,18 @@ def test_oracle_merge_sorted(mode, dim, lens):
     assert np.array_equal(plain, exp)
     for p in range(3):  # party p's share 1 is party p-1's share 0
         assert np.array_equal(sh[p, 1], sh[(p + 2) % 3, 0])
+
+
+def test_oracle_merge_orders():
+    """The reference's sequential order of a level's merges (Sort.cpp:423-429)
+    and the batched one reveal the same list from different randomness draws;
+    with a single merge per level (two lists) they are the same computation."""
+    rng = np.random.default_rng(7)
+    cir = nt.circuit("cmp_swap", 64)
+    lists = [np.sort(rng.integers(-(2**62), 2**62, size=n, dtype=np.int64)) for n in (5, 7, 8, 3)]
+    pb, sb = orc.sim_merge(cir, lists, 0, 0, with_shares=True)
+    ps, ss = orc.sim_merge(cir, lists, 4, 0, with_shares=True)
+    assert np.array_equal(pb, ps) and not np.array_equal(sb, ss)
+    two = lists[:2]
+    assert np.array_equal(orc.sim_merge(cir, two, 0, 0, with_shares=True)[1],
+                          orc.sim_merge(cir, two, 4, 0, with_shares=True)[1])

@@ -292,7 +292,7 @@ int aby3h_sim_shuffle(int device, int mode, const int64_t* x, uint64_t len, uint
 int aby3h_sim_merge(int device, int mode, const uint64_t* lens, uint64_t nlists, uint64_t dim, const int64_t* keys,
                     int64_t* out_sorted, int64_t* out_shares) {
     return guarded([&] {
-        if (mode < 0 || mode > 4) throw std::runtime_error("unknown merge mode");
+        if (mode < 0 || mode > 5) throw std::runtime_error("unknown merge mode");
         if (!nlists) throw std::runtime_error("no lists");
         std::vector<i64Matrix> lists;
         u64 off = 0;
@@ -301,7 +301,7 @@ int aby3h_sim_merge(int device, int mode, const uint64_t* lens, uint64_t nlists,
             off += lens[k];
         }
         const u64 total = off;
-        if ((mode == 2 || mode == 3) && (!dim || nlists % dim)) throw std::runtime_error("nlists must be a multiple of dim");
+        if ((mode == 2 || mode == 3 || mode == 5) && (!dim || nlists % dim)) throw std::runtime_error("nlists must be a multiple of dim");
         if (mode == 3 && nlists != 2 * dim) throw std::runtime_error("high_dimensional_odd_even_merge: 2 lists per dim");
         run3(device, [&](SimParty& p) {
             sbMatrix sorted;
@@ -331,8 +331,9 @@ int aby3h_sim_merge(int device, int mode, const uint64_t* lens, uint64_t nlists,
                     }
                 }
                 std::vector<sbMatrix> out;
-                if (mode == 2) {
-                    high_dimensional_odd_even_multi_merge(data, out, p.idx, p.eval, p.rt);
+                if (mode == 2 || mode == 5) {
+                    high_dimensional_odd_even_multi_merge(data, out, p.idx, p.eval, p.rt,
+                                                          mode == 5 ? MergeOrder::Sequential : MergeOrder::Batched);
                 } else {
                     std::vector<sbMatrix> d1(dim), d2(dim);
                     for (u64 i = 0; i < dim; ++i) {

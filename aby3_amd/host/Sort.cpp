@@ -343,7 +343,7 @@ int high_dimensional_odd_even_merge(std::vector<sbMatrix>& data1, std::vector<sb
 }
 
 int high_dimensional_odd_even_multi_merge(std::vector<std::vector<sbMatrix>>& data, std::vector<sbMatrix>& sorted,
-                                          int pIdx, Sh3Evaluator& eval, Sh3Runtime& runtime) {
+                                          int pIdx, Sh3Evaluator& eval, Sh3Runtime& runtime, MergeOrder order) {
     const size_t dim = data.size();
     if (!dim) {
         sorted.clear();
@@ -384,7 +384,10 @@ int high_dimensional_odd_even_multi_merge(std::vector<std::vector<sbMatrix>>& da
                 firsts.push_back(i);
                 dsts.push_back(i / 2);
             }
-            level(firsts, dsts);
+            if (order == MergeOrder::Sequential)
+                for (size_t p = 0; p < firsts.size(); ++p) level({firsts[p]}, {dsts[p]});
+            else
+                level(firsts, dsts);
             k >>= 1;
         }
     }

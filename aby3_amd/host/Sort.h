@@ -80,6 +80,7 @@ int high_dimensional_odd_even_merge(std::vector<sbMatrix>& data1, std::vector<sb
 // Sort.cpp:585-628: data[dim][k] -> sorted[dim]; every level's merges over all
 // pairs and dimensions form one batch (pair-major, then dimension).
 int high_dimensional_odd_even_multi_merge(std::vector<std::vector<sbMatrix>>& data, std::vector<sbMatrix>& sorted,
-                                          int pIdx, Sh3Evaluator& eval, Sh3Runtime& runtime);
+                                          int pIdx, Sh3Evaluator& eval, Sh3Runtime& runtime,
+                                          MergeOrder order = MergeOrder::Batched);
 
 }  // namespace aby3

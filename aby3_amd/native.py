@@ -486,8 +486,8 @@ class sim:
         """The merge network (aby3h_sim_merge): mode 0 odd_even_multi_merge of
         separately shared lists, 1 the flat form (singletons: the sort),
         2 high_dimensional_odd_even_multi_merge (lists [dim][k], flattened),
-        3 high_dimensional_odd_even_merge, 4 mode 0 in the reference's
-        sequential merge order. Returns the revealed result, and
+        3 high_dimensional_odd_even_merge, 4 / 5 mode 0 / 2 in the
+        reference's sequential merge order. Returns the revealed result, and
         with shares=True also every party's shares [3][2][n]."""
         np = cls._np()
         lens = np.asarray([len(x) for x in lists], np.uint64)

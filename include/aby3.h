@@ -146,7 +146,7 @@ int aby3h_sim_cipher_gt(int device, const int64_t* a, const int64_t* b, uint64_t
  *        (all lists of length 1: odd_even_merge_sort);
  * mode 2 high_dimensional_odd_even_multi_merge, lists [dim][nlists / dim];
  * mode 3 high_dimensional_odd_even_merge (nlists = 2 * dim);
- * mode 4 mode 0 in the reference's sequential merge order (MergeOrder).
+ * mode 4 / 5 mode 0 / 2 in the reference's sequential merge order (MergeOrder).
  * out_sorted: the revealed merged list(s) back to back; out_shares
  * [party][share][total] of the same (either may be NULL). */
 int aby3h_sim_merge(int device, int mode, const uint64_t* lens, uint64_t nlists, uint64_t dim, const int64_t* keys,

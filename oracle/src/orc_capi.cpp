@@ -290,7 +290,7 @@ int orc_sim_fetch_msb(uint32_t wires, const uint32_t* gates, uint64_t ngates, co
 // lists shared on its own; 1: the same over all keys shared as one matrix;
 // 2: high_dimensional_odd_even_multi_merge, lists [dim][nlists / dim] shared
 // in that order; 3: high_dimensional_odd_even_merge (nlists = 2 * dim);
-// 4: mode 0 with the reference's sequential merge order.
+// 4 / 5: mode 0 / 2 with the reference's sequential merge order.
 // out_sorted / out_shares: the merged list(s) back to back.
 int orc_sim_merge(uint32_t wires, const uint32_t* gates, uint64_t ngates, const uint32_t* levels, uint64_t nlevels,
                   const uint32_t* inWires, const uint32_t* inSizes, uint64_t nin, const uint32_t* outWires,
@@ -319,7 +319,7 @@ int orc_sim_merge(uint32_t wires, const uint32_t* gates, uint64_t ngates, const 
                 }
             }
             res = multiMerge(ev, c, flat, std::vector<u64>(lens, lens + nlists), mode == 4);
-        } else if (mode == 2 || mode == 3) {
+        } else if (mode == 2 || mode == 3 || mode == 5) {
             if (!dim || nlists % dim) throw std::runtime_error("nlists must be a multiple of dim");
             const u64 k = nlists / dim;
             if (mode == 3 && k != 2) throw std::runtime_error("high_dimensional_odd_even_merge takes two lists per dim");
@@ -330,7 +330,7 @@ int orc_sim_merge(uint32_t wires, const uint32_t* gates, uint64_t ngates, const 
                     data[i][j] = shareBin(enc, 0, toMat(keys + off, lens[li], 1));
                     off += lens[li];
                 }
-            auto sorted = hdMultiMerge(ev, c, data);
+            auto sorted = hdMultiMerge(ev, c, data, mode == 5);
             for (int p = 0; p < 3; ++p) res[p] = SMat(total, 1);
             off = 0;
             for (auto& x : sorted) {

@@ -277,8 +277,9 @@ void mergeBatch(std::array<Party, 3>& ev, const Circuit& cmpSwap, Shared& data, 
 Shared multiMerge(std::array<Party, 3>& ev, const Circuit& cmpSwap, const Shared& flat, std::vector<u64> lens,
                   bool sequential = false);
 // high_dimensional_odd_even_multi_merge (Sort.cpp:585-628): data[dim][k]
+// (sequential: a level's pairs one after the other, the reference's loop)
 std::vector<Shared> hdMultiMerge(std::array<Party, 3>& ev, const Circuit& cmpSwap,
-                                 std::vector<std::vector<Shared>> data);
+                                 std::vector<std::vector<Shared>> data, bool sequential = false);
 
 }  // namespace orc
 

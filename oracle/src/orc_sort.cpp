@@ -169,7 +169,8 @@ Shared multiMerge(std::array<Party, 3>& ev, const Circuit& cir, const Shared& fl
     return cur;
 }
 
-std::vector<Shared> hdMultiMerge(std::array<Party, 3>& ev, const Circuit& cir, std::vector<std::vector<Shared>> data) {
+std::vector<Shared> hdMultiMerge(std::array<Party, 3>& ev, const Circuit& cir, std::vector<std::vector<Shared>> data,
+                                 bool sequential) {
     const size_t dim = data.size();
     size_t k = data[0].size();
     // one level: merges (data[i][a], data[i][a + 1]), pair-major then dimension
@@ -208,7 +209,10 @@ std::vector<Shared> hdMultiMerge(std::array<Party, 3>& ev, const Circuit& cir, s
                 firsts.push_back(i);
                 dsts.push_back(i / 2);
             }
-            level(firsts, dsts);
+            if (sequential)
+                for (size_t p = 0; p < firsts.size(); ++p) level({firsts[p]}, {dsts[p]});
+            else
+                level(firsts, dsts);
             k >>= 1;
         }
     }

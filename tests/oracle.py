@@ -176,8 +176,8 @@ def sim_merge(cir, lists, mode: int = 0, dim: int = 0, with_shares: bool = False
     """The batched merge network (orc_sim_merge): mode 0 odd_even_multi_merge
     of separately shared lists, 1 all keys shared as one matrix, 2
     high_dimensional_odd_even_multi_merge ([dim][k] lists, flattened), 3
-    high_dimensional_odd_even_merge, 4 mode 0 in the reference's sequential
-    merge order. cir: the cmp_swap(64) circuit."""
+    high_dimensional_odd_even_merge, 4 / 5 mode 0 / 2 in the reference's
+    sequential merge order. cir: the cmp_swap(64) circuit."""
     args, keep = _cir_args(cir)
     lens = np.asarray([len(x) for x in lists], dtype=np.uint64)
     keys = np.ascontiguousarray(np.concatenate([np.asarray(x, dtype=np.int64) for x in lists]))

@@ -127,6 +127,8 @@ MERGE_CASES = [
     (4, 0, [5, 7, 8, 3]),             # the reference's sequential merge order (MergeOrder::Sequential)
     (4, 0, [100, 3, 17, 250, 9]),
     (4, 0, [64] * 8),
+    (5, 3, [16] * 12),                # high-dimensional, sequential order
+    (5, 2, [4, 2, 3, 5, 1, 4]),
 ]
 
 
@@ -140,7 +142,7 @@ def test_merge_vs_oracle(gpu, mode, dim, lens):
     p_o, sh_o = orc.sim_merge(nt.circuit("cmp_swap", 64), lists, mode, dim, with_shares=True)
     assert np.array_equal(sh_g, sh_o)
     assert np.array_equal(p_g, p_o)
-    if mode in (2, 3):
+    if mode in (2, 3, 5):
         k = len(lists) // dim
         exp = np.concatenate([np.sort(np.concatenate(lists[i * k:(i + 1) * k])) for i in range(dim)])
     else:

@@ -71,12 +71,13 @@ def test_c5_round_count():
 @pytest.mark.parametrize("mode,dim,lens", [
     (0, 0, [8, 8]), (0, 0, [5, 7, 8, 3]), (0, 0, [100, 3, 17, 250, 9]), (1, 0, [1] * 300),
     (2, 3, [6] * 9), (3, 2, [5, 9, 2, 2]), (4, 0, [5, 7, 8, 3]), (4, 0, [100, 3, 17, 250, 9]),
+    (5, 3, [6] * 12),
 ])
 def test_oracle_merge_sorted(mode, dim, lens):
     rng = np.random.default_rng(len(lens))
     lists = [np.sort(rng.integers(-(2**62), 2**62, size=n, dtype=np.int64)) for n in lens]
     plain, sh = orc.sim_merge(nt.circuit("cmp_swap", 64), lists, mode, dim, with_shares=True)
-    if mode in (2, 3):
+    if mode in (2, 3, 5):
         k = len(lists) // dim
         exp = np.concatenate([np.sort(np.concatenate(lists[i * k:(i + 1) * k])) for i in range(dim)])
     else:

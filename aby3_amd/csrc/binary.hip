@@ -81,6 +81,9 @@ __global__ void __launch_bounds__(kGateBlock) k_bin_gates(const aby3g_gate* __re
 // between batches: a gate only ever reads words of its own rows, so the
 // per-workgroup barrier orders every dependency of the level.
 constexpr u32 kLevelWords = 32;
+// launches of fewer workgroups than this take the 32-slot form (more gate
+// parallelism per workgroup), larger ones the 8-slot form
+constexpr u32 kLevelSmallMaxWgs = 128;
 
 // Operands of one gate on one word, loaded ahead of its evaluation so that a
 // slot can have several independent gates' loads in flight.
@@ -644,7 +647,7 @@ int aby3g_bin_level_hs(const aby3g_gate* gates, const uint32_t* recv_rows, const
         // with hand-offs the send rows are stored write-through and the
         // received ones read past L1 (both ways, so one instantiation covers
         // a launch that only waits or only posts)
-        if (wgs < 128) {
+        if (wgs < kLevelSmallMaxWgs) {
             if (hs)
                 launch(PROBE_BINARY, k_bin_level<32, true>, dim3(wgs), dim3(32 * 32), 0, S(stream), gates, rrows,
                        batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp);
@@ -659,6 +662,19 @@ int aby3g_bin_level_hs(const aby3g_gate* gates, const uint32_t* recv_rows, const
                 launch(PROBE_BINARY, k_bin_level<8, false>, dim3(wgs), dim3(8 * 32), 0, S(stream), gates, rrows,
                        batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp);
         }
+    });
+}
+
+int aby3g_bin_level_residency(int* cus, int* per_cu_small, int* per_cu_large, int* small_max_wgs) {
+    return guarded([&] {
+        ABY3G_REQUIRE(cus && per_cu_small && per_cu_large && small_max_wgs, "null argument");
+        const int dev = current_device();
+        ABY3G_CHECK_HIP(hipDeviceGetAttribute(cus, hipDeviceAttributeMultiprocessorCount, dev));
+        ABY3G_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            per_cu_small, reinterpret_cast<const void*>(k_bin_level<32, true>), 32 * 32, 0));
+        ABY3G_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            per_cu_large, reinterpret_cast<const void*>(k_bin_level<8, true>), 8 * 32, 0));
+        *small_max_wgs = (int)kLevelSmallMaxWgs;
     });
 }
 

@@ -420,33 +420,56 @@ __device__ __forceinline__ void gate_local(u32 type, u64 x0, u64 x1, u64 y0, u64
 // bypass its CU's L1 -- the R1 form of the guides' inter-workgroup recipe,
 // no release or acquire fence. A wait gives up after kHandoffTimeoutTicks of
 // the 100 MHz wall clock (a peer stream that cannot progress, e.g. two
-// streams sharing a hardware queue), sets the device's status word (pinned
-// host memory, a plain system-scope store) and lets every later wait on the
-// device give up at once: the results are then wrong, never hung, and the
-// host raises an error (aby3g_handoff_status).
+// streams sharing a hardware queue), adds 1 to the device's timeout counter
+// (pinned host memory, a system-scope atomic) and lets every wait enqueued
+// before the host saw that count give up at once (each wait carries the
+// count at its enqueue, `status0`): the results are then wrong, never hung,
+// and the host raises an error (aby3g_handoff_status: callers compare the
+// count before and after their run, so concurrent callers on one device
+// cannot clear each other's timeout).
 typedef __attribute__((address_space(1))) u64 gu64;
 typedef __attribute__((address_space(1))) u32 gu32;
 typedef u32 v4u32 __attribute__((ext_vector_type(4)));
-constexpr u64 kHandoffTimeoutTicks = 500000000ull;  // 5 s
+constexpr u64 kHandoffTimeoutTicks = 500000000ull;  // 5 s (default; aby3g_set_handoff_timeout_us)
 constexpr u64 kHandoffRows = ABY3G_HANDOFF_ROWS;
 
-// the current device's hand-off status word (pinned host memory, mapped):
-// nonzero once a wait timed out
+// the current device's hand-off timeout counter (pinned host memory, mapped)
 u32* handoff_status_word();
+// the wait limit kernels launched now use, in wall-clock ticks
+u64 handoff_timeout_ticks();
+
+// What a waiting kernel needs to give up: the counter, its value when the
+// wait was enqueued, and the limit.
+struct HsStatus {
+    u32* word;
+    u32 base;
+    u64 limit;
+};
+inline HsStatus hs_status() {
+    u32* w = handoff_status_word();
+    return HsStatus{w, *(volatile u32*)w, handoff_timeout_ticks()};
+}
+// true once any wait on the device has timed out since this wait was enqueued
+__device__ __forceinline__ bool hs_failed(const HsStatus& s) {
+    return __hip_atomic_load(s.word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != s.base;
+}
+__device__ __forceinline__ void hs_fail(const HsStatus& s) {
+    __hip_atomic_fetch_add(s.word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 struct HsWait {
     const u64* flags;  // null: nothing to wait for
     u64 seq;
     u64* ticks;        // optional: wall-clock ticks the first workgroup waited
-    u32* status;
+    HsStatus status;
 };
 struct HsPost {
     u64* flags;  // null: nothing to publish
     u64 seq;
 };
 inline HsWait hs_wait_arg(const aby3g_handoff* h) {
-    if (!h || !h->flags) return HsWait{nullptr, 0, nullptr, nullptr};
-    return HsWait{h->flags, h->seq, h->wait_ticks, handoff_status_word()};
+    if (!h || !h->flags) return HsWait{nullptr, 0, nullptr, HsStatus{nullptr, 0, 0}};
+    return HsWait{h->flags, h->seq, h->wait_ticks, hs_status()};
 }
 inline HsPost hs_post_arg(const aby3g_handoff* h) {
     if (!h || !h->flags) return HsPost{nullptr, 0};
@@ -466,12 +489,12 @@ __device__ __forceinline__ bool hs_wait(const HsWait& w, u64 c0, u64 c1) {
                                                   __HIP_MEMORY_SCOPE_AGENT) < w.seq;) {
                 __builtin_amdgcn_s_sleep(1);
                 if ((++spins & 63) == 0) {
-                    if (__hip_atomic_load(w.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+                    if (hs_failed(w.status)) {
                         good = 0;
                         break;
                     }
-                    if (wall_clock64() - t0 > kHandoffTimeoutTicks) {
-                        __hip_atomic_store(w.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (wall_clock64() - t0 > w.status.limit) {
+                        hs_fail(w.status);
                         good = 0;
                         break;
                     }

@@ -155,7 +155,7 @@ __device__ __forceinline__ u64 stream_word(const u32* T, const u32* k, u64 j) {
 
 // waits for a neighbour's flag `f` (one lane polls; the workgroup leaves
 // together); false after a timeout
-__device__ __forceinline__ bool lr_wait(const u64* box, u32 f, u64 epoch, u64* ticks, u32* status) {
+__device__ __forceinline__ bool lr_wait(const u64* box, u32 f, u64 epoch, u64* ticks, const HsStatus& status) {
     return hs_wait(HsWait{box, epoch, ticks, status}, f, f + 1);
 }
 // publishes this party's flag `f` after every wave's write-through stores
@@ -168,31 +168,51 @@ __device__ __forceinline__ void lr_post(u64* box, u32 f, u64 epoch) { hs_post(Hs
 // carry this epoch -- no drain, no flag and no second round trip for the
 // payload. The mailbox regions alternate by epoch parity, so a word left from
 // two epochs before never matches.
-__device__ __forceinline__ void msg_put(u64* m, u64 i, u64 v, u32 tag) {
-    hs_store(m + 2 * i, ((u64)tag << 32) | (u32)v);
-    hs_store(m + 2 * i + 1, ((u64)tag << 32) | (u32)(v >> 32));
+// Peers on this device (in this process or another, through an IPC mapping)
+// share its L2s: agent-scope write-through stores and L1-bypassing loads.
+// Peers on other GPUs read this party's mailbox over xGMI: system scope
+// (aby3g_lr_iter.sys_scope), the mailboxes allocated uncached.
+struct MsgTag {
+    u32 tag;
+    bool sys;
+};
+__device__ __forceinline__ void msg_store(u64* p, u64 v, bool sys) {
+    if (sys)
+        __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else
+        hs_store(p, v);
 }
-// A thread's reads of one receive loop: after a timeout or an abort (status
-// set) it stops polling and the workgroup leaves together at msg_done.
+__device__ __forceinline__ u64 msg_load(const u64* p, bool sys) {
+    if (sys) return __hip_atomic_load((const gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return hs_load(p);
+}
+__device__ __forceinline__ void msg_put(u64* m, u64 i, u64 v, MsgTag tag) {
+    msg_store(m + 2 * i, ((u64)tag.tag << 32) | (u32)v, tag.sys);
+    msg_store(m + 2 * i + 1, ((u64)tag.tag << 32) | (u32)(v >> 32), tag.sys);
+}
+// A thread's reads of one receive loop: after a timeout or an abort (another
+// wait timed out) it stops polling and the workgroup leaves together at
+// msg_done.
 struct MsgWait {
     u32 tag;
-    u32* status;
+    bool sys;
+    HsStatus status;
     u64 t0;
     bool ok;
 };
-__device__ __forceinline__ MsgWait msg_begin(u64 epoch, u32* status) {
-    return MsgWait{(u32)epoch, status, (u64)wall_clock64(), true};
+__device__ __forceinline__ MsgWait msg_begin(MsgTag tag, const HsStatus& status) {
+    return MsgWait{tag.tag, tag.sys, status, (u64)wall_clock64(), true};
 }
 __device__ __forceinline__ u64 msg_get(const u64* m, u64 i, MsgWait& w) {
     if (!w.ok) return 0;
     for (u32 spins = 0;;) {
-        const u64 a = hs_load(m + 2 * i), b = hs_load(m + 2 * i + 1);
+        const u64 a = msg_load(m + 2 * i, w.sys), b = msg_load(m + 2 * i + 1, w.sys);
         if ((u32)(a >> 32) == w.tag && (u32)(b >> 32) == w.tag) return (u64)(u32)a | ((u64)(u32)b << 32);
         __builtin_amdgcn_s_sleep(1);
         if ((++spins & 63) == 0) {
-            if (__hip_atomic_load(w.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
-            if (wall_clock64() - w.t0 > kHandoffTimeoutTicks) {
-                __hip_atomic_store(w.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (hs_failed(w.status)) break;
+            if (wall_clock64() - w.t0 > w.status.limit) {
+                hs_fail(w.status);
                 break;
             }
         }
@@ -219,7 +239,7 @@ __device__ __forceinline__ bool msg_done(const MsgWait& w, u32* bad, u64* ticks)
 // next stream's, [256, 512) the prev stream's, one block each, into tw (512
 // u64 of LDS), then the tile's elements are formed from it.
 __device__ __forceinline__ void lr_trunc_pair(const u32* T, const u32* keys, u64 nw0, u64 pw0, u32 n, u32 d,
-                                              const u64* prod, u64* out, u32 tag, u64* own, u64* c0, u64* c1,
+                                              const u64* prod, u64* out, MsgTag tag, u64* own, u64* c0, u64* c1,
                                               u64* tw) {
     const u32 tid = threadIdx.x, half = tid >> 8, t = tid & 255;
     for (u32 i0 = 0; i0 < n; i0 += 256) {
@@ -283,7 +303,7 @@ __device__ __forceinline__ void lr_arrive(u64* box, u32 f) {
 // A wave per row (rows wave, wave + 8, ...), lanes over k pairs (16-byte
 // loads), kLrHelperUnroll rows of a wave in flight.
 constexpr u32 kLrHelperUnroll = 4;
-__device__ __forceinline__ void lr_helper(const aby3g_lr_iter& it, u32* status, u64* part) {
+__device__ __forceinline__ void lr_helper(const aby3g_lr_iter& it, const HsStatus& status, u64* part) {
     const u32 B = it.B, d = it.d, G = lr_helpers(B), h = blockIdx.x - 1;
     const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const Layout L(B, d, it.cir);
@@ -344,8 +364,7 @@ __device__ __forceinline__ void lr_helper(const aby3g_lr_iter& it, u32* status, 
         const u64 t0 = wall_clock64();
         for (u32 spins = 0; __hip_atomic_load((const gu64*)box + F_P3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ep;) {
             __builtin_amdgcn_s_sleep(32);
-            if ((++spins & 15) == 0 && (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
-                                        wall_clock64() - t0 > kHandoffTimeoutTicks))
+            if ((++spins & 15) == 0 && (hs_failed(status) || wall_clock64() - t0 > status.limit))
                 break;  // the close wait below gives up too
         }
     }
@@ -408,7 +427,7 @@ __device__ __forceinline__ void lr_stamp(u64* ticks, u32 s) {
 // access waits for the wave's outstanding global stores too -- in the levels,
 // for the write-through AND shares just sent (~1 us a level).
 template <bool kLds>
-__device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it, const LrKeys& K, u32* status,
+__device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it, const LrKeys& K, const HsStatus& status,
                                          u32* lds, u32* keys, u64* dyn, u64* tw) {
     u64* const PT = it.phase_ticks;
     lr_stamp(PT, 0);
@@ -505,14 +524,14 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
     prod = sc + L.hprod;
     __syncthreads();
     lr_stamp(PT, 2);
-    const u32 tag = (u32)ep;
+    const MsgTag tag{(u32)ep, it.sys_scope != 0};
     __shared__ u32 msgBad;
     if (tid == 0) msgBad = 0;
     lr_trunc_pair(T, keys, it.t1_next_off / 8, it.t1_prev_off / 8, B, it.D, prod, my + L.z1, tag, sc + L.z1own, xw0,
                   xw1, tw);
     lr_stamp(PT, 3);
     {
-        MsgWait mw = msg_begin(ep, status);
+        MsgWait mw = msg_begin(tag, status);
         if (p < 2) lr_trunc_finalize(nx + L.z1, pv + L.z1, sc + L.z1own, B, it.D, p == 0 ? xw0 : xw1, mw);
         if (!msg_done(mw, &msgBad, p < 2 ? ticks : nullptr)) return;
     }
@@ -523,7 +542,7 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
     if (p == 0)
         for (u32 i = tid; i < B; i += kLrThreads) msg_put(my + L.v, i, xw0[i] + xw1[i], tag);
     const u64* vrecv = pv + L.v;  // P1
-    MsgWait vw = msg_begin(ep, status);
+    MsgWait vw = msg_begin(tag, status);
     // inputs straight into the wires (setTwoInputSharing): source s in
     // {aa_0, aa_1, b}, share h; a wave transposes the bits of its 64 rows
     const u64 WS = (u64)cir.wires * W;  // share stride
@@ -554,7 +573,7 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
         if (lv > 0 && levelsL[lv - 1].nand) {
             const aby3g_lr_level& pl = levelsL[lv - 1];
             const u64* grows = pv + L.lvl + 2 * (u64)pl.and_wire_off * W;
-            MsgWait mw = msg_begin(ep, status);
+            MsgWait mw = msg_begin(tag, status);
             for (u32 q = tid; q < pl.nand * W32 && mw.ok; q += kLrThreads) {
                 const u64 v = msg_get(grows, q, mw);
                 const u32 j = q / W32, w = q - j * W32;
@@ -664,7 +683,7 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
             }
         }
         if (tid == 0) hs_store(box + F_P3, ep);  // sends done: the helpers poll for err closely from here
-        MsgWait mw = msg_begin(ep, status);
+        MsgWait mw = msg_begin(tag, status);
         for (u32 i = tid; i < B; i += kLrThreads) {
             g0[i] = msg_get(nx + L.pmb, i, mw);  // P1's share of the product
             g1[i] = msg_get(pv + L.pmb, i, mw);  // P2's
@@ -692,7 +711,7 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
             }
         }
         if (tid == 0) hs_store(box + F_P3, ep);  // sends done: the helpers poll for err closely from here
-        MsgWait mw = msg_begin(ep, status);
+        MsgWait mw = msg_begin(tag, status);
         for (u32 i = tid; i < B; i += kLrThreads) {
             // c0 = recv(P2's send, P0's help; choice b1) + recv(P0's send, P2's help; choice b0)
             const u64 m1 = msg_get(nx + L.ots, 2 * i + (r1b[i] & 1), mw) ^ msg_get(pv + L.oth, i, mw);
@@ -737,7 +756,7 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
             }
         }
         if (tid == 0) hs_store(box + F_P3, ep);  // sends done: the helpers poll for err closely from here
-        MsgWait mw = msg_begin(ep, status);
+        MsgWait mw = msg_begin(tag, status);
         for (u32 i = tid; i < B; i += kLrThreads) {
             fr1[i] = msg_get(pv + L.otc, i, mw);
             g1[i] = msg_get(nx + L.pmb, 2 * i + (r2b[i] & 1), mw) ^ msg_get(pv + L.pma, i, mw);
@@ -775,7 +794,7 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
     lr_trunc_pair(T, keys, it.t2_next_off / 8, it.t2_prev_off / 8, d, sh2, prod, my + L.z2, tag, sc + L.z2own, u0, u1, tw);
     lr_stamp(PT, 10);
     {
-        MsgWait mw = msg_begin(ep, status);
+        MsgWait mw = msg_begin(tag, status);
         if (p < 2) lr_trunc_finalize(nx + L.z2, pv + L.z2, sc + L.z2own, d, sh2, p == 0 ? u0 : u1, mw);
         if (!msg_done(mw, &msgBad, p < 2 ? ticks : nullptr)) return;
     }
@@ -787,7 +806,7 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
 }
 
 __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict__ T0g, aby3g_lr_iter it, LrKeys K,
-                                                           u32* status, int memInLds) {
+                                                           HsStatus status, int memInLds) {
     __shared__ u32 lds[kAesLdsWords];
     __shared__ u64 part[kLrThreads];
     __shared__ __attribute__((aligned(16))) u32 keys[kLrKeys * kKeyWords];
@@ -851,7 +870,7 @@ int aby3g_lr_iteration(const aby3g_lr_iter* it, aby3g_stream stream) {
         ABY3G_REQUIRE(attr || !inLds, "could not raise the fused iteration's dynamic LDS limit");
         // block 0 runs the protocol, blocks 1..G help with the dataset products
         launch(PROBE_OTHER, k_lr_iter, dim3(1 + lr_helpers(it->B)), dim3(kLrThreads), inLds ? dynBytes : 0, S(stream),
-               aes_table(), *it, K, handoff_status_word(), inLds);
+               aes_table(), *it, K, hs_status(), inLds);
     });
 }
 

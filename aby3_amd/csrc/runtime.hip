@@ -1,6 +1,7 @@
 // Runtime plumbing of the C-ABI: errors, device memory, streams, events, the
 // kernel-timing probe, and the host half of AES (key schedule, T-table).
 #include "common.h"
+#include <atomic>
 #include <cstring>
 #include <mutex>
 #include <map>
@@ -109,6 +110,9 @@ u32* handoff_status_word() {
     g_status_dev[dev] = (u32*)p;
     return (u32*)p;
 }
+
+static std::atomic<u64> g_handoff_timeout_ticks{kHandoffTimeoutTicks};
+u64 handoff_timeout_ticks() { return g_handoff_timeout_ticks.load(std::memory_order_relaxed); }
 
 void set_error(const std::string& msg) { t_err = msg; }
 thread_local int t_device = -1;
@@ -224,6 +228,12 @@ int aby3g_malloc(void** ptr, size_t bytes) {
         if (e != hipSuccess) throw Error{ABY3G_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e)};
     });
 }
+int aby3g_malloc_uncached(void** ptr, size_t bytes) {
+    return guarded([&] {
+        hipError_t e = hipExtMallocWithFlags(ptr, bytes ? bytes : 16, hipDeviceMallocUncached);
+        if (e != hipSuccess) throw Error{ABY3G_ENOMEM, std::string("hipExtMallocWithFlags: ") + hipGetErrorString(e)};
+    });
+}
 int aby3g_free(void* ptr) {
     return guarded([&] { ABY3G_CHECK_HIP(hipFree(ptr)); });
 }
@@ -254,15 +264,32 @@ int aby3g_memset(void* dst, int value, size_t bytes, aby3g_stream stream) {
         if (bytes) ABY3G_CHECK_HIP(hipMemsetAsync(dst, value, bytes, S(stream)));
     });
 }
+static std::mutex g_stream_mu;
+static std::map<hipStream_t, int> g_streams;  // live streams -> device
 int aby3g_stream_create(aby3g_stream* stream) {
     return guarded([&] {
         hipStream_t s;
         ABY3G_CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
         *stream = s;
+        std::lock_guard<std::mutex> lk(g_stream_mu);
+        g_streams[s] = current_device();
     });
 }
 int aby3g_stream_destroy(aby3g_stream stream) {
-    return guarded([&] { ABY3G_CHECK_HIP(hipStreamDestroy(S(stream))); });
+    return guarded([&] {
+        ABY3G_CHECK_HIP(hipStreamDestroy(S(stream)));
+        std::lock_guard<std::mutex> lk(g_stream_mu);
+        g_streams.erase(S(stream));
+    });
+}
+int aby3g_stream_count(int device, int* n) {
+    return guarded([&] {
+        ABY3G_REQUIRE(n != nullptr, "null argument");
+        std::lock_guard<std::mutex> lk(g_stream_mu);
+        int c = 0;
+        for (const auto& e : g_streams) c += e.second == device;
+        *n = c;
+    });
 }
 int aby3g_stream_sync(aby3g_stream stream) {
     return guarded([&] { ABY3G_CHECK_HIP(hipStreamSynchronize(S(stream))); });
@@ -330,9 +357,13 @@ int aby3g_stream_wait_value(aby3g_stream stream, uint64_t* word, uint64_t value)
 int aby3g_handoff_status(uint32_t* timeouts) {
     return guarded([&] {
         ABY3G_REQUIRE(timeouts != nullptr, "null argument");
-        volatile u32* w = handoff_status_word();
-        *timeouts = *w;
-        if (*timeouts) *w = 0;
+        *timeouts = *(volatile u32*)handoff_status_word();
+    });
+}
+int aby3g_set_handoff_timeout_us(uint64_t us) {
+    return guarded([&] {
+        ABY3G_REQUIRE(us >= 1 && us <= 60000000ull, "timeout must be 1 us .. 60 s");
+        g_handoff_timeout_ticks.store(us * 100, std::memory_order_relaxed);  // 100 MHz wall clock
     });
 }
 
@@ -365,6 +396,14 @@ int aby3g_host_register(void* host, size_t bytes, void** dev) {
 }
 int aby3g_host_unregister(void* host) {
     return guarded([&] { ABY3G_CHECK_HIP(hipHostUnregister(host)); });
+}
+int aby3g_device_uuid(int device, uint8_t uuid[16]) {
+    return guarded([&] {
+        ABY3G_REQUIRE(uuid != nullptr, "null argument");
+        hipUUID u;
+        ABY3G_CHECK_HIP(hipDeviceGetUuid(&u, device));
+        std::memcpy(uuid, u.bytes, 16);
+    });
 }
 int aby3g_enable_peer_access(int device, int peer) {
     return guarded([&] {

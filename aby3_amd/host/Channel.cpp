@@ -65,10 +65,9 @@ struct LinkSlot {
 
 // in-kernel hand-offs: messages of at most kHandoffMaxChunks chunks (128 Ki
 // rows), or of at most kHandoffChunks chunks (1 Mi rows) from a light
-// producer. Residency bound: the level kernel (94 VGPRs, 5 waves per SIMD)
-// takes one wave per SIMD per 2048-row workgroup, so two parties' consumer
-// launches of 512 workgroups spinning on 256 CUs hold 4 of the 5 slots of
-// every SIMD and the producer always finds one (binary.hip, k_bin_level).
+// producer -- and only within the device's residency rule
+// (handoffResidencyOk: with the level kernel at 94 VGPRs, 5 workgroups of the
+// large form per CU, two 512-chunk consumers hold 206 of 256 CUs on MI355X).
 constexpr u64 kHandoffMaxChunks = 64;
 constexpr u64 kHandoffChunks = 512;  // flags per direction
 // A producing launch of at most this many HBM bytes is light: its consumer's
@@ -348,7 +347,13 @@ struct Pipe {
             }
             LinkSlot& s = lslots[(size_t)k];
             if (!s.ptr) {
-                s.cap = std::max<size_t>(bytes, 64 << 10);
+                // capacities are powers of two: a slot is outgrown at most
+                // log2(largest message / 64 KiB) times, so the retired buffers
+                // behind it (kept until teardown) add up to less than its
+                // current capacity, whatever the sequence of message sizes
+                size_t cap = 64 << 10;
+                while (cap < bytes) cap <<= 1;
+                s.cap = cap;
                 GPU_CALL(aby3g_malloc(&s.ptr, s.cap));
                 GPU_CALL(aby3g_ipc_get_handle(s.ptr, &s.h));
                 ++s.gen;
@@ -578,6 +583,9 @@ aby3g_handoff Channel::handoffPost(Gpu& gpu, u64 rows, u64 producerBytes) {
         return aby3g_handoff{nullptr, 0, nullptr};
     }
     const u64 chunks = std::max<u64>(1, (rows + ABY3G_HANDOFF_ROWS - 1) / ABY3G_HANDOFF_ROWS);
+    // the residency rule first: a consumer launch that could starve its
+    // producer of slots keeps the stream hand-off
+    if (!handoffResidencyOk(handoffResidency(gpu.device()), chunks)) return aby3g_handoff{nullptr, 0, nullptr};
     // Large messages from a heavy producer keep the stream hand-off: a
     // consumer launch of many workgroups would hold its CUs spinning while the
     // producer still runs (measured slower on C3 / C5 at 512 chunks with every
@@ -592,6 +600,32 @@ bool Channel::handoffCapable(const Gpu& gpu) const {
     for (const Pipe* p : {mOut.get(), mIn.get()})
         if (!p->kernelHandoff || p->link || p->signalDevice != gpu.device()) return false;
     return true;
+}
+
+bool handoffResidencyOk(const HandoffResidency& r, u64 chunks) {
+    const int per = chunks < (u64)std::max(0, r.smallMaxWgs) ? r.perCuSmall : r.perCuLarge;
+    if (per <= 0 || r.cus <= 0 || !chunks) return false;
+    const u64 cusHeld = (chunks + (u64)per - 1) / (u64)per;
+    return 2 * cusHeld + (u64)std::max(0, r.otherSpinners) + 1 <= (u64)r.cus;
+}
+
+const HandoffResidency& handoffResidency(int device) {
+    static std::mutex mu;
+    static std::map<int, HandoffResidency> byDevice;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = byDevice.find(device);
+    if (it != byDevice.end()) return it->second;
+    HandoffResidency r;
+    GPU_CALL(aby3g_set_device(device));
+    GPU_CALL(aby3g_bin_level_residency(&r.cus, &r.perCuSmall, &r.perCuLarge, &r.smallMaxWgs));
+    // stream-operation waits can spin on every stream of the device: at most
+    // one per hardware queue of the process
+    r.otherSpinners = hwQueuesPerDevice();
+    return byDevice.emplace(device, r).first->second;
+}
+
+bool Channel::linkedConcurrent() const {
+    return mOut && mIn && mOut->link && mIn->link && !kernelsSerialized();
 }
 
 void Channel::asyncSendShared(std::shared_ptr<DeviceBuffer> buf, size_t bytes, Gpu& gpu, const aby3g_handoff& posted) {

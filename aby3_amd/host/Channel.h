@@ -89,6 +89,11 @@ public:
     // ring allows kernel hand-offs (a fused launch may then address the
     // peer's device memory and poll it).
     bool handoffCapable(const Gpu& gpu) const;
+    // Both directions are links to parties in other processes
+    // (makeProcessRing): each party's streams own their hardware queues, so a
+    // kernel may poll a peer's IPC-mapped memory while kernels run
+    // concurrently (not under a kernel-serialising profiler).
+    bool linkedConcurrent() const;
     void asyncSendShared(std::shared_ptr<DeviceBuffer> buf, size_t bytes, Gpu& gpu, const aby3g_handoff& posted);
 
     u64 bytesSent() const;
@@ -117,6 +122,28 @@ bool kernelsSerialized();
 // 4): streams beyond it share queues, and a kernel waiting in a shared queue
 // would block the work queued behind it.
 int hwQueuesPerDevice();
+
+// The in-kernel hand-off residency rule. A consumer launch's workgroups spin
+// until their chunks arrive, so the producer of a message must always find a
+// slot: at most two parties' consumer launches spin at once (a party's next
+// level waits behind its own current one on its stream, so one of the three
+// is always the producer), besides at most `otherSpinners` stream-operation
+// wait kernels (one per stream on the device). Counted in whole CUs, since
+// the dispatcher may spread a launch over every CU: a consumer of c chunks
+// (c workgroups of the small form when c < smallMaxWgs, else of the large
+// one) holds at most ceil(c / perCu) CUs' worth of its kernel's slots, and
+//     2 ceil(c / perCu) + otherSpinners + 1 <= cus
+// leaves the producer a CU.
+struct HandoffResidency {
+    int cus = 0;
+    int perCuSmall = 0, perCuLarge = 0;  // level-kernel workgroups resident per CU
+    int smallMaxWgs = 0;
+    int otherSpinners = 0;
+};
+bool handoffResidencyOk(const HandoffResidency& r, u64 chunks);
+// the current device's figures (aby3g_bin_level_residency, computed once per
+// device; otherSpinners = GPU_MAX_HW_QUEUES)
+const HandoffResidency& handoffResidency(int device);
 
 // Three in-process parties connected in a ring: result[i].mNext talks to
 // party i+1, result[i].mPrev to party i-1. With `devices` (party i runs on

@@ -301,6 +301,18 @@ void DeviceBuffer::free() {
     mBytes = 0;
 }
 
+u32 handoffTimeouts(int device) {
+    u32 n = 0;
+    GPU_CALL(aby3g_set_device(device));
+    GPU_CALL(aby3g_handoff_status(&n));
+    return n;
+}
+int liveStreams(int device) {
+    int n = 0;
+    GPU_CALL(aby3g_stream_count(device, &n));
+    return n;
+}
+
 void toDevice(void* dst, const void* src, size_t bytes, Gpu& gpu) {
     GPU_CALL(aby3g_memcpy(dst, src, bytes, 0, gpu.stream()));
     // the host source may be reused by the caller right away

@@ -178,6 +178,12 @@ private:
     std::shared_ptr<DeviceBuffer> mParent;  // views only
 };
 
+// The device's count of in-kernel hand-off timeouts so far (aby3g_handoff_status):
+// compare before and after a run.
+u32 handoffTimeouts(int device);
+// Streams of this process currently alive on `device` (aby3g_stream_count).
+int liveStreams(int device);
+
 // Convenience copies on the current Gpu's stream.
 void toDevice(void* dst, const void* src, size_t bytes, Gpu& gpu);
 void toHost(void* dst, const void* src, size_t bytes, Gpu& gpu);  // synchronizes the stream

@@ -46,6 +46,8 @@ struct Job {
     virtual void step(PartyCtx& p) = 0;
     virtual bool check(PartyCtx&) { return true; }
     virtual void info(double* out) = 0;
+    // party i's result matrix of the last step (both shares), for digests
+    virtual const SharedMat* result(int) const { return nullptr; }
     // parties seeded as aby3ML::init (aby3ML.cpp:4-17) instead of the unit tests' toBlock(c, i)
     virtual bool mlSeeds() const { return false; }
 };
@@ -110,6 +112,7 @@ struct MulJob : Job {
         o[ABY3H_INFO_MULTS_PER_STEP] = mode == MulMode::Gemm ? (double)M * N * K : (double)M * N;
         o[ABY3H_INFO_GEMM_INT8_OPS] = mode == MulMode::Gemm ? 144.0 * M * N * K : 0;
     }
+    const SharedMat* result(int i) const override { return &C[i]; }
 };
 
 // gate-kernel algorithmic bytes per padded word
@@ -150,6 +153,7 @@ struct MsbJob : Job {
         }
     }
     void step(PartyCtx& p) override { cipher_gt(p.idx, A[p.idx], B[p.idx], R[p.idx], p.eval, p.rt); }
+    const SharedMat* result(int i) const override { return &R[i]; }
     bool check(PartyCtx& p) override {
         i64Matrix r;
         p.enc.revealAll(p.rt, R[p.idx], r).get();
@@ -197,6 +201,7 @@ struct A2bJob : Job {
         cp[p.idx].init(p);
     }
     void step(PartyCtx& p) override { cp[p.idx].conv.toBinaryMatrix(p.rt, A[p.idx], R[p.idx]).get(); }
+    const SharedMat* result(int i) const override { return &R[i]; }
     bool check(PartyCtx& p) override {
         i64Matrix r;
         p.enc.revealAll(p.rt, R[p.idx], r).get();
@@ -235,6 +240,7 @@ struct BitInjJob : Job {
         cp[p.idx].init(p);
     }
     void step(PartyCtx& p) override { cp[p.idx].conv.bitInjection(p.rt, A[p.idx], R[p.idx]).get(); }
+    const SharedMat* result(int i) const override { return &R[i]; }
     bool check(PartyCtx& p) override {
         i64Matrix r;
         p.enc.revealAll(p.rt, R[p.idx], r).get();
@@ -253,27 +259,38 @@ struct BitInjJob : Job {
 // ---- C4: one logistic-regression SGD iteration ----------------------------
 // The reference's driver (main-logistic.cpp:82-140, Regression.h:249-293):
 // LogisticModelGen data, aby3ML::init seeds, getSubset mini-batches.
+// sample = 0: the mini-batches of the first kBatches iterations are drawn at
+// construction and kept resident (an iteration is the protocol alone);
+// sample = 1: every step draws its batch with getSubset inside the step
+// (DeviceBatchSampler), as SGD_Logistic's loop does (Regression.h:249-253).
 struct LrJob : Job {
     static constexpr u64 kBatches = 8192;  // mini-batches precomputed (and resident) per session
-    u64 n, d, B, D, aB;
+    u64 n, d, B, D, aB, sample;
     i64Matrix X, Y, w0;
     si64Matrix sX[3], sY[3], sW[3];
     std::unique_ptr<aby3ML> ml[3];
     SgdState st[3];
-    std::vector<u32> batches;  // [kBatches][B], getSubset order
+    std::vector<u32> batches;  // [kBatches][B], getSubset order (sample = 0)
     DeviceBuffer dbatch[3];     // the same, resident per party
+    std::unique_ptr<DeviceBatchSampler> sampler[3];  // sample = 1
     u64 iter[3] = {0, 0, 0};
-    LrJob(u64 n_, u64 d_, u64 b_, u64 D_, u64 aB_) : n(n_), d(d_), B(b_), D(D_), aB(aB_) {
+    LrJob(u64 n_, u64 d_, u64 b_, u64 D_, u64 aB_, u64 sample_)
+        : n(n_), d(d_), B(b_), D(D_), aB(aB_), sample(sample_) {
         if (!n || !d || !B || B > n) throw std::runtime_error("lr job: need 0 < batch <= rows");
         logisticModelGen(logisticModel(d), n, D, X, Y);
         w0.resize(d, 1);
-        BatchSampler sampler(n);
+        if (!sample) batches = drawBatches(kBatches);
+    }
+    // the first `iters` mini-batches of getSubset, [iters][B]
+    std::vector<u32> drawBatches(u64 iters) const {
+        BatchSampler s(n);
         std::vector<u64> b(B);
-        batches.resize(kBatches * B);
-        for (u64 t = 0; t < kBatches; ++t) {
-            sampler.next(b);
-            for (u64 i = 0; i < B; ++i) batches[t * B + i] = (u32)b[i];
+        std::vector<u32> out(iters * B);
+        for (u64 t = 0; t < iters; ++t) {
+            s.next(b);
+            for (u64 i = 0; i < B; ++i) out[t * B + i] = (u32)b[i];
         }
+        return out;
     }
     bool mlSeeds() const override { return true; }
     void setup(PartyCtx& p) override {
@@ -290,14 +307,23 @@ struct LrJob : Job {
             p.enc.remoteIntMatrix(p.rt, sW[p.idx]).get();
         }
         ml[p.idx] = std::make_unique<aby3ML>(p.rt, p.enc, p.eval, D);
-        dbatch[p.idx].reset(p.rt.gpu(), batches.size() * 4);
-        toDevice(dbatch[p.idx].data(), batches.data(), batches.size() * 4, p.rt.gpu());
+        if (sample) {
+            sampler[p.idx] = std::make_unique<DeviceBatchSampler>(p.rt.gpu(), n, B);
+        } else {
+            dbatch[p.idx].reset(p.rt.gpu(), batches.size() * 4);
+            toDevice(dbatch[p.idx].data(), batches.data(), batches.size() * 4, p.rt.gpu());
+        }
     }
     void step(PartyCtx& p) override {
         const u64 t = iter[p.idx]++;
-        if (t >= kBatches) throw std::runtime_error("lr job: more iterations than precomputed mini-batches");
-        sgdLogisticStep(*ml[p.idx], sX[p.idx], sY[p.idx], sW[p.idx], dbatch[p.idx].as<u32>() + t * B, B, aB,
-                        st[p.idx]);
+        const u32* idx;
+        if (sample) {
+            idx = sampler[p.idx]->next();  // getSubset + the batch's indices on the device
+        } else {
+            if (t >= kBatches) throw std::runtime_error("lr job: more iterations than precomputed mini-batches");
+            idx = dbatch[p.idx].as<u32>() + t * B;
+        }
+        sgdLogisticStep(*ml[p.idx], sX[p.idx], sY[p.idx], sW[p.idx], idx, B, aB, st[p.idx]);
     }
     // Smoke check of the revealed model against a plaintext fixed-point
     // restatement of the same iterations (floor shifts as Sh3FixedPoint.h:
@@ -313,8 +339,10 @@ struct LrJob : Job {
         if (p.idx != 0) return true;
         std::vector<i64> w(w0.mData);
         const i64 half = 1ll << (D - 1), one = 1ll << D;
+        const std::vector<u32> drawn = sample ? drawBatches(iter[0]) : std::vector<u32>();
+        const std::vector<u32>& bl = sample ? drawn : batches;
         for (u64 t = 0; t < iter[0]; ++t) {
-            const u32* rows = batches.data() + t * B;
+            const u32* rows = bl.data() + t * B;
             std::vector<i64> err(B);
             for (u64 i = 0; i < B; ++i) {
                 i64 xw = 0;
@@ -345,7 +373,11 @@ struct LrJob : Job {
                          (unsigned long long)iter[0], maxD, maxW, n0 > 0 && n1 > 0 ? dot / std::sqrt(n0 * n1) : 0.0);
         return ok;
     }
-    void info(double* o) override { o[ABY3H_INFO_MULTS_PER_STEP] = 2.0 * B * d; }
+    void info(double* o) override {
+        o[ABY3H_INFO_MULTS_PER_STEP] = 2.0 * B * d;
+        o[ABY3H_INFO_LR_FUSED] = (st[0].fused || st[1].fused || st[2].fused) ? 1 : 0;
+    }
+    const SharedMat* result(int i) const override { return &sW[i]; }
 };
 
 // ---- C5: odd-even merge sort of `keys` 64-bit keys ------------------------
@@ -370,6 +402,7 @@ struct SortJob : Job {
             p.enc.remoteBinMatrix(p.rt, S[p.idx]).get();
     }
     void step(PartyCtx& p) override { odd_even_merge_sort(S[p.idx], R[p.idx], p.idx, p.eval, p.rt); }
+    const SharedMat* result(int i) const override { return &R[i]; }
     // every key, in order: the revealed output equals std::sort of the input
     bool check(PartyCtx& p) override {
         i64Matrix r;
@@ -412,6 +445,7 @@ struct Session {
     u64 probeN[8] = {0};
     int probeFamily = 0;
     bool checkOk = true;
+    u64 digests[3] = {0, 0, 0};
     std::vector<CommPkg> comms;
     double hostEnqueueUs[3] = {0, 0, 0}, hostDrainUs[3] = {0, 0, 0}, hostRecvWaitUs[3] = {0, 0, 0};
     double hostApiUs[3] = {0, 0, 0}, hostApiCalls[3] = {0, 0, 0};
@@ -533,6 +567,17 @@ struct Session {
                     probeN[0] += cnt;
                 } else if (c == 4) {
                     GPU_CALL(aby3g_probe_reset());
+                } else if (c == 6) {
+                    const SharedMat* r = job->result(i);
+                    u64 h = 0xcbf29ce484222325ull;  // FNV-1a over both shares' bytes
+                    if (r && !r->empty())
+                        for (int sh = 0; sh < 2; ++sh) {
+                            const std::vector<i64> v = r->shareToHost(sh);
+                            const u8* b = (const u8*)v.data();
+                            for (size_t k = 0; k < v.size() * 8; ++k) h = (h ^ b[k]) * 0x100000001b3ull;
+                        }
+                    std::lock_guard<std::mutex> lk(mu);
+                    digests[i] = h;
                 } else if (c == 5) {
                     bool ok = job->check(p);
                     p.rt.gpu().sync();
@@ -570,7 +615,8 @@ std::unique_ptr<Job> makeJob(int job, const uint64_t* params, int nparams) {
             return std::make_unique<MulJob>(P(0, 128), P(1, 128), P(2, 128), 0, P(3, 0) ? MulMode::Gemm : MulMode::Hadamard,
                                             false);
         case ABY3H_JOB_MSB: return std::make_unique<MsbJob>(P(0, 1 << 20));
-        case ABY3H_JOB_LR: return std::make_unique<LrJob>(P(0, 1000000), P(1, 128), P(2, 256), P(3, 16), P(4, 11));
+        case ABY3H_JOB_LR:
+            return std::make_unique<LrJob>(P(0, 1000000), P(1, 128), P(2, 256), P(3, 16), P(4, 11), P(5, 0));
         case ABY3H_JOB_SORT: return std::make_unique<SortJob>(P(0, 1 << 20));
         case ABY3H_JOB_A2B: return std::make_unique<A2bJob>(P(0, 1 << 20));
         case ABY3H_JOB_BITINJ: return std::make_unique<BitInjJob>(P(0, 1 << 16), P(1, 64));
@@ -604,8 +650,10 @@ aby3h_session* aby3h_session_create(int job, const uint64_t* params, int nparams
             // all three parties on one device: one stream each (aux aliased)
             // plus the shared draw stream, each with a hardware queue of its
             // own, so their kernels may hand messages over on the device
+            // (and only while no other live stream of this process on the
+            // device, e.g. another open session, could take one of the queues)
             const bool oneDevice = dv[0] == dv[1] && dv[1] == dv[2];
-            s.comms = makeLocalRing(dv, oneDevice && hwQueuesPerDevice() >= 4);
+            s.comms = makeLocalRing(dv, oneDevice && liveStreams(dv[0]) + 4 <= hwQueuesPerDevice());
         }
         s.colocated = !devices || devices[0] == devices[1] || devices[1] == devices[2] || devices[0] == devices[2];
         {
@@ -668,16 +716,22 @@ aby3h_session* aby3h_party_create(int job, const uint64_t* params, int nparams, 
 
 int aby3h_session_run(aby3h_session* h, uint64_t steps) {
     Session& s = h->s;
+    // an in-kernel hand-off that gave up during the run invalidates it
+    // (common.h): the device's timeout count before and after
+    u32 before[3] = {0, 0, 0};
+    try {
+        for (int q : s.locals) before[q] = handoffTimeouts(s.devices[q]);
+    } catch (const std::exception& e) {
+        t_err = e.what();
+        return 1;
+    }
     s.command(1, steps);
     if (s.err.empty()) {
-        // an in-kernel hand-off that gave up invalidates the run (common.h)
         try {
             for (int q : s.locals) {
-                u32 timeouts = 0;
-                GPU_CALL(aby3g_set_device(s.devices[q]));
-                GPU_CALL(aby3g_handoff_status(&timeouts));
-                if (timeouts)
-                    throw std::runtime_error(std::to_string(timeouts) +
+                const u32 n = handoffTimeouts(s.devices[q]) - before[q];
+                if (n)
+                    throw std::runtime_error(std::to_string(n) +
                                              " in-kernel hand-off wait(s) timed out: a party stream without a "
                                              "hardware queue of its own?");
             }
@@ -725,6 +779,21 @@ int aby3h_session_info(aby3h_session* h, double* out, int n) {
     for (int l : h->s.locals) dw += h->s.deviceWaitUs[l];
     tmp[ABY3H_INFO_DEVICE_WAIT_US] = dw / (double)h->s.locals.size();
     for (int i = 0; i < n && i < ABY3H_INFO_COUNT; ++i) out[i] = tmp[i];
+    return 0;
+}
+
+int aby3h_session_digest(aby3h_session* h, int party, uint64_t* out) {
+    Session& s = h->s;
+    if (std::find(s.locals.begin(), s.locals.end(), party) == s.locals.end()) {
+        t_err = "digest: party " + std::to_string(party) + " is not run by this session";
+        return 1;
+    }
+    s.command(6);
+    if (!s.err.empty()) {
+        t_err = s.err;
+        return 1;
+    }
+    *out = s.digests[party];
     return 0;
 }
 

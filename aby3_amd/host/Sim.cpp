@@ -29,7 +29,10 @@ void run3(int device, const std::function<void(SimParty&)>& f, bool mlSeeded = f
     // one stream per party (aux aliased below), so the parties' kernels hand
     // their messages over on the device (Channel::handoffPost)
     const int dv[3] = {device, device, device};
-    auto comms = makeLocalRing(dv, hwQueuesPerDevice() >= 3);
+    // (only while every stream on the device can own a hardware queue: other
+    // live streams of this process -- an open session -- count too)
+    auto comms = makeLocalRing(dv, liveStreams(device) + 3 <= hwQueuesPerDevice());
+    const u32 timeouts0 = handoffTimeouts(device);
     std::exception_ptr err[3];
     std::thread th[3];
     for (int i = 0; i < 3; ++i)
@@ -56,10 +59,9 @@ void run3(int device, const std::function<void(SimParty&)>& f, bool mlSeeded = f
     for (auto& t : th) t.join();
     for (auto& e : err)
         if (e) std::rethrow_exception(e);
-    u32 timeouts = 0;  // an in-kernel hand-off that gave up invalidates the call
-    GPU_CALL(aby3g_set_device(device));
-    GPU_CALL(aby3g_handoff_status(&timeouts));
-    if (timeouts) throw std::runtime_error("in-kernel hand-off wait timed out");
+    // an in-kernel hand-off that gave up (here, or in a concurrent caller on
+    // the device) invalidates the call
+    if (handoffTimeouts(device) != timeouts0) throw std::runtime_error("in-kernel hand-off wait timed out");
 }
 
 i64Matrix hostMat(const int64_t* p, u64 r, u64 c) {

@@ -1,7 +1,9 @@
 #include "aby3ML.h"
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <random>
+#include <thread>
 
 namespace aby3 {
 
@@ -39,17 +41,40 @@ struct FusedLr {
     DeviceBuffer scratch, mailbox;
     const void* nextBox = nullptr;
     const void* prevBox = nullptr;
+    // one party per process: this party's mailbox is a raw allocation exported
+    // through IPC, the neighbours' are IPC mappings
+    void* ownBox = nullptr;
+    void* mapped[2] = {nullptr, nullptr};
+    int device = 0;
+    bool sysScope = false;
     u64 epoch = 0;
     u64 d = 0, B = 0;
     i64 thrOff[2] = {0, 0}, half = 0, slope = 0, one = 0;
 
+    ~FusedLr() {
+        if (!ownBox && !mapped[0] && !mapped[1]) return;
+        // at teardown: every party's last iteration has completed (a session
+        // drains its stream before it ends), and a neighbour's IPC mapping
+        // keeps this allocation alive until it closes it
+        aby3g_set_device(device);
+        aby3g_device_sync();
+        for (void* m : mapped)
+            if (m) aby3g_ipc_close(m);
+        if (ownBox) aby3g_free(ownBox);
+    }
+
     // The fused form applies to the logistic piecewise of aby3ML (regions
     // {}, {c, integer slope}, {c}) with randomization on, B <= 2048 rows, and
-    // a ring of co-located parties; every party decides alike.
+    // a ring whose parties' kernels may poll each other's memory: co-located
+    // parties of one process (Channel::handoffCapable), or one party per
+    // process (Channel::linkedConcurrent; the mailboxes exchanged as IPC
+    // handles, on one GPU or across GPUs). Every party decides alike.
     static std::shared_ptr<FusedLr> make(aby3ML& ml, u64 d, u64 B) {
         Gpu& g = ml.mRt.gpu();
         CommPkg& comm = ml.mRt.mComm;
-        if (!comm.mNext.handoffCapable(g) || !comm.mPrev.handoffCapable(g)) return nullptr;
+        const bool local = comm.mNext.handoffCapable(g) && comm.mPrev.handoffCapable(g);
+        const bool linked = !local && comm.mNext.linkedConcurrent() && comm.mPrev.linkedConcurrent();
+        if (!local && !linked) return nullptr;
         if (ml.mEval.DEBUG_disable_randomization || B == 0 || B > 2048 || d == 0 || d > 4096) return nullptr;
         Sh3Piecewise& pw = ml.logistic();
         const auto& co = pw.mCoefficients;
@@ -59,26 +84,54 @@ struct FusedLr {
         auto f = std::make_shared<FusedLr>();
         f->d = d;
         f->B = B;
+        f->device = g.device();
         for (int t = 0; t < 2; ++t) f->thrOff[t] = (i64)(0 - (u64)pw.mThresholds[t].getFixedPoint(ml.mD));
         f->half = co[1][0].getFixedPoint(ml.mD);
         f->slope = co[1][1].getInteger();
         f->one = co[2][0].getFixedPoint(ml.mD);
         f->upload(g);
         const u64 mb = aby3g_lr_mailbox_bytes((u32)B, (u32)d, &f->cir);
-        f->mailbox.reset(g, mb);
         f->scratch.reset(g, aby3g_lr_scratch_bytes((u32)B, (u32)d, &f->cir));
-        // zeroed before any peer can poll it: the address leaves only after
-        // this stream has drained the memset
-        GPU_CALL(aby3g_memset(f->mailbox.data(), 0, mb, g.stream()));
-        g.sync();
-        const u64 mine = (u64)(uintptr_t)f->mailbox.data();
-        comm.mNext.asyncSendCopy(mine);
-        comm.mPrev.asyncSendCopy(mine);
-        u64 nb = 0, pb = 0;
-        comm.mNext.recv(nb);
-        comm.mPrev.recv(pb);
-        f->nextBox = (const void*)(uintptr_t)nb;
-        f->prevBox = (const void*)(uintptr_t)pb;
+        if (local) {
+            f->mailbox.reset(g, mb);
+            // zeroed before any peer can poll it: the address leaves only after
+            // this stream has drained the memset
+            GPU_CALL(aby3g_memset(f->mailbox.data(), 0, mb, g.stream()));
+            g.sync();
+            const u64 mine = (u64)(uintptr_t)f->mailbox.data();
+            comm.mNext.asyncSendCopy(mine);
+            comm.mPrev.asyncSendCopy(mine);
+            u64 nb = 0, pb = 0;
+            comm.mNext.recv(nb);
+            comm.mPrev.recv(pb);
+            f->nextBox = (const void*)(uintptr_t)nb;
+            f->prevBox = (const void*)(uintptr_t)pb;
+            return f;
+        }
+        // one party per process: which GPUs the neighbours run on decides the
+        // scope of the messages (the three parties reach the same answer: in
+        // a ring of three every party neighbours both others)
+        u8 uuid[16], un[16], up[16];
+        GPU_CALL(aby3g_device_uuid(g.device(), uuid));
+        comm.mNext.asyncSendCopy(uuid, 16);
+        comm.mPrev.asyncSendCopy(uuid, 16);
+        comm.mNext.recv(un, 16);
+        comm.mPrev.recv(up, 16);
+        f->sysScope = std::memcmp(un, uuid, 16) != 0 || std::memcmp(up, uuid, 16) != 0;
+        GPU_CALL(aby3g_set_device(g.device()));
+        GPU_CALL(f->sysScope ? aby3g_malloc_uncached(&f->ownBox, mb) : aby3g_malloc(&f->ownBox, mb));
+        GPU_CALL(aby3g_memset(f->ownBox, 0, mb, g.stream()));
+        g.sync();  // zeroed before its handle leaves
+        aby3g_ipc_handle h{}, hn{}, hp{};
+        GPU_CALL(aby3g_ipc_get_handle(f->ownBox, &h));
+        comm.mNext.asyncSendCopy(h);
+        comm.mPrev.asyncSendCopy(h);
+        comm.mNext.recv(hn);
+        comm.mPrev.recv(hp);
+        GPU_CALL(aby3g_ipc_open(&hn, &f->mapped[0]));
+        GPU_CALL(aby3g_ipc_open(&hp, &f->mapped[1]));
+        f->nextBox = f->mapped[0];
+        f->prevBox = f->mapped[1];
         return f;
     }
 
@@ -164,7 +217,8 @@ struct FusedLr {
         it.batch = batchIdx;
         it.cir = cir;
         it.scratch = scratch.data();
-        it.mailbox = mailbox.data();
+        it.mailbox = ownBox ? ownBox : mailbox.data();
+        it.sys_scope = sysScope ? 1 : 0;
         it.next_mailbox = nextBox;
         it.prev_mailbox = prevBox;
         it.epoch = ++epoch;
@@ -319,13 +373,116 @@ void BatchSampler::next(std::vector<u64>& dest) {
         mIter += step;
         d += step;
         if (mIter == mPool.size()) {
-            for (u64 i = 1; i < mPool.size(); ++i) {
-                const u64 j = mPrng.get<u64>() % (i + 1);
-                if (i != j) std::swap(mPool[i], mPool[j]);
-            }
+            randomShuffle(mPool.data(), mPool.size(), mPrng);
             mIter = 0;
         }
     }
+}
+
+// Pool k (k = 0: the identity, then one reshuffle per epoch) lives in pinned
+// host buffer k & 1 and device buffer k & 1. The host thread that shuffles
+// pool k + 1 starts when pool k becomes current: it copies pool k into the
+// other pinned buffer (pool k - 1's, whose upload finished an epoch ago) and
+// shuffles it in place. When pool k runs out, next() joins the thread and
+// enqueues the upload of pool k + 1 into the other device buffer. Every
+// device-side reuse (a pool buffer, a batch slot) is ordered behind the
+// iterations that read it by the party's stream itself; the host waits only
+// before it rewrites a pinned buffer whose upload might still be in flight.
+struct DeviceBatchSampler::Impl {
+    Gpu& g;
+    u64 n, B;
+    HostPrng prng{toBlock(234543234)};
+    u32* pinned[2] = {nullptr, nullptr};  // pool k & 1 (host)
+    u32* bslot = nullptr;                 // [2][B] pinned: batches across a reshuffle
+    DeviceBuffer dpool[2], dbatch[2];
+    Event upEv[2], bEv[2];
+    bool upRec[2] = {false, false}, bRec[2] = {false, false};
+    u64 k = 0, iter = 0, bnext = 0;
+    std::thread shuffler;
+
+    Impl(Gpu& gg, u64 n_, u64 B_) : g(gg), n(n_), B(B_) {
+        if (!n || !B || B > n || n > 0xffffffffull)
+            throw std::runtime_error("DeviceBatchSampler: need 0 < B <= n < 2^32");
+        for (auto& p : pinned) GPU_CALL(aby3g_host_malloc((void**)&p, n * 4));
+        GPU_CALL(aby3g_host_malloc((void**)&bslot, 2 * B * 4));
+        for (u64 i = 0; i < n; ++i) pinned[0][i] = (u32)i;
+        for (auto& d : dpool) d.reset(g, n * 4);
+        for (auto& d : dbatch) d.reset(g, B * 4);
+        toDevice(dpool[0].data(), pinned[0], n * 4, g);
+        iter = n;  // idxIter = indices.end(): the first getSubset reshuffles (Regression.h:236)
+        startShuffle();
+    }
+    ~Impl() {
+        if (shuffler.joinable()) shuffler.join();
+        for (int b = 0; b < 2; ++b) {  // uploads out of the pinned buffers
+            if (upRec[b]) upEv[b].sync();
+            if (bRec[b]) bEv[b].sync();
+        }
+        for (auto* p : pinned) aby3g_host_free(p);
+        aby3g_host_free(bslot);
+    }
+    void startShuffle() {
+        const int b = (int)((k + 1) & 1);
+        if (upRec[b]) upEv[b].sync();  // pool k - 1's upload (an epoch ago)
+        const u32* src = pinned[k & 1];
+        u32* dst = pinned[b];
+        shuffler = std::thread([this, src, dst] {
+            std::memcpy(dst, src, n * 4);
+            randomShuffle(dst, n, prng);
+        });
+    }
+    // pool k ran out: pool k + 1 becomes current
+    void reshuffle() {
+        shuffler.join();
+        const int b = (int)((k + 1) & 1);
+        GPU_CALL(aby3g_memcpy(dpool[b].data(), pinned[b], n * 4, 0, g.stream()));
+        upEv[b].record(g.stream());
+        upRec[b] = true;
+        ++k;
+        iter = 0;
+        startShuffle();
+    }
+    const u32* next() {
+        if (iter == n) reshuffle();
+        if (iter + B <= n) {
+            const u32* p = dpool[k & 1].as<u32>() + iter;
+            iter += B;
+            if (iter == n) reshuffle();
+            return p;
+        }
+        // the batch spans a reshuffle: the tail of this pool, the head of the next
+        const int s = (int)(bnext++ & 1);
+        if (bRec[s]) bEv[s].sync();
+        u32* dst = bslot + (u64)s * B;
+        u64 d = 0;
+        while (d != B) {
+            const u64 step = std::min<u64>(n - iter, B - d);
+            std::memcpy(dst + d, pinned[k & 1] + iter, step * 4);
+            iter += step;
+            d += step;
+            if (iter == n) reshuffle();
+        }
+        GPU_CALL(aby3g_memcpy(dbatch[s].data(), dst, B * 4, 0, g.stream()));
+        bEv[s].record(g.stream());
+        bRec[s] = true;
+        return dbatch[s].as<u32>();
+    }
+};
+
+DeviceBatchSampler::DeviceBatchSampler(Gpu& g, u64 n, u64 B) : mImpl(std::make_unique<Impl>(g, n, B)) {}
+DeviceBatchSampler::~DeviceBatchSampler() = default;
+const u32* DeviceBatchSampler::next() { return mImpl->next(); }
+u64 DeviceBatchSampler::reshuffles() const { return mImpl->k; }
+
+void SGD_Logistic(RegressionParam& params, aby3ML& engine, const si64Matrix& X, const si64Matrix& Y, si64Matrix& w) {
+    if (X.rows() != Y.rows() || Y.cols() != 1) throw std::runtime_error(LOCATION);
+    const u64 B = params.mBatchSize;
+    // the learning rate in log2 form: truncate this many bits (Regression.h:246)
+    const u64 aB = (u64)std::log2(1 / (params.mLearningRate / (double)B));
+    DeviceBatchSampler sampler(engine.mRt.gpu(), X.rows(), B);
+    SgdState st;
+    for (u64 i = 0; i < params.mIterations; ++i)
+        sgdLogisticStep(engine, X, Y, w, sampler.next(), B, aB, st);
 }
 
 MlSeeds mlSeeds(int pIdx) {

@@ -4,6 +4,7 @@
 #include "Sh3Encryptor.h"
 #include "Sh3Evaluator.h"
 #include "Sh3Piecewise.h"
+#include <algorithm>
 #include <vector>
 
 namespace aby3 {
@@ -101,6 +102,51 @@ private:
     u64 mIter;
     HostPrng mPrng;
 };
+
+// getSubset's pool shuffle (std::random_shuffle(pool, prng), Regression.h:36):
+// for i = 1..n-1 swap pool[i] with pool[prng.get<u64>() % (i + 1)].
+template <class T>
+void randomShuffle(T* pool, u64 n, HostPrng& prng) {
+    for (u64 i = 1; i < n; ++i) {
+        const u64 j = prng.get<u64>() % (i + 1);
+        if (i != j) std::swap(pool[i], pool[j]);
+    }
+}
+
+// getSubset (Regression.h:24-40) for iterations that run on the device: the
+// same mini-batches as BatchSampler, the pool resident in HBM. next() returns
+// the next B row indices as a device pointer, usable by work enqueued on the
+// party's stream before the following call: a slice of the device pool when
+// the batch lies inside one pool, else (a batch across a reshuffle) the batch
+// assembled on the host and uploaded into a small slot. The reshuffle for the
+// next epoch -- std::random_shuffle of the current pool, the PRNG advanced
+// exactly as the reference advances it -- runs on a host thread during the
+// current epoch and is uploaded asynchronously when the pool runs out, so no
+// iteration waits for it or synchronises the stream.
+class DeviceBatchSampler {
+public:
+    DeviceBatchSampler(Gpu& g, u64 n, u64 B);
+    ~DeviceBatchSampler();
+    DeviceBatchSampler(const DeviceBatchSampler&) = delete;
+    DeviceBatchSampler& operator=(const DeviceBatchSampler&) = delete;
+    const u32* next();
+    u64 reshuffles() const;  // pools started so far (the first getSubset reshuffles at once)
+
+private:
+    struct Impl;
+    std::unique_ptr<Impl> mImpl;
+};
+
+// RegressionParam / SGD_Logistic (Regression.h:15-20, 216-295): the whole
+// training loop on device shares -- getSubset, extractBatch, xw = XX w,
+// logistic, err, w -= XX^T err >> (D + aB) with aB = log2(B / rate) -- each
+// iteration one sgdLogisticStep on a DeviceBatchSampler batch.
+struct RegressionParam {
+    u64 mIterations = 0;
+    u64 mBatchSize = 0;
+    double mLearningRate = 0;
+};
+void SGD_Logistic(RegressionParam& params, aby3ML& engine, const si64Matrix& X, const si64Matrix& Y, si64Matrix& w);
 // aby3ML::init (aby3ML.cpp:4-17): party i's seed toBlock(i); PRNG(seed)'s
 // first block is its Sh3Encryptor seed, the second its Sh3Evaluator seed,
 // each exchanged with the neighbours (Sh3ShareGen.h:25-31): returns the

@@ -54,6 +54,10 @@ class Gate(ctypes.Structure):
                 ("z_row", c_uint32), ("send_row", c_uint32)]
 
 
+class Handoff(ctypes.Structure):
+    _fields_ = [("flags", c_void_p), ("seq", c_uint64), ("wait_ticks", c_void_p)]
+
+
 class RowMap(ctypes.Structure):
     """aby3g_rowmap: element p -> idx[first + p], or the affine
     start + rep * rep_stride + k * step with (rep, k) = divmod(first + p, per_rep)."""
@@ -157,6 +161,11 @@ _SIGS = {
     "aby3g_bin_level_hs": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_uint32, c_void_p, c_void_p, ctypes.c_uint32,
                                    c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "aby3g_handoff_status": (c_int, [POINTER(ctypes.c_uint32)]),
+    "aby3g_set_handoff_timeout_us": (c_int, [c_uint64]),
+    "aby3g_bin_level_residency": (c_int, [POINTER(c_int), POINTER(c_int), POINTER(c_int), POINTER(c_int)]),
+    "aby3g_stream_count": (c_int, [c_int, POINTER(c_int)]),
+    "aby3g_malloc_uncached": (c_int, [POINTER(c_void_p), c_size_t]),
+    "aby3g_device_uuid": (c_int, [c_int, c_void_p]),
     "aby3g_event_query": (c_int, [c_void_p, POINTER(c_int)]),
     "aby3g_lr_mailbox_bytes": (c_uint64, [ctypes.c_uint32, ctypes.c_uint32, c_void_p]),
     "aby3g_lr_scratch_bytes": (c_uint64, [ctypes.c_uint32, ctypes.c_uint32, c_void_p]),
@@ -222,7 +231,7 @@ class _Lib:
 JOB_MUL_TRUNC, JOB_MUL, JOB_MSB, JOB_LR, JOB_SORT, JOB_A2B, JOB_BITINJ = range(7)
 INFO = dict(mults_per_step=0, gemm_int8_ops=1, and_words=2, gate_words=3, gate_bytes=4, bytes_sent=5,
             host_enqueue_us=6, host_drain_us=7, host_recv_wait_us=8, host_api_us=9, host_api_calls=10,
-            device_wait_us=11)
+            device_wait_us=11, lr_fused=12)
 
 _HOST_SIGS = {
     "aby3h_last_error": (c_char_p, []),
@@ -233,6 +242,7 @@ _HOST_SIGS = {
     "aby3h_session_probe_reset": (c_int, [c_void_p]),
     "aby3h_session_info": (c_int, [c_void_p, POINTER(c_double), c_int]),
     "aby3h_session_check": (c_int, [c_void_p]),
+    "aby3h_session_digest": (c_int, [c_void_p, c_int, c_void_p]),
     "aby3h_session_destroy": (None, [c_void_p]),
     "aby3h_circuit": (c_int, [c_char_p, c_uint64, c_uint64, POINTER(c_uint64), c_void_p, c_void_p, c_void_p,
                               c_void_p, c_void_p, c_void_p]),
@@ -324,6 +334,13 @@ class Session:
         if rc == 2:
             raise NativeError("aby3h_session_check: " + self.host.aby3h_last_error().decode())
         return rc == 0
+
+    def digest(self, party: int) -> int:
+        """FNV-1a digest of `party`'s two shares of the last step's result."""
+        out = c_uint64()
+        if self.host.aby3h_session_digest(self._h, party, ctypes.byref(out)) != 0:
+            raise NativeError("aby3h_session_digest: " + self.host.aby3h_last_error().decode())
+        return out.value
 
     def close(self):
         if self._h:

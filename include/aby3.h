@@ -33,9 +33,12 @@ enum {
     /* params: rows. One step = cipher_gt / fetch_msb over `rows` 64-bit
      * values: reshare + MSB(a+b) circuit (BuildingBlocks.cpp:464-532). */
     ABY3H_JOB_MSB = 2,
-    /* params: rows (dataset), dim, batch, D, lr_log2. One step = one
+    /* params: rows (dataset), dim, batch, D, lr_log2[, sample]. One step = one
      * SGD_Logistic iteration (aby3-ML/Regression.h:249-293): xw = X_B w,
-     * sigmoid (Sh3Piecewise), err = f - Y_B, w -= X_B^T err >> (D + aB). */
+     * sigmoid (Sh3Piecewise), err = f - Y_B, w -= X_B^T err >> (D + aB).
+     * sample 0 (default): the first 8192 mini-batches are drawn at setup and
+     * kept in HBM; 1: each step draws its batch with getSubset
+     * (DeviceBatchSampler, the pool resident in HBM) inside the step. */
     ABY3H_JOB_LR = 3,
     /* params: keys. One step = odd_even_merge_sort of `keys` 64-bit keys
      * (distinct, (U[0, 2^43) << 20) | i): the multi-merge of singleton lists,
@@ -63,7 +66,8 @@ enum {
     ABY3H_INFO_HOST_API_US = 9,       /* last run: host time per step inside aby3g_* calls (party 0) */
     ABY3H_INFO_HOST_API_CALLS = 10,   /* last run: aby3g_* calls per step (party 0) */
     ABY3H_INFO_DEVICE_WAIT_US = 11,   /* last run: in-kernel wait for peers per step and party (us, mean of the local parties) */
-    ABY3H_INFO_COUNT = 12
+    ABY3H_INFO_LR_FUSED = 12,         /* JOB_LR: 1 when the iterations ran as the fused launch (aby3g_lr_iteration) */
+    ABY3H_INFO_COUNT = 13
 };
 
 const char* aby3h_last_error(void);
@@ -90,6 +94,10 @@ int aby3h_session_run(aby3h_session* s, uint64_t steps);
 int aby3h_session_probe(aby3h_session* s, int family, double* ms, uint64_t* launches);
 int aby3h_session_probe_reset(aby3h_session* s);
 int aby3h_session_info(aby3h_session* s, double* out, int n);
+/* FNV-1a digest of party `party`'s two shares of the last step's result (a
+ * party this session runs): share-level comparisons between layouts, e.g. one
+ * party per process against three in one process on the same seeds. */
+int aby3h_session_digest(aby3h_session* s, int party, uint64_t* out);
 /* reveals the last step's result and checks it against plaintext; 0 = ok */
 int aby3h_session_check(aby3h_session* s);
 void aby3h_session_destroy(aby3h_session* s);

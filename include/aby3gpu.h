@@ -57,12 +57,19 @@ int aby3g_api_time(double* us, uint64_t* calls);
  * 3 let the runtime infer (also peer copies between devices). */
 int aby3g_malloc(void** ptr, size_t bytes);
 int aby3g_free(void* ptr);
+/* device memory that no cache holds (hipDeviceMallocUncached): flags and
+ * mailboxes polled from other GPUs; free with aby3g_free */
+int aby3g_malloc_uncached(void** ptr, size_t bytes);
 int aby3g_host_malloc(void** ptr, size_t bytes); /* pinned host memory */
 int aby3g_host_free(void* ptr);
 int aby3g_memcpy(void* dst, const void* src, size_t bytes, int kind, aby3g_stream stream);
 int aby3g_memset(void* dst, int value, size_t bytes, aby3g_stream stream);
 int aby3g_stream_create(aby3g_stream* stream);
 int aby3g_stream_destroy(aby3g_stream stream);
+/* streams created through aby3g_stream_create and not yet destroyed on
+ * `device` in this process (HIP gives a process GPU_MAX_HW_QUEUES hardware
+ * queues per device; more live streams share them) */
+int aby3g_stream_count(int device, int* n);
 int aby3g_stream_sync(aby3g_stream stream);
 int aby3g_device_sync(void);
 int aby3g_event_create(aby3g_event* ev);       /* ordering only (no timestamp: cheaper to record) */
@@ -98,18 +105,23 @@ int aby3g_stream_wait_value(aby3g_stream stream, uint64_t* word, uint64_t value)
  * an aby3g_handoff accept NULL or flags == NULL for "no hand-off".
  * A waiting kernel can only progress while the producer's stream has a
  * hardware queue of its own; a wait gives up after 5 s, counts a timeout and
- * makes every later wait on the device give up too (wrong results, no hang). */
+ * makes every wait enqueued before that count was seen give up too (wrong
+ * results, no hang). */
 #define ABY3G_HANDOFF_ROWS 2048
 typedef struct {
     uint64_t* flags;
     uint64_t seq;
     uint64_t* wait_ticks;
 } aby3g_handoff;
-/* Nonzero when an in-kernel hand-off wait on the current device timed out
- * since the last call (then resets it). Read after the streams drained; no
- * GPU call (the status word is pinned host memory). Nonzero: results since
- * the last call are invalid. */
+/* The count of in-kernel hand-off waits on the current device that timed
+ * out since the process started (never reset: a caller compares the count
+ * before and after its run; a change means its results are invalid, also
+ * when another caller on the device caused it). No GPU call (the counter is
+ * pinned host memory). */
 int aby3g_handoff_status(uint32_t* timeouts);
+/* Debug: the wait limit of in-kernel hand-offs enqueued from now on
+ * (default 5 s), so tests can force a timeout quickly. */
+int aby3g_set_handoff_timeout_us(uint64_t us);
 
 /* Cross-process transport: one party per process (the
  * reference's parties are processes joined by cryptoTools Channels over TCP,
@@ -131,6 +143,9 @@ int aby3g_host_unregister(void* host);
 /* lets `device` read and write `peer`'s memory (0 also when already enabled;
  * an error when the two devices cannot reach each other) */
 int aby3g_enable_peer_access(int device, int peer);
+/* the device's 16-byte UUID (hipDeviceGetUuid): which physical GPU an
+ * ordinal is, comparable between processes whatever their visible devices */
+int aby3g_device_uuid(int device, uint8_t uuid[16]);
 
 /* Kernel timing probe: when enabled, every kernel launched by this library on
  * the calling thread is bracketed by events; aby3g_probe_read() returns the
@@ -393,6 +408,13 @@ int aby3g_bin_level_hs(const aby3g_gate* gates, const uint32_t* recv_rows, const
                        uint32_t nbatches, const uint64_t* recvbuf, const uint32_t* unpack_wires, uint32_t nunpack,
                        uint64_t* mem, uint64_t wires, uint64_t words, const uint64_t* z, uint64_t* sendbuf,
                        const aby3g_handoff* wait, const aby3g_handoff* post, aby3g_stream stream);
+/* Residency of the hand-off level kernels on the current device, for the
+ * host's in-kernel hand-off budget (a consumer's workgroups spin, so two
+ * consumer launches must leave a producer workgroup a slot): CUs, and
+ * workgroups of each hand-off instantiation resident per CU
+ * (hipOccupancyMaxActiveBlocksPerMultiprocessor) -- the small-grid form
+ * (launches of fewer than *small_max_wgs workgroups) and the large one. */
+int aby3g_bin_level_residency(int* cus, int* per_cu_small, int* per_cu_large, int* small_max_wgs);
 int aby3g_bin_unpack(const uint64_t* recvbuf, const uint32_t* out_wires, uint32_t n, uint64_t* mem, uint64_t wires,
                      uint64_t words, aby3g_stream stream);
 /* setInput (:200-276): bit-transpose a [rows][cols64] i64 share matrix into
@@ -504,8 +526,12 @@ typedef struct {
 
 /* Arguments of one iteration of one party. Mailboxes: aby3g_lr_mailbox_bytes
  * each, zeroed before the first iteration; a party writes only its own and
- * reads its neighbours' (next = party + 1, prev = party + 2 mod 3). epoch:
- * 1 for the first iteration, +1 per iteration, the same for the three. */
+ * reads its neighbours' (next = party + 1, prev = party + 2 mod 3) -- in
+ * this process, or mapped from another process (aby3g_ipc_open). epoch:
+ * 1 for the first iteration, +1 per iteration, the same for the three.
+ * sys_scope: 0 when the three mailboxes are on this device (agent-scope
+ * messages), 1 when a neighbour's is on another GPU (system scope; every
+ * mailbox then from aby3g_malloc_uncached). */
 typedef struct {
     int32_t party;
     uint32_t B, d, D, aB;
@@ -520,6 +546,7 @@ typedef struct {
     const void* next_mailbox;
     const void* prev_mailbox;
     uint64_t epoch;
+    uint32_t sys_scope;
     uint64_t* wait_ticks;    /* optional: in-kernel wait (100 MHz ticks) added here */
     uint64_t* phase_ticks;   /* optional: [32] wall-clock stamps of the phases (profiling) */
     /* the evaluator's ShareGen streams (seeds) and zero-share keys */

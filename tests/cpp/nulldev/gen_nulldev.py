@@ -20,6 +20,8 @@ OVERRIDES = {
     "aby3g_enable_peer_access": "return nd_peer(device, peer);",
     "aby3g_api_time": "*us = 0; *calls = 0; return 0;",
     "aby3g_malloc": "*ptr = nd_alloc(bytes); return *ptr ? 0 : 1;",
+    "aby3g_malloc_uncached": "*ptr = nd_alloc(bytes); return *ptr ? 0 : 1;",
+    "aby3g_device_uuid": "memset(uuid, 0, 16); uuid[0] = (uint8_t)device; return 0;",
     "aby3g_free": "nd_free(ptr); return 0;",
     "aby3g_host_malloc": "*ptr = calloc(1, bytes ? bytes : 1); return *ptr ? 0 : 1;",
     "aby3g_host_free": "free(ptr); return 0;",
@@ -41,6 +43,8 @@ OVERRIDES = {
     "aby3g_host_register": "*dev = host; return 0;",
     "aby3g_probe_read": "*ms = 0; *launches = 0; return 0;",
     "aby3g_handoff_status": "*timeouts = 0; return 0;",
+    "aby3g_stream_count": "*n = 0; return 0;",
+    "aby3g_bin_level_residency": "*cus = 256; *per_cu_small = 1; *per_cu_large = 5; *small_max_wgs = 128; return 0;",
     "aby3g_aes_block_host": "for (int i = 0; i < 16; ++i) out[i] = key[i] ^ (uint8_t)(ctr >> (8 * (i & 7))); return 0;",
     "aby3g_lr_mailbox_bytes": "return 4096;",
     "aby3g_lr_scratch_bytes": "return 4096;",

@@ -31,6 +31,7 @@ static void run3ml(bool fused, const std::function<void(Sh3Runtime&, Sh3Encrypto
                    int device = 0) {
     const int dv[3] = {device, device, device};
     auto comms = fused ? makeLocalRing(dv, true) : makeLocalRing();
+    const u32 timeouts0 = handoffTimeouts(device);
     std::exception_ptr err[3];
     std::thread th[3];
     for (int i = 0; i < 3; ++i)
@@ -53,9 +54,7 @@ static void run3ml(bool fused, const std::function<void(Sh3Runtime&, Sh3Encrypto
     for (auto& t : th) t.join();
     for (auto& e : err)
         if (e) std::rethrow_exception(e);
-    u32 timeouts = 0;
-    GPU_CALL(aby3g_handoff_status(&timeouts));
-    check(timeouts == 0, "an in-kernel hand-off timed out");
+    check(handoffTimeouts(device) == timeouts0, "an in-kernel hand-off timed out");
 }
 
 static void lrParity(bool fused, u64 n, u64 d, u64 B, u64 iters) {

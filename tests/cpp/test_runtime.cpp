@@ -2,6 +2,7 @@
 // Task_schedule_test and Sh3_Runtime_schedule_test
 // (aby3_tests/Sh3RuntimeTests.cpp:15-154, 156-266): exact execution order.
 // CPU-only (the runtime is created without a device).
+#include "Channel.h"
 #include "Sh3Runtime.h"
 #include <cstdio>
 #include <functional>
@@ -132,7 +133,40 @@ static void nested_closure_test() {
     CHECK(counter == 2);
 }
 
+// The in-kernel hand-off residency rule (Channel.h): two spinning consumer
+// launches + the other spinners must leave the producer a CU.
+static void handoff_residency_test() {
+    // MI355X as measured: 256 CUs, one 32-slot workgroup (16 waves) or five
+    // 8-slot workgroups per CU (94 VGPRs), four hardware queues
+    HandoffResidency r{256, 1, 5, 128, 4};
+    CHECK(handoffResidencyOk(r, 1));
+    CHECK(handoffResidencyOk(r, 64));    // light levels (C3's last five)
+    CHECK(handoffResidencyOk(r, 125));   // 2 * 125 + 4 + 1 = 255
+    CHECK(!handoffResidencyOk(r, 126));  // 257 CUs: a small-form consumer pair could fill the chip
+    CHECK(handoffResidencyOk(r, 128));   // the large form: 2 * 26 + 5
+    CHECK(handoffResidencyOk(r, 512));   // 2^20 rows: 2 * 103 + 5 = 211
+    CHECK(handoffResidencyOk(r, 625));
+    CHECK(!handoffResidencyOk(r, 626));
+    // a register regression to 4 waves per SIMD: the 2^20-row messages go back
+    // to the stream hand-off (2 * 128 + 5 > 256), smaller ones stay
+    r.perCuLarge = 4;
+    CHECK(!handoffResidencyOk(r, 512));
+    CHECK(handoffResidencyOk(r, 500));
+    CHECK(!handoffResidencyOk(r, 501));
+    // a part with fewer CUs: the small form's limit drops below the large form's
+    HandoffResidency s{80, 1, 5, 128, 4};
+    CHECK(handoffResidencyOk(s, 37));
+    CHECK(!handoffResidencyOk(s, 38));
+    CHECK(!handoffResidencyOk(s, 100));  // small form (16-wave workgroups), 2 * 100 + 5 > 80
+    CHECK(handoffResidencyOk(s, 185));   // large form: 2 * 37 + 5 = 79
+    // a kernel that cannot be resident at all never hands off in-kernel
+    HandoffResidency z{256, 0, 0, 128, 4};
+    CHECK(!handoffResidencyOk(z, 1));
+    CHECK(!handoffResidencyOk(r, 0));
+}
+
 int main() {
+    run("handoff_residency_test", handoff_residency_test);
     run("Task_schedule_test", task_schedule_test);
     run("Sh3_Runtime_schedule_test", runtime_schedule_test);
     run("Sh3_Runtime_reentrancy_test", reentrancy_test);

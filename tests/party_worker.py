@@ -19,6 +19,10 @@ def main():
     lag = float(os.environ.get("ABY3_TEST_LAG_MS", "0")) / 1e3
     try:
         s.run(1)  # warm-up
+        # bench: more untimed steps first (clock ramp after setup)
+        warm = int(os.environ.get("ABY3_WARMUP_STEPS", "0"))
+        if warm:
+            s.run(warm)
         t0 = time.perf_counter()
         if lag:
             for _ in range(steps):
@@ -27,12 +31,14 @@ def main():
         else:
             s.run(steps)
         dt = time.perf_counter() - t0
+        digest = s.digest(party)  # this party's shares of the result, before check() reveals
         ok = s.check()
         info = s.info()
     finally:
         s.close()
     print(json.dumps({"party": party, "ok": ok, "ms_per_step": 1e3 * dt / steps,
-                      "recv_wait_us": info["host_recv_wait_us"]}), flush=True)
+                      "recv_wait_us": info["host_recv_wait_us"], "digest": digest,
+                      "lr_fused": info["lr_fused"]}), flush=True)
 
 
 if __name__ == "__main__":

@@ -537,6 +537,71 @@ def test_bin_level_matches_unpack_then_batches(gpu, words):
     assert np.array_equal(host(s1)[:zrow * words], host(s3)[:zrow * words])
 
 
+def _timeouts():
+    n = ctypes.c_uint32(0)
+    nt.lib().handoff_status(ctypes.byref(n))
+    return n.value
+
+
+def test_handoff_residency_rule(gpu):
+    """The device's residency figures behind the in-kernel hand-off budget
+    (Channel.h handoffResidencyOk): printed for the log, and the C3 / C5
+    messages (<= 512 chunks) must still qualify, else a register regression
+    of k_bin_level has silently moved them back to stream hand-offs."""
+    cus, small, large, smax = (ctypes.c_int() for _ in range(4))
+    nt.lib().bin_level_residency(ctypes.byref(cus), ctypes.byref(small), ctypes.byref(large), ctypes.byref(smax))
+    print(f"residency: {cus.value} CUs, k_bin_level<32,true> {small.value}/CU, <8,true> {large.value}/CU, "
+          f"small form below {smax.value} workgroups")
+    assert cus.value >= 1 and small.value >= 1 and large.value >= 1
+    per = lambda c: small.value if c < smax.value else large.value  # noqa: E731
+    ok = lambda c: 2 * -(-c // per(c)) + 4 + 1 <= cus.value  # noqa: E731
+    assert ok(64) and ok(512), "C3/C5 level messages no longer fit the residency rule"
+
+
+def test_handoff_timeout_gives_up_and_counts(gpu):
+    """A level launch waiting on a hand-off whose flags are never written
+    gives up after the (shortened) timeout instead of hanging, the device's
+    timeout count goes up by one, and a launch enqueued after that -- whose
+    flags are set -- runs normally without being aborted by the old timeout."""
+    import time
+
+    import torch
+
+    words, wires = 32, 8
+    lib = nt.lib()
+    gates = (nt.Gate * 1)()
+    gates[0].in0, gates[0].in1, gates[0].out, gates[0].type = 0, 1, 2, 0  # one XOR
+    gdev = torch.frombuffer(bytearray(bytes(gates)), dtype=torch.uint8).to("cuda")
+    ends = torch.tensor([1], dtype=torch.int32, device="cuda")
+    uw = torch.tensor([3], dtype=torch.int32, device="cuda")
+    mem, recv = empty(2 * wires * words), empty(words)
+    flags = empty(4)  # zero: never posted
+    before = _timeouts()
+    lib.set_handoff_timeout_us(20000)
+    try:
+        wait = nt.Handoff(ctypes.c_void_p(flags.data_ptr()), 1, None)
+        t0 = time.perf_counter()
+        lib.bin_level_hs(P(gdev), None, P(ends), 1, P(recv), P(uw), 1, P(mem), wires, words, None, None,
+                         ctypes.byref(wait), None, None)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        assert _timeouts() == before + 1
+        assert dt < 5, f"the wait took {dt:.2f} s with a 20 ms limit"
+        # posted flags now: a fresh wait completes and counts nothing
+        flags.fill_(1)
+        torch.cuda.synchronize()
+        lib.bin_level_hs(P(gdev), None, P(ends), 1, P(recv), P(uw), 1, P(mem), wires, words, None, None,
+                         ctypes.byref(wait), None, None)
+        torch.cuda.synchronize()
+        assert _timeouts() == before + 1
+    finally:
+        lib.set_handoff_timeout_us(5000000)
+    # and a three-party call after it is unaffected by the earlier timeout
+    a = np.arange(64, dtype=np.int64).reshape(8, 8)
+    sh, plain = nt.sim.mul(1, 0, 0, a, a, 8, 8, 8)
+    assert np.array_equal(plain.reshape(8, 8), a @ a)
+
+
 def test_lincomb_bitops(gpu):
     import torch
 

@@ -42,20 +42,38 @@ def run_parties(job, params, steps, tag, timeout=150, lag_ms=0):
     return outs
 
 
+def colocated_digests(job, params, steps):
+    """The same job run by three parties in one process (the same seeds):
+    each party's digest of its result shares."""
+    with nt.Session(job, params, probe=False) as s:
+        s.run(steps)
+        return [s.digest(p) for p in range(3)]
+
+
 @pytest.mark.parametrize("job,params,steps", [
     (nt.JOB_MUL_TRUNC, [1024, 1024, 1024, 16, 1], 3),   # C2 shapes
     (nt.JOB_MUL_TRUNC, [257, 200, 250, 8, 1], 2),       # ragged GEMM, D8
     (nt.JOB_MUL, [128, 128, 128, 0], 3),                # C1 Hadamard
     (nt.JOB_MSB, [1 << 16], 2),                         # C3 circuit levels
-    (nt.JOB_LR, [20000, 128, 256, 16, 11], 5),          # C4 (dataset trimmed)
+    (nt.JOB_LR, [20000, 128, 256, 16, 11], 5),          # C4 (dataset trimmed), fused across processes
+    (nt.JOB_LR, [20000, 128, 256, 16, 11, 1], 90),      # C4 with getSubset in every step, across a reshuffle
     (nt.JOB_SORT, [4096], 1),                           # C5 network, every key checked
     (nt.JOB_A2B, [5000], 2),                            # toBinaryMatrix
     (nt.JOB_BITINJ, [777, 13], 2),                      # bitInjection (OT messages)
 ])
 def test_three_party_processes(gpu, job, params, steps):
-    outs = run_parties(job, params, steps, f"{job}_{params[0]}")
+    """Every job by three processes: the revealed result checked against
+    plaintext, and every party's result shares identical to the same job's
+    in one process (share-exact across the two layouts)."""
+    outs = run_parties(job, params, steps, f"{job}_{params[0]}_{len(params)}")
     assert sorted(o["party"] for o in outs) == [0, 1, 2]
     assert all(o["ok"] for o in outs), outs
+    if job == nt.JOB_LR:
+        # the fused iteration runs across the processes (IPC-mapped mailboxes)
+        assert all(o["lr_fused"] == 1 for o in outs), outs
+    ref = colocated_digests(job, params, steps + 1)  # the worker's warm-up step + steps
+    got = [o["digest"] for o in sorted(outs, key=lambda o: o["party"])]
+    assert got == ref
 
 
 def test_lagging_party_many_steps(gpu):

@@ -158,6 +158,8 @@ def test_merge_vs_oracle(gpu, mode, dim, lens):
     (nt.JOB_MUL, [128, 128, 128, 1], 3),                # C1 GEMM
     (nt.JOB_MSB, [1 << 20], 2),                         # C3 every row checked
     (nt.JOB_LR, [100000, 128, 256, 16, 11], 20),        # C4 shapes (dataset trimmed)
+    (nt.JOB_LR, [1000000, 128, 256, 16, 11], 20),       # C4 at its 10^6 x 128 dataset
+    (nt.JOB_LR, [1000000, 128, 256, 16, 11, 1], 40),    # C4 with getSubset inside every step
     (nt.JOB_SORT, [1 << 20], 1),                        # C5 the whole 2^20-key sort, every key checked
     (nt.JOB_SORT, [777], 2),                            # sort of a ragged count
     (nt.JOB_A2B, [1 << 20], 2),                         # toBinaryMatrix, every value checked

@@ -56,3 +56,15 @@ def test_link_large_cyclic_exchange(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
     assert "link_exchange: ok" in r.stdout
+
+
+@pytest.mark.parametrize("sanitizer", ["address", "thread"])
+def test_device_batch_sampler(tmp_path, sanitizer):
+    """DeviceBatchSampler (getSubset with the pool in device memory and the
+    reshuffle on a host thread) yields BatchSampler's mini-batches exactly."""
+    exe = _build(str(tmp_path), sanitizer, "sampler_check.cpp")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1", TSAN_OPTIONS="halt_on_error=1")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    assert "sampler_check: ok" in r.stdout
+    assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-4000:]

@@ -78,8 +78,9 @@ def test_lr_gpu_matches_fixture(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,B,iters", [(20000, 256, 5), (3000, 64, 4)])
+@pytest.mark.parametrize("n,B,iters", [(20000, 256, 5), (3000, 64, 4), (1000000, 256, 3)])
 def test_lr_vs_oracle(gpu, n, B, iters):
+    # (1000000, 256, 3): C4's own dataset (BASELINE configs[3]), 2 GB of shares per party
     X, Y, _ = nt.lr_dataset(n, 128, 16)
     b = nt.lr_batches(n, B, iters)
     sh_g, w_g = nt.sim.lr(X, Y, b)

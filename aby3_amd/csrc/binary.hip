@@ -147,6 +147,16 @@ constexpr u32 kLevelUnroll = 4;
 // publishes its own send rows for the next party's same workgroup (hp) --
 // the levels of the three parties pipeline chunk by chunk.
 static_assert(kLevelWords * 64 == ABY3G_HANDOFF_ROWS, "a level workgroup is one hand-off chunk");
+// The circuit's few-bit output fused into its last level (aby3g_bin_level_out):
+// after the gates, a thread per (share, row) of the workgroup's chunk gathers
+// bit (row & 63) of each output wire's word, as k_w2b_few does.
+struct OutFuse {
+    const u32* wires;  // nbits output wires; nbits == 0: none
+    u32 nbits;
+    i64* out;          // [2][rows] (one column)
+    u64 rows;
+};
+
 template <u32 SLOTS, bool HS>
 __global__ void __launch_bounds__(SLOTS * 32) k_bin_level(const aby3g_gate* __restrict__ gates,
                                                          const uint2* __restrict__ rrows,
@@ -155,7 +165,7 @@ __global__ void __launch_bounds__(SLOTS * 32) k_bin_level(const aby3g_gate* __re
                                                          const u32* __restrict__ unpack_wires, u32 nunpack,
                                                          u64* __restrict__ mem, u64 wires, u64 words,
                                                          const u64* __restrict__ z, u64* __restrict__ sendbuf,
-                                                         HsWait hw, HsPost hp) {
+                                                         HsWait hw, HsPost hp, OutFuse of) {
     // HS: the in-kernel hand-off instantiation (sc1 payload accesses, waits
     // and posts); the other is the plain streaming kernel
     if (HS && !hs_wait(hw, blockIdx.x, blockIdx.x + 1)) return;
@@ -190,6 +200,114 @@ __global__ void __launch_bounds__(SLOTS * 32) k_bin_level(const aby3g_gate* __re
         begin = end;
     }
     if (HS) hs_post(hp, blockIdx.x, blockIdx.x + 1);
+    if (of.nbits) {
+        __syncthreads();
+        for (u32 k = threadIdx.x; k < 2 * kLevelWords * 64; k += SLOTS * 32) {
+            const u32 sh = k / (kLevelWords * 64);
+            const u64 r = (u64)blockIdx.x * kLevelWords * 64 + (k % (kLevelWords * 64));
+            if (r >= of.rows) continue;
+            const u64* m = sh ? s1 : s0;
+            const u64 wr = r >> 6;
+            const u32 bit = (u32)(r & 63);
+            u64 v = 0;
+            for (u32 j = 0; j < of.nbits; ++j) v |= ((m[(u64)of.wires[j] * words + wr] >> bit) & 1ull) << j;
+            of.out[(u64)sh * of.rows + r] = (i64)v;
+        }
+    }
+}
+
+// Several consecutive levels in one launch (aby3g_bin_levels), every message
+// between them handed over in-kernel: a workgroup carries its chunk through
+// the levels -- wait for the previous party's same chunk of the previous
+// level, unpack, this level's batches, publish its send rows -- so the three
+// parties' launches pipeline chunk by chunk and level by level with no launch
+// boundary between levels. Level descriptors are kernel arguments.
+struct LevelRun {
+    u32 first_gate, batch_off, nbatches, nunpack;
+    const u32* unpack_wires;
+    const u64* recv;  // the previous level's AND shares, or null
+    u64* send;        // this level's send rows, or null
+    u64 wait_seq;     // 0: nothing to wait for (none received, or a stream hand-off before the launch)
+    u64 post_seq;     // 0: nothing sent
+};
+constexpr u32 kMaxRuns = ABY3G_LEVELS_MAX;
+struct LevelRuns {
+    LevelRun l[kMaxRuns];
+};
+
+// A persistent grid: at most one workgroup per CU per party (the three
+// parties' grids are then resident together whatever else runs, so no
+// workgroup spins waiting for a peer's workgroup that has no slot); each
+// carries its chunks c = blockIdx.x + k gridDim.x level by level.
+template <u32 SLOTS>
+__global__ void __launch_bounds__(SLOTS * 32) k_bin_levels(LevelRuns runs, u32 nruns, u32 nchunks,
+                                                          const aby3g_gate* __restrict__ gates,
+                                                          const uint2* __restrict__ rrows,
+                                                          const u32* __restrict__ batch_ends, u64* __restrict__ mem,
+                                                          u64 wires, u64 words, const u64* __restrict__ z, HsWait hw,
+                                                          u64* postFlags, OutFuse of) {
+    const u32 lane = threadIdx.x & 31, slot = threadIdx.x >> 5;
+    u64* s0 = mem;
+    u64* s1 = mem + wires * words;
+#pragma unroll 1
+    for (u32 li = 0; li < nruns; ++li) {
+        const LevelRun& L = runs.l[li];
+        const u64* __restrict__ recv = L.recv;
+        const uint2* rr0 = (rrows && recv) ? rrows + L.first_gate : nullptr;
+        const aby3g_gate* gl = gates + L.first_gate;
+        const u32* be = batch_ends + L.batch_off;
+#pragma unroll 1
+        for (u32 c = blockIdx.x; c < nchunks; c += gridDim.x) {
+            const u64 w = (u64)c * kLevelWords + lane;
+            if (L.wait_seq) {
+                HsWait h = hw;
+                h.seq = L.wait_seq;
+                if (!hs_wait(h, c, c + 1)) return;
+            }
+#pragma unroll 4
+            for (u32 j = slot; j < L.nunpack; j += SLOTS)
+                s1[(u64)L.unpack_wires[j] * words + w] = hs_load(recv + (u64)j * words + w);
+            u32 begin = 0;
+            for (u32 b = 0; b < L.nbatches; ++b) {
+                if (b || !rr0) __syncthreads();
+                const u32 end = be[b];
+                for (u32 g0 = begin + slot; g0 < end; g0 += kLevelUnroll * SLOTS) {
+                    aby3g_gate g[kLevelUnroll];
+                    uint2 rr[kLevelUnroll];
+                    GateOps o[kLevelUnroll];
+#pragma unroll
+                    for (u32 k = 0; k < kLevelUnroll; ++k)
+                        if (g0 + k * SLOTS < end) {
+                            g[k] = gl[g0 + k * SLOTS];
+                            rr[k] = rr0 ? rr0[g0 + k * SLOTS] : make_uint2(~0u, ~0u);
+                        }
+#pragma unroll
+                    for (u32 k = 0; k < kLevelUnroll; ++k)
+                        if (g0 + k * SLOTS < end) gate_load(g[k], rr[k], s0, s1, recv, words, w, z, o[k], true);
+#pragma unroll
+                    for (u32 k = 0; k < kLevelUnroll; ++k)
+                        if (g0 + k * SLOTS < end) gate_eval(g[k], o[k], s0, s1, words, w, L.send, true);
+                }
+                begin = end;
+            }
+            if (L.post_seq) hs_post(HsPost{postFlags, L.post_seq}, c, c + 1);
+            __syncthreads();  // the next chunk / level: this one's words are done
+        }
+    }
+    if (of.nbits) {
+        for (u32 c = blockIdx.x; c < nchunks; c += gridDim.x)
+            for (u32 k = threadIdx.x; k < 2 * kLevelWords * 64; k += SLOTS * 32) {
+                const u32 sh = k / (kLevelWords * 64);
+                const u64 r = (u64)c * kLevelWords * 64 + (k % (kLevelWords * 64));
+                if (r >= of.rows) continue;
+                const u64* m = sh ? s1 : s0;
+                const u64 wr = r >> 6;
+                const u32 bit = (u32)(r & 63);
+                u64 v = 0;
+                for (u32 j = 0; j < of.nbits; ++j) v |= ((m[(u64)of.wires[j] * words + wr] >> bit) & 1ull) << j;
+                of.out[(u64)sh * of.rows + r] = (i64)v;
+            }
+    }
 }
 
 __global__ void __launch_bounds__(kGateBlock) k_bin_unpack(const u64* __restrict__ recv, const u32* __restrict__ outw,
@@ -440,6 +558,147 @@ __global__ void __launch_bounds__(64) k_b2w_lin_regs(WireSrcs ws, u64 rows, u64 
         if (c * 64 + b < src.nbits) out[(c * 64 + b) * words + w] = R[b];
 }
 
+// copy_out of every source only (aby3g_lin_copy_out), a thread per element
+__global__ void __launch_bounds__(256) k_lin_copy(WireSrcs ws, u32 nsrc, u64 rows) {
+    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
+#pragma unroll
+    for (u32 k = 0; k < ABY3G_WIRE_SRC_MAX; ++k) {
+        if (k >= nsrc) break;
+        const aby3g_wire_src& src = ws.s[k];
+        if (!src.copy_out || i >= rows * src.cols64) continue;
+        u64 v = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            if (src.term[t]) v += (u64)src.coef[t] * (u64)src.term[t][i];
+        src.copy_out[i] = (i64)v;
+    }
+}
+
+// The first level with its inputs (aby3g_bin_level_in). A source: one 64-bit
+// input (at most 64 wires from `wire` on) of one share, the sum of its terms
+// plus the constant on rows < rows.
+struct LevelInSrc {
+    const u64* term[4];
+    u64 coef[4];
+    u64 constant;
+    u32 wire, share, nbits, pad;
+};
+struct LevelInSrcs {
+    LevelInSrc s[ABY3G_WIRE_SRC_MAX];
+};
+constexpr u32 kInMax = ABY3G_LEVEL_IN_MAX_WIRES;
+
+// operands of one gate: input wires through tab (the LDS row of (wire - inLo,
+// share) in win, kInZero: an all-zero source), other wires from mem
+constexpr u32 kInZero = 0xffff;
+__device__ __forceinline__ u64 in_word(const u64* win, unsigned short row, u32 wl) {
+    return row == kInZero ? 0 : win[(u32)row * kLevelWords + wl];
+}
+__device__ __forceinline__ void gate_load_in(const aby3g_gate& g, const u64* win, const unsigned short* tab, u32 inLo, u32 nin,
+                                             const u64* s0, const u64* s1, u64 words, u64 w, u32 wl,
+                                             const u64* __restrict__ z, GateOps& o) {
+    const bool unary = g.type == ABY3G_GATE_COPY || g.type == ABY3G_GATE_INV;
+    const u32 in1 = unary ? g.in0 : g.in1;
+    const u32 a = g.in0 - inLo, b = in1 - inLo;
+    if (a < nin) {
+        o.x0 = in_word(win, tab[2 * a], wl);
+        o.x1 = in_word(win, tab[2 * a + 1], wl);
+    } else {
+        o.x0 = s0[(u64)g.in0 * words + w];
+        o.x1 = s1[(u64)g.in0 * words + w];
+    }
+    if (b < nin) {
+        o.y0 = in_word(win, tab[2 * b], wl);
+        o.y1 = in_word(win, tab[2 * b + 1], wl);
+    } else {
+        o.y0 = s0[(u64)in1 * words + w];
+        o.y1 = s1[(u64)in1 * words + w];
+    }
+    o.z = gate_is_and(g.type) ? z[(u64)g.z_row * words + w] : 0;
+}
+
+// One workgroup per ABY3G_HANDOFF_ROWS chunk, as k_bin_level. Its waves first
+// build the chunk's input words of every source WITH terms in LDS (16 KiB a
+// source, dynamic: a source without terms is all zero and takes no LDS, so a
+// party's comparison input -- one or two non-zero sources of the four --
+// keeps the level kernel's occupancy): a wave per (source, word), lane = row,
+// the sum of the terms transposed with transpose64 (lane b gets bit b of the
+// 64 rows). The inputs are read once, as the rows of the shares, and the
+// level's gates then read the input wires from LDS instead of HBM (the first
+// level of a 64-bit comparison reads each input wire 2-3 times).
+template <u32 SLOTS, bool HS>
+__global__ void __launch_bounds__(SLOTS * 32) k_bin_level_in(LevelInSrcs srcs, u32 nsrc, u64 rows, u32 inLo, u32 nin,
+                                                            int writeInputs, const aby3g_gate* __restrict__ gates,
+                                                            const u32* __restrict__ batch_ends, u32 nbatches,
+                                                            u64* __restrict__ mem, u64 wires, u64 words,
+                                                            const u64* __restrict__ z, u64* __restrict__ sendbuf,
+                                                            HsPost hp) {
+    extern __shared__ __attribute__((aligned(16))) u64 win[];  // [source][64 wires][32 words]
+    __shared__ unsigned short tab[2 * kInMax];                           // (wire - inLo, share) -> win row
+    constexpr u32 kT = SLOTS * 32, kWaves = kT / 64;
+    const u32 tid = threadIdx.x, lane64 = tid & 63, wave = tid >> 6;
+    for (u32 i = tid; i < 2 * nin; i += kT) tab[i] = kInZero;  // uncovered wires read zero
+    __syncthreads();
+    // sources are in LDS-slot order (the launcher passes only sources with terms)
+    for (u32 i = tid; i < nsrc * 64; i += kT) {
+        const u32 k = i >> 6, b = i & 63;
+        u32 wire = 0, share = 0, nbits = 0;
+#pragma unroll
+        for (u32 j = 0; j < ABY3G_WIRE_SRC_MAX; ++j)
+            if (j == k) wire = srcs.s[j].wire, share = srcs.s[j].share, nbits = srcs.s[j].nbits;
+        if (b < nbits) tab[2 * (wire - inLo + b) + share] = (unsigned short)(k * 64 + b);
+    }
+    const u64 w0 = (u64)blockIdx.x * kLevelWords;
+#pragma unroll
+    for (u32 k = 0; k < ABY3G_WIRE_SRC_MAX; ++k) {
+        if (k >= nsrc) break;
+        const LevelInSrc& src = srcs.s[k];
+        for (u32 wl = wave; wl < kLevelWords; wl += kWaves) {
+            const u64 r = (w0 + wl) * 64 + lane64;
+            u64 v = 0;
+            if (r < rows) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    if (src.term[t]) v += src.coef[t] * src.term[t][r];
+                v += src.constant;
+            }
+            const u64 tw = transpose64(v, lane64);
+            win[(k * 64 + lane64) * kLevelWords + wl] = tw;  // rows >= nbits: never looked up
+        }
+    }
+    __syncthreads();
+    u64* s0 = mem;
+    u64* s1 = mem + wires * words;
+    if (writeInputs)
+        for (u32 i = tid; i < nin * 2 * kLevelWords; i += kT) {
+            const u32 wl = i % kLevelWords, sh = (i / kLevelWords) & 1, wi = i / (2 * kLevelWords);
+            (sh ? s1 : s0)[(u64)(inLo + wi) * words + w0 + wl] = in_word(win, tab[2 * wi + sh], wl);
+        }
+    const u32 lane = tid & 31, slot = tid >> 5;
+    const u64 w = w0 + lane;
+    u32 begin = 0;
+    for (u32 b = 0; b < nbatches; ++b) {
+        if (b) __syncthreads();
+        const u32 end = batch_ends[b];
+        for (u32 g0 = begin + slot; g0 < end; g0 += kLevelUnroll * SLOTS) {
+            aby3g_gate g[kLevelUnroll];
+            GateOps o[kLevelUnroll];
+#pragma unroll
+            for (u32 k = 0; k < kLevelUnroll; ++k)
+                if (g0 + k * SLOTS < end) g[k] = gates[g0 + k * SLOTS];
+#pragma unroll
+            for (u32 k = 0; k < kLevelUnroll; ++k)
+                if (g0 + k * SLOTS < end) gate_load_in(g[k], win, tab, inLo, nin, s0, s1, words, w, lane, z, o[k]);
+#pragma unroll
+            for (u32 k = 0; k < kLevelUnroll; ++k)
+                if (g0 + k * SLOTS < end) gate_eval(g[k], o[k], s0, s1, words, w, sendbuf, HS);
+        }
+        begin = end;
+    }
+    if (HS) hs_post(hp, blockIdx.x, blockIdx.x + 1);
+}
+
+
 // Rows p, p + 64, p + 128, ... of a merge round's compare-exchange list ->
 // rows of the merge array (aby3g_rowmap), without a division per row (a 32-
 // or 64-bit division is ~20-40 VALU ops, 16 of them per thread made the
@@ -624,17 +883,19 @@ int aby3g_bin_level_rr(const aby3g_gate* gates, const uint32_t* recv_rows, const
                               z, sendbuf, nullptr, nullptr, stream);
 }
 
-int aby3g_bin_level_hs(const aby3g_gate* gates, const uint32_t* recv_rows, const uint32_t* batch_ends,
-                       uint32_t nbatches, const uint64_t* recvbuf, const uint32_t* unpack_wires, uint32_t nunpack,
-                       uint64_t* mem, uint64_t wires, uint64_t words, const uint64_t* z, uint64_t* sendbuf,
-                       const aby3g_handoff* wait, const aby3g_handoff* post, aby3g_stream stream) {
+static int bin_level(const aby3g_gate* gates, const uint32_t* recv_rows, const uint32_t* batch_ends,
+                     uint32_t nbatches, const uint64_t* recvbuf, const uint32_t* unpack_wires, uint32_t nunpack,
+                     uint64_t* mem, uint64_t wires, uint64_t words, const uint64_t* z, uint64_t* sendbuf,
+                     const aby3g_handoff* wait, const aby3g_handoff* post, const OutFuse& of, aby3g_stream stream) {
     const uint2* rrows = reinterpret_cast<const uint2*>(recv_rows);
     return guarded([&] {
+        ABY3G_REQUIRE(of.nbits <= 64 && (!of.nbits || (of.wires && of.out && of.rows <= words * 64)),
+                      "fused output: at most 64 wires, rows within the engine's words");
         ABY3G_REQUIRE(!rrows || recvbuf, "recv_rows without a recv buffer");
         ABY3G_REQUIRE(words % kLevelWords == 0, "words must be padded to a multiple of 32 (2048 rows)");
         ABY3G_REQUIRE(!(wait && wait->flags) || nunpack, "a hand-off wait without received shares");
         ABY3G_REQUIRE(!(post && post->flags) || sendbuf, "a hand-off post without a send buffer");
-        if ((!nbatches && !nunpack) || !words) return;
+        if ((!nbatches && !nunpack && !of.nbits) || !words) return;
         // one workgroup per chunk; in-kernel hand-offs are used only for
         // launches of at most 64 chunks, or 512 from a light producer
         // (Channel::handoffPost), so the spinning workgroups of two parties'
@@ -650,18 +911,83 @@ int aby3g_bin_level_hs(const aby3g_gate* gates, const uint32_t* recv_rows, const
         if (wgs < kLevelSmallMaxWgs) {
             if (hs)
                 launch(PROBE_BINARY, k_bin_level<32, true>, dim3(wgs), dim3(32 * 32), 0, S(stream), gates, rrows,
-                       batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp);
+                       batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp, of);
             else
                 launch(PROBE_BINARY, k_bin_level<32, false>, dim3(wgs), dim3(32 * 32), 0, S(stream), gates, rrows,
-                       batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp);
+                       batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp, of);
         } else {
             if (hs)
                 launch(PROBE_BINARY, k_bin_level<8, true>, dim3(wgs), dim3(8 * 32), 0, S(stream), gates, rrows,
-                       batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp);
+                       batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp, of);
             else
                 launch(PROBE_BINARY, k_bin_level<8, false>, dim3(wgs), dim3(8 * 32), 0, S(stream), gates, rrows,
-                       batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp);
+                       batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp, of);
         }
+    });
+}
+
+int aby3g_bin_level_hs(const aby3g_gate* gates, const uint32_t* recv_rows, const uint32_t* batch_ends,
+                       uint32_t nbatches, const uint64_t* recvbuf, const uint32_t* unpack_wires, uint32_t nunpack,
+                       uint64_t* mem, uint64_t wires, uint64_t words, const uint64_t* z, uint64_t* sendbuf,
+                       const aby3g_handoff* wait, const aby3g_handoff* post, aby3g_stream stream) {
+    return bin_level(gates, recv_rows, batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z,
+                     sendbuf, wait, post, OutFuse{nullptr, 0, nullptr, 0}, stream);
+}
+
+int aby3g_bin_level_out(const aby3g_gate* gates, const uint32_t* recv_rows, const uint32_t* batch_ends,
+                        uint32_t nbatches, const uint64_t* recvbuf, const uint32_t* unpack_wires, uint32_t nunpack,
+                        uint64_t* mem, uint64_t wires, uint64_t words, const uint64_t* z, uint64_t* sendbuf,
+                        const aby3g_handoff* wait, const aby3g_handoff* post, const uint32_t* out_wires,
+                        uint32_t nout, int64_t* out, uint64_t rows, aby3g_stream stream) {
+    return bin_level(gates, recv_rows, batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z,
+                     sendbuf, wait, post, OutFuse{out_wires, nout, out, rows}, stream);
+}
+
+int aby3g_bin_levels(const aby3g_level_run* runs, uint32_t nruns, const aby3g_gate* gates, const uint32_t* recv_rows,
+                     const uint32_t* batch_ends, uint64_t* mem, uint64_t wires, uint64_t words, const uint64_t* z,
+                     const aby3g_handoff* wait, uint64_t* post_flags, const uint32_t* out_wires, uint32_t nout,
+                     int64_t* out, uint64_t rows, aby3g_stream stream) {
+    return guarded([&] {
+        ABY3G_REQUIRE(nruns <= kMaxRuns, "too many levels for one launch");
+        ABY3G_REQUIRE(words % kLevelWords == 0, "words must be padded to a multiple of 32 (2048 rows)");
+        ABY3G_REQUIRE(nout <= 64 && (!nout || (out_wires && out && rows <= words * 64)), "fused output");
+        if (!nruns || !words) return;
+        LevelRuns lr{};
+        bool waits = false;
+        for (u32 i = 0; i < nruns; ++i) {
+            const aby3g_level_run& r = runs[i];
+            ABY3G_REQUIRE(!r.nunpack || r.recv, "received shares without a buffer");
+            ABY3G_REQUIRE(!r.post_seq || (r.send && post_flags), "a post without a send buffer or flags");
+            ABY3G_REQUIRE(!r.wait_seq || (r.nunpack && wait && wait->flags), "a wait without received shares");
+            ABY3G_REQUIRE(!r.wait_seq || i == 0 || r.wait_seq > runs[i - 1].wait_seq, "wait sequence numbers");
+            // a level after the first receives only in-kernel (a stream wait
+            // cannot sit inside the launch)
+            ABY3G_REQUIRE(i == 0 || !r.nunpack || r.wait_seq, "a later level's shares must be handed over in-kernel");
+            LevelRun& d = lr.l[i];
+            d.first_gate = r.first_gate;
+            d.batch_off = r.batch_off;
+            d.nbatches = r.nbatches;
+            d.nunpack = r.nunpack;
+            d.unpack_wires = r.unpack_wires;
+            d.recv = r.recv;
+            d.send = r.send;
+            d.wait_seq = r.wait_seq;
+            d.post_seq = r.post_seq;
+            waits = waits || r.wait_seq;
+        }
+        const HsWait hw = waits ? hs_wait_arg(wait) : HsWait{nullptr, 0, nullptr, HsStatus{nullptr, 0, 0}};
+        const u32 chunks = (u32)(words / kLevelWords);
+        const OutFuse of{out_wires, nout, out, rows};
+        const uint2* rr = reinterpret_cast<const uint2*>(recv_rows);
+        static thread_local int cus = 0;
+        if (!cus) ABY3G_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, current_device()));
+        const u32 grid = std::min<u32>(chunks, (u32)cus);  // persistent: a workgroup per CU at most
+        if (chunks < kLevelSmallMaxWgs)
+            launch(PROBE_BINARY, k_bin_levels<32>, dim3(grid), dim3(32 * 32), 0, S(stream), lr, nruns, chunks, gates, rr,
+                   batch_ends, mem, wires, words, z, hw, post_flags, of);
+        else
+            launch(PROBE_BINARY, k_bin_levels<8>, dim3(grid), dim3(8 * 32), 0, S(stream), lr, nruns, chunks, gates, rr,
+                   batch_ends, mem, wires, words, z, hw, post_flags, of);
     });
 }
 
@@ -670,10 +996,19 @@ int aby3g_bin_level_residency(int* cus, int* per_cu_small, int* per_cu_large, in
         ABY3G_REQUIRE(cus && per_cu_small && per_cu_large && small_max_wgs, "null argument");
         const int dev = current_device();
         ABY3G_CHECK_HIP(hipDeviceGetAttribute(cus, hipDeviceAttributeMultiprocessorCount, dev));
+        // the consumers that spin: the hand-off level kernel and the
+        // multi-level one (the smaller residency of the two)
+        int a = 0, b = 0;
         ABY3G_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            per_cu_small, reinterpret_cast<const void*>(k_bin_level<32, true>), 32 * 32, 0));
+            &a, reinterpret_cast<const void*>(k_bin_level<32, true>), 32 * 32, 0));
         ABY3G_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            per_cu_large, reinterpret_cast<const void*>(k_bin_level<8, true>), 8 * 32, 0));
+            &b, reinterpret_cast<const void*>(k_bin_levels<32>), 32 * 32, 0));
+        *per_cu_small = std::min(a, b);
+        ABY3G_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &a, reinterpret_cast<const void*>(k_bin_level<8, true>), 8 * 32, 0));
+        ABY3G_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &b, reinterpret_cast<const void*>(k_bin_levels<8>), 8 * 32, 0));
+        *per_cu_large = std::min(a, b);
         *small_max_wgs = (int)kLevelSmallMaxWgs;
     });
 }
@@ -742,6 +1077,88 @@ int aby3g_bits_to_wires_lin(const aby3g_wire_src* srcs, uint32_t nsrc, uint64_t 
         if (!cols) return;
         const u64 wgs = ((words + 63) / 64) * cols;
         launch(PROBE_OTHER, k_b2w_lin_regs, dim3((u32)wgs, nsrc), dim3(64), 0, S(stream), ws, (u64)rows, (u64)words);
+    });
+}
+
+int aby3g_lin_copy_out(const aby3g_wire_src* srcs, uint32_t nsrc, uint64_t rows, aby3g_stream stream) {
+    return guarded([&] {
+        ABY3G_REQUIRE(nsrc <= ABY3G_WIRE_SRC_MAX, "too many sources");
+        WireSrcs ws{};
+        u64 n = 0;
+        for (u32 k = 0; k < nsrc; ++k) {
+            ws.s[k] = srcs[k];
+            if (srcs[k].copy_out) n = std::max<u64>(n, rows * srcs[k].cols64);
+        }
+        if (!n) return;
+        launch(PROBE_OTHER, k_lin_copy, dim3((u32)((n + 255) / 256)), dim3(256), 0, S(stream), ws, nsrc, (u64)rows);
+    });
+}
+
+int aby3g_bin_level_in(const aby3g_wire_src* srcs, uint32_t nsrc, uint64_t rows, uint32_t in_lo, uint32_t in_hi,
+                       int write_inputs, const aby3g_gate* gates, const uint32_t* batch_ends, uint32_t nbatches,
+                       uint64_t* mem, uint64_t wires, uint64_t words, const uint64_t* z, uint64_t* sendbuf,
+                       const aby3g_handoff* post, aby3g_stream stream) {
+    return guarded([&] {
+        ABY3G_REQUIRE(nsrc <= ABY3G_WIRE_SRC_MAX, "too many sources");
+        ABY3G_REQUIRE(words % kLevelWords == 0, "words must be padded to a multiple of 32 (2048 rows)");
+        ABY3G_REQUIRE(words * 64 >= rows, "words too small for rows");
+        ABY3G_REQUIRE(in_lo <= in_hi && in_hi - in_lo <= kInMax && in_hi <= wires, "input wires out of range");
+        ABY3G_REQUIRE(!(post && post->flags) || sendbuf, "a hand-off post without a send buffer");
+        if (!words) return;
+        const u64 shareStride = wires * words;
+        LevelInSrcs ls{};
+        u32 nl = 0;  // sources with terms, in LDS-slot order
+        for (u32 k = 0; k < nsrc; ++k) {
+            const aby3g_wire_src& s = srcs[k];
+            ABY3G_REQUIRE(s.wire_rows != nullptr, "null wire rows");
+            ABY3G_REQUIRE(s.cols64 == 1 && s.nbits <= 64, "fused inputs take one 64-bit column per source");
+            ABY3G_REQUIRE(s.copy_out == nullptr, "copy_out: call aby3g_lin_copy_out first");
+            const u64 off = (u64)(s.wire_rows - mem);
+            ABY3G_REQUIRE(s.wire_rows >= mem && off % words == 0 && off / words < 2 * wires, "wire_rows outside mem");
+            if (!s.term[0] && !s.term[1] && !s.term[2] && !s.term[3]) continue;  // all zero: no LDS
+            LevelInSrc& d = ls.s[nl++];
+            for (int t = 0; t < 4; ++t) {
+                d.term[t] = (const u64*)s.term[t];
+                d.coef[t] = (u64)s.coef[t];
+            }
+            d.constant = (u64)s.constant;
+            d.share = (u32)(off / shareStride);
+            d.wire = (u32)((off % shareStride) / words);
+            d.nbits = s.nbits;
+            ABY3G_REQUIRE(d.wire >= in_lo && d.wire + d.nbits <= in_hi, "source wires outside [in_lo, in_hi)");
+        }
+        const u32 wgs = (u32)(words / kLevelWords);
+        const HsPost hp = hs_post_arg(post);
+        const u32 nin = in_hi - in_lo;
+        const size_t lds = (size_t)nl * 64 * kLevelWords * 8;
+        static const bool attr = [] {  // up to 8 sources (128 KiB) of dynamic LDS, once per process
+            bool ok = true;
+            for (const void* f : {(const void*)k_bin_level_in<32, true>, (const void*)k_bin_level_in<32, false>,
+                                  (const void*)k_bin_level_in<8, true>, (const void*)k_bin_level_in<8, false>})
+                ok = ok && hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 128 << 10) == hipSuccess;
+            return ok;
+        }();
+        ABY3G_REQUIRE(attr || lds <= (64 << 10), "could not raise the fused level's dynamic LDS limit");
+        nsrc = nl;
+        if (wgs < kLevelSmallMaxWgs) {
+            if (hp.flags)
+                launch(PROBE_BINARY, k_bin_level_in<32, true>, dim3(wgs), dim3(32 * 32), lds, S(stream), ls, nsrc,
+                       (u64)rows, in_lo, nin, write_inputs, gates, batch_ends, nbatches, mem, wires, words, z, sendbuf,
+                       hp);
+            else
+                launch(PROBE_BINARY, k_bin_level_in<32, false>, dim3(wgs), dim3(32 * 32), lds, S(stream), ls, nsrc,
+                       (u64)rows, in_lo, nin, write_inputs, gates, batch_ends, nbatches, mem, wires, words, z, sendbuf,
+                       hp);
+        } else {
+            if (hp.flags)
+                launch(PROBE_BINARY, k_bin_level_in<8, true>, dim3(wgs), dim3(8 * 32), lds, S(stream), ls, nsrc,
+                       (u64)rows, in_lo, nin, write_inputs, gates, batch_ends, nbatches, mem, wires, words, z, sendbuf,
+                       hp);
+            else
+                launch(PROBE_BINARY, k_bin_level_in<8, false>, dim3(wgs), dim3(8 * 32), lds, S(stream), ls, nsrc,
+                       (u64)rows, in_lo, nin, write_inputs, gates, batch_ends, nbatches, mem, wires, words, z, sendbuf,
+                       hp);
+        }
     });
 }
 

@@ -69,14 +69,19 @@ struct LrKeys {
     AesKey zsp, zsn;        // zero-share keys
     AesKey mp, mn;          // circuit masks (setCir)
     AesKey otn, otp;        // SharedOT keys
+    AesKey mp2, mn2;        // the next iteration's circuit masks (drawn ahead)
 };
 
 // Block 0 copies the schedules into LDS (AesRkLds): as kernel arguments the
 // eight of them spill out of SGPRs (loaded up front, one dependent scalar load
 // per 64 bytes: ~7 us at the start of every launch).
-enum : u32 { kKeyPrev, kKeyNext, kKeyZsp, kKeyZsn, kKeyMp, kKeyMn, kKeyOtn, kKeyOtp, kLrKeys };
+enum : u32 { kKeyPrev, kKeyNext, kKeyZsp, kKeyZsn, kKeyMp, kKeyMn, kKeyOtn, kKeyOtp, kKeyMp2, kKeyMn2, kLrKeys };
 constexpr u32 kKeyWords = 44;
 static_assert(sizeof(LrKeys) == kLrKeys * kKeyWords * 4, "LrKeys is the schedules in kKey order");
+
+// Pads of the OT and public products per batch row drawn ahead (the most any
+// party uses: P0's 7 OT-product words and 5 public-product words).
+constexpr u64 kPads = 12;
 
 // Mailbox and scratch layouts, in u64 words.
 struct Layout {
@@ -86,6 +91,10 @@ struct Layout {
     u64 z1, v, lvl, ots, oth, otc, pma, pmb, z2;
     // scratch
     u64 xw, a, fr, f2, yy, err, z1own, z2own, upd, reg, zmask, mem, prod, hprod, hy, hpart, total;
+    // randomness drawn ahead: two slots (epoch parity), each the circuit's
+    // masks, the two truncation pairs' stream words and the OT / public
+    // product pads (kPads words per batch row, party-specific)
+    u64 pre, preSlot, pzm, ptw1, ptw2, ppad;
     __host__ __device__ Layout(u32 B, u32 d, const aby3g_lr_circuit& c) {
         W = (B + 63) / 64;
         Wpad = 32 * (((u64)B + 2047) / 2048);
@@ -119,6 +128,12 @@ struct Layout {
         hprod = o, o += B;                          // helpers: XX w products, one per batch row
         hy = o, o += 2 * (u64)B;                    // helpers: YY (both shares)
         hpart = o, o += (u64)lr_helpers(B) * d;     // helpers: partial XX^T err, one d-vector each
+        pzm = 0;
+        ptw1 = pzm + (u64)c.nand * W;               // next-stream words [B], prev-stream words [B]
+        ptw2 = ptw1 + 2 * (u64)B;                   // the same for the second pair [d], [d]
+        ppad = ptw2 + 2 * (u64)d;                   // pads [kPads][B]
+        preSlot = ppad + kPads * (u64)B;
+        pre = o, o += 2 * preSlot;
         total = o;
     }
     __host__ __device__ u64 mailboxWords() const { return flags + 2 * region; }
@@ -238,10 +253,23 @@ __device__ __forceinline__ bool msg_done(const MsgWait& w, u32* bad, u64* ticks)
 // a tile needs at most 129 blocks of each stream -- threads [0, 256) draw the
 // next stream's, [256, 512) the prev stream's, one block each, into tw (512
 // u64 of LDS), then the tile's elements are formed from it.
+// pw: the stream words drawn ahead (pw[i] next, pw[n + i] prev), or null.
 __device__ __forceinline__ void lr_trunc_pair(const u32* T, const u32* keys, u64 nw0, u64 pw0, u32 n, u32 d,
                                               const u64* prod, u64* out, MsgTag tag, u64* own, u64* c0, u64* c1,
-                                              u64* tw) {
+                                              u64* tw, const u64* pw) {
     const u32 tid = threadIdx.x, half = tid >> 8, t = tid & 255;
+    if (pw) {
+        for (u32 i = tid; i < n; i += kLrThreads) {
+            const i64 t0 = (i64)pw[i], t1 = (i64)pw[n + i];
+            const u64 z = prod[i] - (u64)(t0 >> 2);
+            own[i] = z;
+            msg_put(out, i, z, tag);
+            c0[i] = (u64)(t0 >> (d + 2));
+            c1[i] = (u64)(t1 >> (d + 2));
+        }
+        __syncthreads();
+        return;
+    }
     for (u32 i0 = 0; i0 < n; i0 += 256) {
         const u32 nt = min(256u, n - i0);
         const u64 w0 = (half ? pw0 : nw0) + i0;  // this half's first stream word of the tile
@@ -294,6 +322,106 @@ __device__ __forceinline__ void lr_arrive(u64* box, u32 f) {
     if (threadIdx.x == 0) __hip_atomic_fetch_add((gu64*)box + f, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The next iteration's randomness, drawn by the helper workgroups into
+// scratch slot `slot` (aby3g_lr_iter.pre_next) exactly as block 0 would draw
+// it -- the circuit's masks, the stream words of the two truncation pairs and
+// the OT / public-product pads of this party -- so that the next launch's
+// protocol workgroup only reads it. One work item per thread, strided over
+// the G helpers: a mask pair of words, a stream word, or a batch row's pads.
+__device__ __forceinline__ void lr_predraw(const aby3g_lr_iter& it, const u32* T, const u32* keys, u64* slot,
+                                           const Layout& L) {
+    const aby3g_lr_rand& r = it.next_rand;
+    const u32 B = it.B, d = it.d, G = lr_helpers(B);
+    const u64 W = L.W, Wh = (W + 1) / 2;
+    const int p = it.party;
+    auto KL = [&](u32 key) -> const u32* { return keys + key * kKeyWords; };
+    const u64 q0 = (u64)(blockIdx.x - 1) * kLrThreads + threadIdx.x, qs = (u64)G * kLrThreads;
+    // masks: words 2 wp, 2 wp + 1 of AND gate k (as phase 0)
+    for (u64 q = q0; q < (u64)it.cir.nand * Wh; q += qs) {
+        asm volatile("" ::: "memory");  // keeps the round-key reads in the loop (hoisted, they held ~90 VGPRs)
+        const u64 k = q / Wh, wp = q % Wh;
+        const u64 c = (k * L.Wpad + 2 * wp) >> 1;
+        u64 lo[2], hi[2];
+        lr_blocks<2>(T, {KL(kKeyMp2), KL(kKeyMn2)}, {c, c}, lo, hi);
+        slot[L.pzm + k * W + 2 * wp] = lo[0] ^ lo[1];
+        if (2 * wp + 1 < W) slot[L.pzm + k * W + 2 * wp + 1] = hi[0] ^ hi[1];
+    }
+    // truncation-pair stream words: [next B | prev B] then [next d | prev d]
+    for (u64 q = q0; q < 2 * ((u64)B + d); q += qs) {
+        asm volatile("" ::: "memory");  // keeps the round-key reads in the loop (hoisted, they held ~90 VGPRs)
+        const bool second = q >= 2 * (u64)B;
+        const u64 e = second ? q - 2 * (u64)B : q;
+        const u32 n = second ? d : B;
+        const bool prev = e >= n;
+        const u64 off = second ? (prev ? r.t2_prev_off : r.t2_next_off) : (prev ? r.t1_prev_off : r.t1_next_off);
+        slot[(second ? L.ptw2 : L.ptw1) + e] = stream_word(T, KL(prev ? kKeyPrev : kKeyNext), off / 8 + (prev ? e - n : e));
+    }
+    // batch row i's pads (phase 3): the OT product's, then the public product's
+    u64* pad = slot + L.ppad;
+    for (u64 q = q0; q < B; q += qs) {
+        asm volatile("" ::: "memory");  // keeps the round-key reads in the loop (hoisted, they held ~90 VGPRs)
+        const u32 i = (u32)q;
+        if (p == 0) {
+            const u64 otw = r.ot_prev_off / 8, wz = otw + 2 * i, wc = wz + 1, wn = r.ot_next_off / 8 + i;
+            u64 lo[3], hi[3];
+            lr_blocks<3>(T, {KL(kKeyPrev), KL(kKeyPrev), KL(kKeyNext)}, {wz >> 1, wc >> 1, wn >> 1}, lo, hi);
+            pad[0 * B + i] = (wz & 1) ? hi[0] : lo[0];
+            pad[1 * B + i] = (wc & 1) ? hi[1] : lo[1];
+            pad[2 * B + i] = (wn & 1) ? hi[2] : lo[2];
+            u64 l2[2], h2[2];
+            lr_blocks<2>(T, {KL(kKeyOtn), KL(kKeyOtn)}, {r.ot_ctr + i, r.ot_ctr + B + i}, l2, h2);
+            pad[3 * B + i] = l2[0];
+            pad[4 * B + i] = h2[0];
+            pad[5 * B + i] = l2[1];
+            pad[6 * B + i] = h2[1];
+        } else if (p == 1) {
+            const u64 wf = r.ot_prev_off / 8 + i, j = r.pm_draw + i;
+            u64 lo[3], hi[3];
+            lr_blocks<3>(T, {KL(kKeyPrev), KL(kKeyZsp), KL(kKeyZsn)}, {wf >> 1, j >> 1, j >> 1}, lo, hi);
+            pad[0 * B + i] = (wf & 1) ? hi[0] : lo[0];
+            pad[1 * B + i] = (j & 1) ? hi[1] - hi[2] : lo[1] - lo[2];
+        } else {
+            const u64 otw = r.ot_next_off / 8, wz = otw + 2 * i, wc = wz + 1;
+            u64 l2[2], h2[2];
+            lr_blocks<2>(T, {KL(kKeyNext), KL(kKeyNext)}, {wz >> 1, wc >> 1}, l2, h2);
+            pad[0 * B + i] = (wz & 1) ? h2[0] : l2[0];
+            pad[1 * B + i] = (wc & 1) ? h2[1] : l2[1];
+            lr_blocks<2>(T, {KL(kKeyOtp), KL(kKeyOtp)}, {r.ot_ctr + i, r.ot_ctr + B + i}, l2, h2);
+            pad[2 * B + i] = l2[0];
+            pad[3 * B + i] = h2[0];
+            pad[4 * B + i] = l2[1];
+            pad[5 * B + i] = h2[1];
+        }
+    }
+    for (u64 q = q0; q < B; q += qs) {
+        asm volatile("" ::: "memory");  // keeps the round-key reads in the loop (hoisted, they held ~90 VGPRs)
+        const u32 i = (u32)q;
+        const u64 j = r.pm_draw + i;
+        u64 l2[2], h2[2];
+        if (p == 0) {
+            lr_blocks<2>(T, {KL(kKeyZsp), KL(kKeyZsn)}, {j >> 1, j >> 1}, l2, h2);
+            pad[7 * B + i] = (j & 1) ? h2[0] - h2[1] : l2[0] - l2[1];
+            lr_blocks<2>(T, {KL(kKeyOtn), KL(kKeyOtp)}, {r.pm_ctr_next + i, r.pm_ctr_prev + i}, l2, h2);
+            pad[8 * B + i] = l2[0];
+            pad[9 * B + i] = h2[0];
+            pad[10 * B + i] = l2[1];
+            pad[11 * B + i] = h2[1];
+        } else if (p == 1) {
+            u64 l1[1], h1[1];
+            lr_blocks<1>(T, {KL(kKeyOtn)}, {r.pm_ctr_next + i}, l1, h1);
+            pad[2 * B + i] = l1[0];
+            pad[3 * B + i] = h1[0];
+        } else {
+            lr_blocks<2>(T, {KL(kKeyZsp), KL(kKeyZsn)}, {j >> 1, j >> 1}, l2, h2);
+            pad[6 * B + i] = (j & 1) ? h2[0] - h2[1] : l2[0] - l2[1];
+            u64 l1[1], h1[1];
+            lr_blocks<1>(T, {KL(kKeyOtp)}, {r.pm_ctr_prev + i}, l1, h1);
+            pad[7 * B + i] = l1[0];
+            pad[8 * B + i] = h1[0];
+        }
+    }
+}
+
 // Helper workgroup h = blockIdx.x - 1 of the launch: batch rows
 // [h R, min(B, (h + 1) R)), R = ceil(B / G).
 //   phase 1: hprod[i] = XX0[i] (w0 + w1) + XX1[i] w0 and hy = YY of its rows,
@@ -303,7 +431,8 @@ __device__ __forceinline__ void lr_arrive(u64* box, u32 f) {
 // A wave per row (rows wave, wave + 8, ...), lanes over k pairs (16-byte
 // loads), kLrHelperUnroll rows of a wave in flight.
 constexpr u32 kLrHelperUnroll = 4;
-__device__ __forceinline__ void lr_helper(const aby3g_lr_iter& it, const HsStatus& status, u64* part) {
+__device__ __forceinline__ void lr_helper(const u32* T0g, const aby3g_lr_iter& it, const LrKeys& K,
+                                          const HsStatus& status, u64* part, u32* lds, u32* keys) {
     const u32 B = it.B, d = it.d, G = lr_helpers(B), h = blockIdx.x - 1;
     const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const Layout L(B, d, it.cir);
@@ -355,6 +484,15 @@ __device__ __forceinline__ void lr_helper(const aby3g_lr_iter& it, const HsStatu
         }
     }
     lr_arrive(box, F_H1);
+
+    // ---- between phases 1 and 4 (block 0 runs the protocol): the next
+    // iteration's randomness, off block 0's path ----
+    if (it.pre_next) {
+        const u32* kw = reinterpret_cast<const u32*>(&K);
+        for (u32 i = threadIdx.x; i < kLrKeys * kKeyWords; i += kLrThreads) keys[i] = kw[i];
+        aes_fill_lds(lds, T0g);  // its barrier publishes the keys too
+        lr_predraw(it, lds, keys, sc + L.pre + ((ep + 1) & 1) * L.preSlot, L);
+    }
 
     // ---- phase 4 ----
     // block 0's err comes only after its circuit and products (~80 us): until
@@ -431,11 +569,15 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
                                          u32* lds, u32* keys, u64* dyn, u64* tw) {
     u64* const PT = it.phase_ticks;
     lr_stamp(PT, 0);
-    {
+    // this iteration's randomness drawn ahead by the previous launch's
+    // helpers (pre_have): no AES on this workgroup at all
+    const Layout L0(it.B, it.d, it.cir);
+    const u64* pre = it.pre_have ? (const u64*)it.scratch + L0.pre + (it.epoch & 1) * L0.preSlot : nullptr;
+    if (!pre) {
         const u32* kw = reinterpret_cast<const u32*>(&K);
         for (u32 i = threadIdx.x; i < kLrKeys * kKeyWords; i += kLrThreads) keys[i] = kw[i];
+        aes_fill_lds(lds, T0g);  // its barrier publishes the keys too
     }
-    aes_fill_lds(lds, T0g);  // its barrier publishes the keys too
     lr_stamp(PT, 12);
     const u32* T = lds;
     auto KL = [&](u32 key) -> const u32* { return keys + key * kKeyWords; };
@@ -494,7 +636,13 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
     }
 
     // ---- phase 0: the circuit's AND masks, words with rows only ----
-    {
+    if (pre) {
+        // drawn ahead: into LDS beside the engine memory, or read in place
+        if (kLds)
+            for (u64 q = tid; q < (u64)cir.nand * W; q += kLrThreads) zmw[q] = pre[L.pzm + q];
+        else
+            zmw = const_cast<u64*>(pre + L.pzm);
+    } else {
         u64* zm = zmw;
         const u64 Wh = (W + 1) / 2;
         // two items per thread (q, q + 512), their four blocks interleaved:
@@ -528,7 +676,7 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
     __shared__ u32 msgBad;
     if (tid == 0) msgBad = 0;
     lr_trunc_pair(T, keys, it.t1_next_off / 8, it.t1_prev_off / 8, B, it.D, prod, my + L.z1, tag, sc + L.z1own, xw0,
-                  xw1, tw);
+                  xw1, tw, pre ? pre + L.ptw1 : nullptr);
     lr_stamp(PT, 3);
     {
         MsgWait mw = msg_begin(tag, status);
@@ -637,6 +785,7 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
     __syncthreads();
     lr_stamp(PT, 7);
     const u64 otw = p == 0 ? it.ot_prev_off / 8 : p == 1 ? it.ot_prev_off / 8 : it.ot_next_off / 8;
+    const u64* pad = pre ? pre + L.ppad : nullptr;  // the pads drawn ahead
     // Each send loop splits its AES blocks over all 512 threads (the OT part
     // on threads [0, B), the public-product part on [B, 2B)) and interleaves a
     // thread's blocks in one lr_blocks<NB> call: one wave of dependent
@@ -647,12 +796,17 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
             if (q < B) {
                 // OT product, sender + helper (Sh3Evaluator.cpp:132-163)
                 const u32 i = q;
-                const u64 wz = otw + 2 * i, wc = wz + 1, wn = nw + i;
-                const u32* const k[5] = {KL(kKeyPrev), KL(kKeyPrev), KL(kKeyNext), KL(kKeyOtn), KL(kKeyOtn)};
-                const u64 c[5] = {wz >> 1, wc >> 1, wn >> 1, it.ot_ctr + i, it.ot_ctr + B + i};
-                u64 lo[5], hi[5];
-                lr_blocks<5>(T, k, c, lo, hi);
-                const u64 zr = (wz & 1) ? hi[0] : lo[0], c1 = (wc & 1) ? hi[1] : lo[1], c0 = (wn & 1) ? hi[2] : lo[2];
+                u64 lo[5], hi[5], zr, c1, c0;
+                if (pad) {
+                    zr = pad[0 * B + i], c1 = pad[1 * B + i], c0 = pad[2 * B + i];
+                    lo[3] = pad[3 * B + i], hi[3] = pad[4 * B + i], lo[4] = pad[5 * B + i], hi[4] = pad[6 * B + i];
+                } else {
+                    const u64 wz = otw + 2 * i, wc = wz + 1, wn = nw + i;
+                    const u32* const k[5] = {KL(kKeyPrev), KL(kKeyPrev), KL(kKeyNext), KL(kKeyOtn), KL(kKeyOtn)};
+                    const u64 c[5] = {wz >> 1, wc >> 1, wn >> 1, it.ot_ctr + i, it.ot_ctr + B + i};
+                    lr_blocks<5>(T, k, c, lo, hi);
+                    zr = (wz & 1) ? hi[0] : lo[0], c1 = (wc & 1) ? hi[1] : lo[1], c0 = (wn & 1) ? hi[2] : lo[2];
+                }
                 fr0[i] = c0;
                 fr1[i] = c1;
                 const u32 bb0 = (u32)((r1a[i] ^ r1b[i]) & 1), bb1 = (u32)(r1a[i] & 1);
@@ -666,12 +820,17 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
             } else {
                 // public product (Sh3Evaluator.cpp:430-447)
                 const u32 i = q - B;
-                const u64 j = it.pm_draw + i;
-                const u32* const k[4] = {KL(kKeyZsp), KL(kKeyZsn), KL(kKeyOtn), KL(kKeyOtp)};
-                const u64 c[4] = {j >> 1, j >> 1, it.pm_ctr_next + i, it.pm_ctr_prev + i};
-                u64 lo[4], hi[4];
-                lr_blocks<4>(T, k, c, lo, hi);
-                const u64 zs = (j & 1) ? hi[0] - hi[1] : lo[0] - lo[1];
+                u64 lo[4], hi[4], zs;
+                if (pad) {
+                    zs = pad[7 * B + i];
+                    lo[2] = pad[8 * B + i], hi[2] = pad[9 * B + i], lo[3] = pad[10 * B + i], hi[3] = pad[11 * B + i];
+                } else {
+                    const u64 j = it.pm_draw + i;
+                    const u32* const k[4] = {KL(kKeyZsp), KL(kKeyZsn), KL(kKeyOtn), KL(kKeyOtp)};
+                    const u64 c[4] = {j >> 1, j >> 1, it.pm_ctr_next + i, it.pm_ctr_prev + i};
+                    lr_blocks<4>(T, k, c, lo, hi);
+                    zs = (j & 1) ? hi[0] - hi[1] : lo[0] - lo[1];
+                }
                 const u32 bb = (u32)((r2a[i] ^ r2b[i]) & 1);
                 u64 t[2];
                 t[bb] = zs;
@@ -694,19 +853,28 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
             if (q < B) {
                 // OT receiver's share 1 (:165-200); public product, helper (:452-487)
                 const u32 i = q;
-                const u64 wf = otw + i, j = it.pm_draw + i;
-                const u32* const k[3] = {KL(kKeyPrev), KL(kKeyZsp), KL(kKeyZsn)};
-                const u64 c[3] = {wf >> 1, j >> 1, j >> 1};
-                u64 lo[3], hi[3];
-                lr_blocks<3>(T, k, c, lo, hi);
-                fr1[i] = (wf & 1) ? hi[0] : lo[0];
-                const u64 zs = (j & 1) ? hi[1] - hi[2] : lo[1] - lo[2];
+                u64 zs;
+                if (pad) {
+                    fr1[i] = pad[0 * B + i];
+                    zs = pad[1 * B + i];
+                } else {
+                    const u64 wf = otw + i, j = it.pm_draw + i;
+                    const u32* const k[3] = {KL(kKeyPrev), KL(kKeyZsp), KL(kKeyZsn)};
+                    const u64 c[3] = {wf >> 1, j >> 1, j >> 1};
+                    u64 lo[3], hi[3];
+                    lr_blocks<3>(T, k, c, lo, hi);
+                    fr1[i] = (wf & 1) ? hi[0] : lo[0];
+                    zs = (j & 1) ? hi[1] - hi[2] : lo[1] - lo[2];
+                }
                 g1[i] = zs;
                 msg_put(my + L.pmb, i, zs, tag);  // mine -> P0
             } else {
                 const u32 i = q - B;
                 u64 lo[1], hi[1];
-                lr_blocks<1>(T, {KL(kKeyOtn)}, {it.pm_ctr_next + i}, lo, hi);
+                if (pad)
+                    lo[0] = pad[2 * B + i], hi[0] = pad[3 * B + i];
+                else
+                    lr_blocks<1>(T, {KL(kKeyOtn)}, {it.pm_ctr_next + i}, lo, hi);
                 msg_put(my + L.pma, i, (r2a[i] & 1) ? hi[0] : lo[0], tag);  // help -> P2
             }
         }
@@ -727,12 +895,17 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
             if (q < B) {
                 // OT product, sender + helper (:202-240)
                 const u32 i = q;
-                const u64 wz = otw + 2 * i, wc = wz + 1;
-                const u32* const k[4] = {KL(kKeyNext), KL(kKeyNext), KL(kKeyOtp), KL(kKeyOtp)};
-                const u64 c[4] = {wz >> 1, wc >> 1, it.ot_ctr + i, it.ot_ctr + B + i};
-                u64 lo[4], hi[4];
-                lr_blocks<4>(T, k, c, lo, hi);
-                const u64 zr = (wz & 1) ? hi[0] : lo[0], c0 = (wc & 1) ? hi[1] : lo[1];
+                u64 lo[4], hi[4], zr, c0;
+                if (pad) {
+                    zr = pad[0 * B + i], c0 = pad[1 * B + i];
+                    lo[2] = pad[2 * B + i], hi[2] = pad[3 * B + i], lo[3] = pad[4 * B + i], hi[3] = pad[5 * B + i];
+                } else {
+                    const u64 wz = otw + 2 * i, wc = wz + 1;
+                    const u32* const k[4] = {KL(kKeyNext), KL(kKeyNext), KL(kKeyOtp), KL(kKeyOtp)};
+                    const u64 c[4] = {wz >> 1, wc >> 1, it.ot_ctr + i, it.ot_ctr + B + i};
+                    lr_blocks<4>(T, k, c, lo, hi);
+                    zr = (wz & 1) ? hi[0] : lo[0], c0 = (wc & 1) ? hi[1] : lo[1];
+                }
                 fr0[i] = c0;
                 const u32 bb0 = (u32)(r1b[i] & 1), bb1 = (u32)((r1a[i] ^ r1b[i]) & 1);
                 u64 s[2];
@@ -744,12 +917,17 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
             } else {
                 // public product, helper
                 const u32 i = q - B;
-                const u64 j = it.pm_draw + i;
-                const u32* const k[3] = {KL(kKeyZsp), KL(kKeyZsn), KL(kKeyOtp)};
-                const u64 c[3] = {j >> 1, j >> 1, it.pm_ctr_prev + i};
-                u64 lo[3], hi[3];
-                lr_blocks<3>(T, k, c, lo, hi);
-                const u64 zs = (j & 1) ? hi[0] - hi[1] : lo[0] - lo[1];
+                u64 lo[3], hi[3], zs;
+                if (pad) {
+                    zs = pad[6 * B + i];
+                    lo[2] = pad[7 * B + i], hi[2] = pad[8 * B + i];
+                } else {
+                    const u64 j = it.pm_draw + i;
+                    const u32* const k[3] = {KL(kKeyZsp), KL(kKeyZsn), KL(kKeyOtp)};
+                    const u64 c[3] = {j >> 1, j >> 1, it.pm_ctr_prev + i};
+                    lr_blocks<3>(T, k, c, lo, hi);
+                    zs = (j & 1) ? hi[0] - hi[1] : lo[0] - lo[1];
+                }
                 g0[i] = zs;
                 msg_put(my + L.pma, i, (r2b[i] & 1) ? hi[2] : lo[2], tag);  // help -> P1
                 msg_put(my + L.pmb, i, zs, tag);                            // mine -> P0
@@ -791,7 +969,8 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
     const u32 sh2 = it.D + it.aB;
     u64* u0 = sc + L.upd;
     u64* u1 = u0 + d;
-    lr_trunc_pair(T, keys, it.t2_next_off / 8, it.t2_prev_off / 8, d, sh2, prod, my + L.z2, tag, sc + L.z2own, u0, u1, tw);
+    lr_trunc_pair(T, keys, it.t2_next_off / 8, it.t2_prev_off / 8, d, sh2, prod, my + L.z2, tag, sc + L.z2own, u0, u1, tw,
+                  pre ? pre + L.ptw2 : nullptr);
     lr_stamp(PT, 10);
     {
         MsgWait mw = msg_begin(tag, status);
@@ -812,7 +991,7 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
     __shared__ __attribute__((aligned(16))) u32 keys[kLrKeys * kKeyWords];
     extern __shared__ __attribute__((aligned(16))) u64 dyn[];  // [2][wires][W] engine memory, then [nand][W] masks
     if (blockIdx.x > 0)
-        lr_helper(it, status, part);
+        lr_helper(T0g, it, K, status, part, lds, keys);
     else if (memInLds)
         lr_party<true>(T0g, it, K, status, lds, keys, dyn, part);
     else
@@ -857,6 +1036,14 @@ int aby3g_lr_iteration(const aby3g_lr_iter* it, aby3g_stream stream) {
         K.mn = expand_key(it->mask_next);
         K.otn = expand_key(it->ot_next_key);
         K.otp = expand_key(it->ot_prev_key);
+        if (it->pre_next) {
+            ABY3G_REQUIRE(it->next_rand.t1_next_off % 8 == 0 && it->next_rand.t1_prev_off % 8 == 0 &&
+                              it->next_rand.t2_next_off % 8 == 0 && it->next_rand.t2_prev_off % 8 == 0 &&
+                              it->next_rand.ot_next_off % 8 == 0 && it->next_rand.ot_prev_off % 8 == 0,
+                          "stream offsets must be multiples of 8");
+            K.mp2 = expand_key(it->next_rand.mask_prev);
+            K.mn2 = expand_key(it->next_rand.mask_next);
+        }
         const Layout L(it->B, it->d, it->cir);
         // engine memory, masks, gates, AND wires (padded to 4), level table, batch ends (<= ngates)
         const u64 dynBytes = (2 * (u64)it->cir.wires + it->cir.nand) * L.W * 8 +

@@ -85,6 +85,9 @@ public:
     // producerBytes: HBM bytes of the producing launch (large messages go
     // in-kernel only from light producers)
     aby3g_handoff handoffPost(Gpu& gpu, u64 rows, u64 producerBytes = 0);
+    // Would handoffPost(gpu, rows, producerBytes) hand the next message over
+    // in-kernel? (no side effects; the same answer handoffPost gives)
+    bool handoffWouldPost(const Gpu& gpu, u64 rows, u64 producerBytes = 0) const;
     // Both directions join parties on `gpu`'s device in this process whose
     // ring allows kernel hand-offs (a fused launch may then address the
     // peer's device memory and poll it).

@@ -4,6 +4,10 @@
 
 namespace aby3 {
 
+// defaults of the binary engine's fused forms (A/B-measured)
+constexpr bool kFuseInputsDefault = false;
+constexpr bool kMergeLevelsDefault = false;
+
 void Sh3BinaryEvaluator::setCir(BetaCircuit* cir, u64 width, Sh3ShareGen& gen) {
     block p = gen.getPrevBlock();
     block n = gen.getNextBlock();
@@ -79,6 +83,24 @@ void Sh3BinaryEvaluator::upload(Gpu& g) {
             all.insert(all.end(), o.begin(), o.end());
         }
         const size_t oOut = put(all.data(), all.size() * 4);
+        for (size_t L = 0; L <= c.mLevelCounts.size(); ++L)
+            if ((L < c.mLevelCounts.size() && !c.mLevelBatches[L].empty()) || (L > 0 && c.mLevelAndCounts[L - 1]))
+                d->lastLaunchLevel = L;
+        // fused first level: the inputs' wire range, and who else reads them
+        if (!c.mInputs.empty() && !c.mLevelCounts.empty()) {
+            u32 lo = ~0u, hi = 0;
+            for (const auto& in : c.mInputs)
+                for (u32 w : in) lo = std::min(lo, w), hi = std::max(hi, w + 1);
+            if (lo < hi && hi - lo <= ABY3G_LEVEL_IN_MAX_WIRES) {
+                d->fuseInputs = true;
+                d->inLo = lo;
+                d->inHi = hi;
+                auto isIn = [&](u32 w) { return w >= lo && w < hi; };
+                for (size_t k = c.mLevelCounts[0]; k < c.mLevelGates.size() && !d->inputsReadLater; ++k)
+                    d->inputsReadLater = isIn(c.mLevelGates[k].in0) || isIn(c.mLevelGates[k].in1);
+                for (u32 w : all) d->inputsReadLater = d->inputsReadLater || isIn(w);
+            }
+        }
         d->blob.reset(g, host.size() ? host.size() : 16);
         if (!host.empty()) toDevice(d->blob.data(), host.data(), host.size(), g);
         u8* base = d->blob.as<u8>();
@@ -99,6 +121,9 @@ void Sh3BinaryEvaluator::setCir(BetaCircuit* cir, u64 width, block prevSeed, blo
     mLevel = 0;
     mKeyPrev = prevSeed;
     mKeyNext = nextSeed;
+    mPendingIn.clear();  // held inputs belong to the previous circuit
+    mFuseOut = nullptr;
+    mFuseOutDone = false;
     Gpu& g = Gpu::current();
     mGpu = &g;
     upload(g);
@@ -222,14 +247,67 @@ void Sh3BinaryEvaluator::setInputs(u64 i, const aby3g_rowmap& mi, u64 j, const a
     mLevel = 0;
 }
 
+// ABY3_FUSE_INPUTS=1 / 0 turns the fused first level on / off (A/B runs)
+static bool fuseInputsEnabled() {
+    static const bool on = [] {
+        const char* e = getenv("ABY3_FUSE_INPUTS");
+        return e ? e[0] == '1' : kFuseInputsDefault;
+    }();
+    return on;
+}
+
+void Sh3BinaryEvaluator::flushPendingInputs() {
+    if (mPendingIn.empty()) return;
+    GPU_CALL(aby3g_bits_to_wires_lin(mPendingIn.data(), (u32)mPendingIn.size(), mRows, mWords, mGpu->stream()));
+    mPendingIn.clear();
+}
+
+bool Sh3BinaryEvaluator::pendingCoversInputs() const {
+    if (mPendingIn.empty()) return false;
+    const u64 W = mCir->mWireCount, stride = W * mWords;
+    const u32 n = mCur->inHi - mCur->inLo;
+    std::vector<u8> have(2 * (size_t)n, 0);
+    for (const auto& src : mPendingIn) {
+        const u64 off = (u64)(src.wire_rows - mMem.as<u64>());
+        const u64 sh = off / stride, w = (off % stride) / mWords;
+        for (u64 b = 0; b < src.nbits; ++b)
+            if (w + b >= mCur->inLo && w + b < mCur->inHi) have[2 * (w + b - mCur->inLo) + sh] = 1;
+    }
+    for (const auto& in : mCir->mInputs)
+        for (u32 w : in)
+            if (!have[2 * (w - mCur->inLo)] || !have[2 * (w - mCur->inLo) + 1]) return false;
+    return true;
+}
+
 void Sh3BinaryEvaluator::setInputs(const std::vector<WireInput>& in) {
     if (!mCir) throw RTE_LOC;
     Gpu& g = *mGpu;
     const u64 W = mCir->mWireCount;
     std::vector<aby3g_wire_src> srcs;
+    // Held for the first level's launch when the circuit allows it and every
+    // source is one 64-bit column: the copy-outs (a message, e.g. P0's
+    // reshared value) are made now, the transposes inside that launch.
+    bool defer = fuseInputsEnabled() && mCur->fuseInputs;
+    for (const WireInput& w : in)
+        if (w.input >= mCir->mInputs.size() || mCir->mInputs[w.input].size() > 64) defer = false;
     auto flush = [&] {
         if (srcs.empty()) return;
-        GPU_CALL(aby3g_bits_to_wires_lin(srcs.data(), (u32)srcs.size(), mRows, mWords, g.stream()));
+        if (defer) {
+            GPU_CALL(aby3g_lin_copy_out(srcs.data(), (u32)srcs.size(), mRows, g.stream()));
+            for (auto& s : srcs) {
+                if (s.copy_out) {
+                    // the level reads the copy (one term) instead of its terms again
+                    s.term[0] = s.copy_out;
+                    s.coef[0] = 1;
+                    for (int t = 1; t < 4; ++t) s.term[t] = nullptr, s.coef[t] = 0;
+                }
+                s.copy_out = nullptr;
+                if (mPendingIn.size() == ABY3G_WIRE_SRC_MAX) flushPendingInputs();
+                mPendingIn.push_back(s);
+            }
+        } else {
+            GPU_CALL(aby3g_bits_to_wires_lin(srcs.data(), (u32)srcs.size(), mRows, mWords, g.stream()));
+        }
         srcs.clear();
     };
     for (const WireInput& w : in) {
@@ -352,10 +430,104 @@ void Sh3BinaryEvaluator::setReplicatedInput(u64 i, const sbMatrix& in) {
     mLevel = 0;
 }
 
+// ABY3_MERGE_LEVELS=1 / 0 turns the merged light levels on / off (A/B runs)
+static bool mergeLevelsEnabled() {
+    static const bool on = [] {
+        const char* e = getenv("ABY3_MERGE_LEVELS");
+        return e ? e[0] == '1' : kMergeLevelsDefault;
+    }();
+    return on;
+}
+
+// The rest of the evaluation as one launch (aby3g_bin_levels) when every
+// message from here on goes in-kernel: the parties' decisions agree (the same
+// circuit, rows and channel kinds), so the previous party hands over in-kernel
+// whatever this one receives after the first of these rounds.
+bool Sh3BinaryEvaluator::mergeRest(CommPkg& comm, Gpu& g) {
+    const u64 n = mCir->mLevelCounts.size();
+    if (!mergeLevelsEnabled() || mLevel == 0 || mLevel > n || !mPendingIn.empty()) return false;
+    if (n + 1 - mLevel > ABY3G_LEVELS_MAX) return false;
+    u32 launches = 0;
+    for (u64 L = mLevel; L <= n; ++L) {
+        const bool gates = L < n && mCur->levelBatches[L];
+        const bool unpack = mCir->mLevelAndCounts[L - 1] != 0;
+        launches += gates || unpack;
+        if (L < n && mCir->mLevelAndCounts[L] &&
+            !comm.mNext.handoffWouldPost(g, mRows, (u64)mCir->mLevelCounts[L] * mWords * 72))
+            return false;
+    }
+    if (launches < 2) return false;
+    {
+        // every party's whole (persistent) grid must be resident at once: a
+        // workgroup per CU at most, three parties, besides the stream-op spinners
+        const HandoffResidency& r = handoffResidency(g.device());
+        const u64 chunks = mWords / 32, grid = std::min<u64>(chunks, (u64)r.cus);
+        const int perCu = chunks < (u64)r.smallMaxWgs ? r.perCuSmall : r.perCuLarge;
+        if (3 * grid + (u64)r.otherSpinners > (u64)r.cus * (u64)std::max(0, perCu)) return false;
+    }
+    const u64 rowBytes = mWords * 8;
+    std::vector<aby3g_level_run> runs;
+    std::vector<std::shared_ptr<DeviceBuffer>> recvs;
+    aby3g_handoff hw{nullptr, 0, nullptr};
+    u64* postFlags = nullptr;
+    for (u64 L = mLevel; L <= n; ++L) {
+        aby3g_level_run r{};
+        const u32 nUnpack = mCir->mLevelAndCounts[L - 1];
+        if (nUnpack) {
+            aby3g_handoff h{nullptr, 0, nullptr};
+            auto recv = mRecvFutr.getSharedHandoff(h);
+            if (h.flags) {
+                if (hw.flags && hw.flags != h.flags) throw std::runtime_error("merged levels: hand-off flags differ");
+                hw = h;
+                r.wait_seq = h.seq;
+            } else if (L != mLevel) {
+                throw std::runtime_error("merged levels: a later level's shares arrived by a stream hand-off");
+            }
+            r.nunpack = nUnpack;
+            r.unpack_wires = mCur->outWires[L - 1];
+            r.recv = recv->as<u64>();
+            recvs.push_back(std::move(recv));
+        }
+        if (L < n) {
+            r.first_gate = mCur->levelFirstGate[L];
+            r.batch_off = mCur->levelBatchOffset[L];
+            r.nbatches = mCur->levelBatches[L];
+            const u32 nAnd = mCir->mLevelAndCounts[L];
+            if (nAnd) {
+                if (!mSendAll) mSendAll = std::make_shared<DeviceBuffer>(g, (u64)mCir->mAndCount * rowBytes);
+                auto send = DeviceBuffer::view(mSendAll, mAndDone * rowBytes, nAnd * rowBytes);
+                const aby3g_handoff hp = comm.mNext.handoffPost(g, mRows, (u64)mCir->mLevelCounts[L] * mWords * 72);
+                if (!hp.flags) throw std::runtime_error("merged levels: the post went by a stream hand-off");
+                if (postFlags && postFlags != hp.flags) throw std::runtime_error("merged levels: post flags differ");
+                postFlags = hp.flags;
+                r.send = send->as<u64>();
+                r.post_seq = hp.seq;
+                // in-kernel posts need no stream operation: sent before the launch
+                comm.mNext.asyncSendShared(send, nAnd * rowBytes, g, hp);
+                mRecvFutr = comm.mPrev.asyncRecvShared(nAnd * rowBytes, g);
+                mAndDone += nAnd;
+            }
+        }
+        runs.push_back(r);
+    }
+    if (mZPending) waitZ();
+    const bool out = mFuseOut != nullptr;
+    const u32 nout = out ? (u32)mCir->mOutputs[mFuseOutIdx].size() : 0;
+    GPU_CALL(aby3g_bin_levels(runs.data(), (u32)runs.size(), mCur->gates, mCur->recvRows, mCur->batchEnds,
+                              mMem.as<u64>(), mCir->mWireCount, mWords, mZPtr, hw.flags ? &hw : nullptr, postFlags,
+                              out ? mCur->allOutputWires + mCur->outputOffsets[mFuseOutIdx] : nullptr, nout,
+                              out ? mFuseOut->data() : nullptr, mRows, g.stream()));
+    if (out) mFuseOutDone = true;
+    for (auto& r : recvs) r->fence(g.stream());
+    mLevel = n + 1;
+    return true;
+}
+
 void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
     if (mLevel > mCir->mLevelCounts.size())
         throw std::runtime_error("evaluateRound() was called but no rounds remain... " LOCATION);
     Gpu& g = task.getRuntime().gpu();
+    if (mergeRest(comm, g)) return;  // no rounds left
     const u64 W = mCir->mWireCount;
     const u64 rowBytes = mWords * 8;
     // share 1 of last level's AND outputs arrived from prev (:555-573); they
@@ -389,13 +561,35 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
     // this level's bytes (about 72 per gate and 64-row word)
     if (nAnd) hp = comm.mNext.handoffPost(g, mRows, (u64)mCir->mLevelCounts[mLevel] * mWords * 72);
     if (nb && mZPending) waitZ();
-    if (nb || nUnpack) {
+    // the first level with its inputs (aby3g_bin_level_in) when the held
+    // sources make up every input wire (an input set another way lives in
+    // mMem, which the fused launch does not read for input wires)
+    const bool fused = mLevel == 0 && nb && pendingCoversInputs();
+    if (!fused) flushPendingInputs();
+    if (fused) {
+        GPU_CALL(aby3g_bin_level_in(mPendingIn.data(), (u32)mPendingIn.size(), mRows, mCur->inLo, mCur->inHi,
+                                    mCur->inputsReadLater ? 1 : 0, mCur->gates + mCur->levelFirstGate[0],
+                                    mCur->batchEnds + mCur->levelBatchOffset[0], nb, mMem.as<u64>(), W, mWords, mZPtr,
+                                    send ? send->as<u64>() : nullptr, &hp, g.stream()));
+        mPendingIn.clear();
+    } else if (nb || nUnpack) {
         const aby3g_gate* gl = nb ? mCur->gates + mCur->levelFirstGate[mLevel] : nullptr;
         const u32* be = nb ? mCur->batchEnds + mCur->levelBatchOffset[mLevel] : nullptr;
         const u32* rr = (nb && recv) ? mCur->recvRows + 2 * (u64)mCur->levelFirstGate[mLevel] : nullptr;
-        GPU_CALL(aby3g_bin_level_hs(gl, rr, be, nb, recv ? recv->as<u64>() : nullptr,
-                                    nUnpack ? mCur->outWires[mLevel - 1] : nullptr, nUnpack, mMem.as<u64>(), W, mWords,
-                                    mZPtr, send ? send->as<u64>() : nullptr, &hw, &hp, g.stream()));
+        if (mFuseOut && mLevel == mCur->lastLaunchLevel) {
+            // the last launch also reads the few-bit output out (getOutput)
+            const u32 nout = (u32)mCir->mOutputs[mFuseOutIdx].size();
+            GPU_CALL(aby3g_bin_level_out(gl, rr, be, nb, recv ? recv->as<u64>() : nullptr,
+                                         nUnpack ? mCur->outWires[mLevel - 1] : nullptr, nUnpack, mMem.as<u64>(), W,
+                                         mWords, mZPtr, send ? send->as<u64>() : nullptr, &hw, &hp,
+                                         mCur->allOutputWires + mCur->outputOffsets[mFuseOutIdx], nout,
+                                         mFuseOut->data(), mRows, g.stream()));
+            mFuseOutDone = true;
+        } else {
+            GPU_CALL(aby3g_bin_level_hs(gl, rr, be, nb, recv ? recv->as<u64>() : nullptr,
+                                        nUnpack ? mCur->outWires[mLevel - 1] : nullptr, nUnpack, mMem.as<u64>(), W,
+                                        mWords, mZPtr, send ? send->as<u64>() : nullptr, &hw, &hp, g.stream()));
+        }
     }
 
     if (recv) {
@@ -436,8 +630,21 @@ Sh3Task Sh3BinaryEvaluator::asyncEvaluate(Sh3Task dep, BetaCircuit* cir, Sh3Shar
         });
 }
 
+void Sh3BinaryEvaluator::fuseOutput(u64 i, sbMatrix& out) {
+    if (!mCir || i >= mCir->mOutputs.size()) throw RTE_LOC;
+    mFuseOut = nullptr;
+    mFuseOutDone = false;
+    // the last launch must be a later level's (the first level's fused-input
+    // form has no read-out), the output few-bit
+    if (mCur->lastLaunchLevel == 0 || mCir->mOutputs[i].size() > 8) return;
+    out.resize(mRows, mCir->mOutputs[i].size());
+    mFuseOut = &out;
+    mFuseOutIdx = i;
+}
+
 void Sh3BinaryEvaluator::getOutput(u64 i, sbMatrix& out) {
     if (i >= mCir->mOutputs.size()) throw RTE_LOC;
+    if (mFuseOutDone && i == mFuseOutIdx && &out == mFuseOut) return;  // read out by the last level
     const auto& wires = mCir->mOutputs[i];
     out.resize(mRows, wires.size());
     Gpu& g = *mGpu;

@@ -59,6 +59,11 @@ public:
     Sh3Task asyncEvaluate(Sh3Task dep, BetaCircuit* cir, Sh3ShareGen& gen, std::vector<const sbMatrix*> inputs,
                           std::vector<sbMatrix*> outputs);
     void getOutput(u64 i, sbMatrix& out);
+    // getOutput(i, out) done by the evaluation's last level launch itself
+    // (outputs of at most 8 wires): call before asyncEvaluate; the later
+    // getOutput(i, out) then has nothing left to do. Falls back to the
+    // separate read-out when the circuit does not allow it.
+    void fuseOutput(u64 i, sbMatrix& out);
     // getOutput into mapped rows of an existing `out` (row map(p) <- circuit
     // row p; other rows untouched): the round's scatter
     void getOutput(u64 i, sbMatrix& out, const aby3g_rowmap& map);
@@ -90,6 +95,16 @@ private:
         std::vector<const u32*> outWires;      // per level
         const u32* allOutputWires = nullptr;
         std::vector<u32> outputOffsets;
+        // the first level may take its inputs straight from setInputs'
+        // linear combinations (aby3g_bin_level_in): the input wires' range,
+        // when it spans at most ABY3G_LEVEL_IN_MAX_WIRES, and whether a later
+        // level or an output reads them (then they are written to mMem too)
+        bool fuseInputs = false;
+        u32 inLo = 0, inHi = 0;
+        bool inputsReadLater = false;
+        // the round whose launch is the evaluation's last (a few-bit output
+        // can be read out by it: aby3g_bin_level_out)
+        u64 lastLaunchLevel = 0;
     };
     std::shared_ptr<DevCircuit> mCur;
     Gpu* mGpu = nullptr;
@@ -114,6 +129,14 @@ private:
     // last level, instead of per level
     std::shared_ptr<DeviceBuffer> mSendAll;
     u64 mAndDone = 0;  // AND outputs of the levels already run (their rows in mSendAll)
+    // setInputs' sources held for the first level's launch (DevCircuit::fuseInputs)
+    std::vector<aby3g_wire_src> mPendingIn;
+    sbMatrix* mFuseOut = nullptr;  // fuseOutput's target, output mFuseOutIdx
+    u64 mFuseOutIdx = 0;
+    bool mFuseOutDone = false;
+    void flushPendingInputs();  // writes them to mMem the separate way
+    bool pendingCoversInputs() const;
+    bool mergeRest(CommPkg& comm, Gpu& g);  // the remaining rounds as one launch (aby3g_bin_levels)
     int mZSlot = -1;
     aby3g_stream mZStream = nullptr;     // the stream the masks are drawn on
     std::unique_ptr<Event> mZEv, mZFresh; // draws done / main stream's position for fresh memory

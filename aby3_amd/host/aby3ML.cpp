@@ -49,6 +49,8 @@ struct FusedLr {
     bool sysScope = false;
     u64 epoch = 0;
     u64 d = 0, B = 0;
+    aby3g_lr_rand pred{};   // the next iteration's randomness as predicted by the last step
+    bool havePred = false;
     i64 thrOff[2] = {0, 0}, half = 0, slope = 0, one = 0;
 
     ~FusedLr() {
@@ -198,6 +200,45 @@ struct FusedLr {
         cir.and_wires = reinterpret_cast<const u32*>(base + oA);
     }
 
+    // One iteration's randomness, in the order the op-by-op path takes it.
+    aby3g_lr_rand takeRand(Sh3ShareGen& gen, u64& otNext, u64& otPrev, int p) const {
+        aby3g_lr_rand r{};
+        // mul(XX, w): the truncation pair (Sh3Evaluator.cpp:526-527)
+        r.t1_next_off = gen.takeNext(8 * B);
+        r.t1_prev_off = gen.takePrev(8 * B);
+        // the piecewise circuit's setCir keys (Sh3BinaryEvaluator.h:96-102)
+        const block kp = gen.getPrevBlock(), kn = gen.getNextBlock();
+        std::memcpy(r.mask_prev, kp.data(), 16);
+        std::memcpy(r.mask_next, kn.data(), 16);
+        // region 1: the OT product (Sh3Evaluator.cpp:132-263)
+        if (p == 0) {
+            r.ot_prev_off = gen.takePrev(16 * B);
+            r.ot_next_off = gen.takeNext(8 * B);
+            r.ot_ctr = otNext;
+            otNext += 2 * B;
+        } else if (p == 1) {
+            r.ot_prev_off = gen.takePrev(8 * B);
+        } else {
+            r.ot_next_off = gen.takeNext(16 * B);
+            r.ot_ctr = otPrev;
+            otPrev += 2 * B;
+        }
+        // region 2: the public product (:430-487)
+        r.pm_draw = gen.takeDraws(B);
+        if (p == 0 || p == 1) {
+            r.pm_ctr_next = otNext;
+            otNext += B;
+        }
+        if (p == 0 || p == 2) {
+            r.pm_ctr_prev = otPrev;
+            otPrev += B;
+        }
+        // mulTruncate(XX^T, err): the truncation pair
+        r.t2_next_off = gen.takeNext(8 * d);
+        r.t2_prev_off = gen.takePrev(8 * d);
+        return r;
+    }
+
     void step(aby3ML& ml, const si64Matrix& X, const si64Matrix& Y, si64Matrix& w, const u32* batchIdx, u64 aB,
               u64* phaseTicks) {
         Gpu& g = ml.mRt.gpu();
@@ -230,39 +271,34 @@ struct FusedLr {
         std::memcpy(it.zs_next, gen.mKeyNext.data(), 16);
         std::memcpy(it.ot_next_key, ev.mOtNextKey.data(), 16);
         std::memcpy(it.ot_prev_key, ev.mOtPrevKey.data(), 16);
-        // mul(XX, w): the truncation pair (Sh3Evaluator.cpp:526-527)
-        it.t1_next_off = gen.takeNext(8 * B);
-        it.t1_prev_off = gen.takePrev(8 * B);
-        // the piecewise circuit's setCir keys (Sh3BinaryEvaluator.h:96-102)
-        const block kp = gen.getPrevBlock(), kn = gen.getNextBlock();
-        std::memcpy(it.mask_prev, kp.data(), 16);
-        std::memcpy(it.mask_next, kn.data(), 16);
-        // region 1: the OT product (Sh3Evaluator.cpp:132-263)
-        if (p == 0) {
-            it.ot_prev_off = gen.takePrev(16 * B);
-            it.ot_next_off = gen.takeNext(8 * B);
-            it.ot_ctr = ev.mOtNextIdx;
-            ev.mOtNextIdx += 2 * B;
-        } else if (p == 1) {
-            it.ot_prev_off = gen.takePrev(8 * B);
-        } else {
-            it.ot_next_off = gen.takeNext(16 * B);
-            it.ot_ctr = ev.mOtPrevIdx;
-            ev.mOtPrevIdx += 2 * B;
+        // this iteration's randomness, taken from the party's state exactly as
+        // the op-by-op path takes it
+        const aby3g_lr_rand cur = takeRand(gen, ev.mOtNextIdx, ev.mOtPrevIdx, p);
+        it.t1_next_off = cur.t1_next_off;
+        it.t1_prev_off = cur.t1_prev_off;
+        std::memcpy(it.mask_prev, cur.mask_prev, 16);
+        std::memcpy(it.mask_next, cur.mask_next, 16);
+        it.ot_prev_off = cur.ot_prev_off;
+        it.ot_next_off = cur.ot_next_off;
+        it.ot_ctr = cur.ot_ctr;
+        it.pm_ctr_next = cur.pm_ctr_next;
+        it.pm_ctr_prev = cur.pm_ctr_prev;
+        it.pm_draw = cur.pm_draw;
+        it.t2_next_off = cur.t2_next_off;
+        it.t2_prev_off = cur.t2_prev_off;
+        // Drawn ahead: the previous launch's helpers drew this iteration's
+        // randomness if they predicted it right (nothing else took from the
+        // party's streams in between); this launch's draw the next one's, as
+        // predicted from a copy of the state (the real state is not advanced).
+        it.pre_have = havePred && std::memcmp(&pred, &cur, sizeof cur) == 0;
+        {
+            Sh3ShareGen g2 = gen;
+            u64 on = ev.mOtNextIdx, op = ev.mOtPrevIdx;
+            pred = takeRand(g2, on, op, p);
         }
-        // region 2: the public product (:430-487)
-        it.pm_draw = gen.takeDraws(B);
-        if (p == 0 || p == 1) {
-            it.pm_ctr_next = ev.mOtNextIdx;
-            ev.mOtNextIdx += B;
-        }
-        if (p == 0 || p == 2) {
-            it.pm_ctr_prev = ev.mOtPrevIdx;
-            ev.mOtPrevIdx += B;
-        }
-        // mulTruncate(XX^T, err): the truncation pair
-        it.t2_next_off = gen.takeNext(8 * d);
-        it.t2_prev_off = gen.takePrev(8 * d);
+        it.pre_next = 1;
+        it.next_rand = pred;
+        havePred = true;
         it.thr_off[0] = thrOff[0];
         it.thr_off[1] = thrOff[1];
         it.half = half;

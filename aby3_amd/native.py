@@ -183,6 +183,15 @@ _SIGS = {
     "aby3g_wires_to_bits_map": (c_int, [c_void_p, c_uint64, c_void_p, ctypes.c_uint32, c_uint64, c_void_p, c_uint64,
                                         POINTER(RowMap), c_uint64, c_void_p]),
     "aby3g_bin_unpack": (c_int, [c_void_p, c_void_p, c_uint32, c_void_p, c_uint64, c_uint64, c_void_p]),
+    # aby3g_wire_src / aby3g_level_run arrays and aby3g_handoff go by pointer
+    "aby3g_lin_copy_out": (c_int, [c_void_p, c_uint32, c_uint64, c_void_p]),
+    "aby3g_bin_level_in": (c_int, [c_void_p, c_uint32, c_uint64, c_uint32, c_uint32, c_int, c_void_p, c_void_p,
+                                   c_uint32, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "aby3g_bin_level_out": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_uint32, c_void_p,
+                                    c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint32,
+                                    c_void_p, c_uint64, c_void_p]),
+    "aby3g_bin_levels": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64,
+                                 c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_void_p, c_uint64, c_void_p]),
     "aby3g_bits_to_wires_lin": (c_int, [c_void_p, c_uint32, c_uint64, c_uint64, c_void_p]),
     "aby3g_bits_to_wires": (c_int, [c_void_p, c_uint64, c_uint64, c_uint32, c_void_p, c_uint64, c_void_p]),
     "aby3g_wires_to_bits": (c_int, [c_void_p, c_void_p, c_uint32, c_uint64, c_void_p, c_uint64, c_void_p]),

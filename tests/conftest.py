@@ -3,6 +3,15 @@ import sys
 
 import pytest
 
+# torch (and its HIP runtime) before the in-tree libraries: with both HIP
+# runtimes in one process, loading libaby3gpu.so first and torch later left
+# hipSetDevice without devices on the GPU box (seen when CPU tests that call
+# the host library ran before the first gpu-marked test of a session)
+try:
+    import torch  # noqa: F401
+except ImportError:
+    pass
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

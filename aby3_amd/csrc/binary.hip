@@ -649,21 +649,32 @@ __global__ void __launch_bounds__(SLOTS * 32) k_bin_level_in(LevelInSrcs srcs, u
         if (b < nbits) tab[2 * (wire - inLo + b) + share] = (unsigned short)(k * 64 + b);
     }
     const u64 w0 = (u64)blockIdx.x * kLevelWords;
+    // a wave's words of a source: every load issued before the first
+    // transpose (one memory latency per source, not one per word)
+    constexpr u32 kPer = kLevelWords / kWaves;
 #pragma unroll
     for (u32 k = 0; k < ABY3G_WIRE_SRC_MAX; ++k) {
         if (k >= nsrc) break;
         const LevelInSrc& src = srcs.s[k];
-        for (u32 wl = wave; wl < kLevelWords; wl += kWaves) {
-            const u64 r = (w0 + wl) * 64 + lane64;
-            u64 v = 0;
-            if (r < rows) {
+        u64 v[kPer];
 #pragma unroll
-                for (int t = 0; t < 4; ++t)
-                    if (src.term[t]) v += src.coef[t] * src.term[t][r];
-                v += src.constant;
+        for (u32 i = 0; i < kPer; ++i) v[i] = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const u64* __restrict__ p = src.term[t];
+            if (!p) continue;
+            const u64 cf = src.coef[t];
+#pragma unroll
+            for (u32 i = 0; i < kPer; ++i) {
+                const u64 r = (w0 + wave + i * kWaves) * 64 + lane64;
+                if (r < rows) v[i] += cf * p[r];
             }
-            const u64 tw = transpose64(v, lane64);
-            win[(k * 64 + lane64) * kLevelWords + wl] = tw;  // rows >= nbits: never looked up
+        }
+#pragma unroll
+        for (u32 i = 0; i < kPer; ++i) {
+            const u64 r = (w0 + wave + i * kWaves) * 64 + lane64;
+            const u64 tw = transpose64(r < rows ? v[i] + src.constant : 0, lane64);
+            win[(k * 64 + lane64) * kLevelWords + wave + i * kWaves] = tw;  // rows >= nbits: never looked up
         }
     }
     __syncthreads();
@@ -981,13 +992,28 @@ int aby3g_bin_levels(const aby3g_level_run* runs, uint32_t nruns, const aby3g_ga
         const uint2* rr = reinterpret_cast<const uint2*>(recv_rows);
         static thread_local int cus = 0;
         if (!cus) ABY3G_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, current_device()));
-        const u32 grid = std::min<u32>(chunks, (u32)cus);  // persistent: a workgroup per CU at most
+        // one workgroup per chunk: the levels merged are light (few gates per
+        // level), so 4 gate slots (two waves) suffice and the three parties'
+        // grids fit the device together (mergeRest checks it)
+        (void)cus;
         if (chunks < kLevelSmallMaxWgs)
-            launch(PROBE_BINARY, k_bin_levels<32>, dim3(grid), dim3(32 * 32), 0, S(stream), lr, nruns, chunks, gates, rr,
-                   batch_ends, mem, wires, words, z, hw, post_flags, of);
+            launch(PROBE_BINARY, k_bin_levels<32>, dim3(chunks), dim3(32 * 32), 0, S(stream), lr, nruns, chunks, gates,
+                   rr, batch_ends, mem, wires, words, z, hw, post_flags, of);
         else
-            launch(PROBE_BINARY, k_bin_levels<8>, dim3(grid), dim3(8 * 32), 0, S(stream), lr, nruns, chunks, gates, rr,
-                   batch_ends, mem, wires, words, z, hw, post_flags, of);
+            launch(PROBE_BINARY, k_bin_levels<4>, dim3(chunks), dim3(4 * 32), 0, S(stream), lr, nruns, chunks, gates,
+                   rr, batch_ends, mem, wires, words, z, hw, post_flags, of);
+    });
+}
+
+int aby3g_bin_levels_residency(int* cus, int* per_cu_small, int* per_cu_large, int* small_max_wgs) {
+    return guarded([&] {
+        ABY3G_REQUIRE(cus && per_cu_small && per_cu_large && small_max_wgs, "null argument");
+        ABY3G_CHECK_HIP(hipDeviceGetAttribute(cus, hipDeviceAttributeMultiprocessorCount, current_device()));
+        ABY3G_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            per_cu_small, reinterpret_cast<const void*>(k_bin_levels<32>), 32 * 32, 0));
+        ABY3G_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            per_cu_large, reinterpret_cast<const void*>(k_bin_levels<4>), 4 * 32, 0));
+        *small_max_wgs = (int)kLevelSmallMaxWgs;
     });
 }
 
@@ -1006,9 +1032,7 @@ int aby3g_bin_level_residency(int* cus, int* per_cu_small, int* per_cu_large, in
         *per_cu_small = std::min(a, b);
         ABY3G_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &a, reinterpret_cast<const void*>(k_bin_level<8, true>), 8 * 32, 0));
-        ABY3G_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &b, reinterpret_cast<const void*>(k_bin_levels<8>), 8 * 32, 0));
-        *per_cu_large = std::min(a, b);
+        *per_cu_large = a;
         *small_max_wgs = (int)kLevelSmallMaxWgs;
     });
 }

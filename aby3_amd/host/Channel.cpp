@@ -41,17 +41,34 @@ struct Msg {
     u64 lgen = 0, lseq = 0;
     int ldevice = -1;
     aby3g_ipc_handle lh{};
+    // or, from another process on this GPU, in the sender's arena at larena
+    // offset, published in-kernel with sequence number lseq
+    bool linkInKernel = false;
+    u64 larena = 0;
 };
 
 // a message descriptor on a link's ring (host payloads follow it)
 struct WireMsg {
     u64 bytes;
-    u32 kind;  // 0 host payload, 1 device payload
+    u32 kind;  // 0 host payload, 1 device payload (staged), 2 in-kernel (arena), 3 arena announce
     u32 slot;
-    u64 gen, seq;
-    i64 device;  // the sender's device
+    u64 gen, seq;  // kind 2: gen = offset in the arena's slots; kind 3: gen = slot bytes
+    i64 device;    // the sender's device
     aby3g_ipc_handle handle;
 };
+
+// In-kernel hand-offs between processes sharing one GPU: the sender's arena
+// per direction, [kHandoffChunks flags][2 slots], exported once through IPC
+// at setup (zeroed before its handle leaves). Each evaluation takes the next
+// slot for all its levels' messages (evalSendBuffer), the level kernels write
+// their AND shares there write-through and publish per-chunk flags, and the
+// receiver's level kernels poll the flags and read the shares in place from
+// their mapping. A slot is rewritten two evaluations later: by then the
+// receiver has finished reading it (the ring of three: a party completes
+// evaluation e+1 only with its previous party's e+1 messages, which need the
+// receiver's e+1 messages, which its kernels produce after its kernels that
+// read evaluation e completed).
+constexpr u64 kArenaFlagBytes = 4096;  // kHandoffChunks flags
 constexpr u32 kNoSlot = ~0u;
 
 // a sender's staging slot of a link (device memory exported through IPC)
@@ -122,6 +139,13 @@ struct Pipe {
     };
     std::vector<Closing> closing;  // receiver: openings of replaced slot buffers, closed once `done`
     u64 linkRead = 0;                         // receiver: messages taken off the ring
+    // the arena (sender: own allocation; receiver: its IPC mapping)
+    void* arena = nullptr;
+    u64 arenaSlot = 0;   // bytes per evaluation slot
+    u64 arenaNext = 0;   // sender: slots handed out
+    bool arenaMapped = false;
+    u64* arenaFlags() const { return (u64*)arena; }
+    u8* arenaSlots() const { return (u8*)arena + kArenaFlagBytes; }
     // sender: the ring is written by a thread of its own, in the order the
     // messages were sent, so a send never blocks on the peer's reads: a host
     // payload larger than the ring (4 MiB) then streams through it while the
@@ -192,6 +216,13 @@ struct Pipe {
             for (auto& m : mapped) aby3g_ipc_close(m.second);
             for (auto& c : closing) aby3g_ipc_close(c.ptr);
             closing.clear();
+            if (arena) {
+                if (arenaMapped)
+                    aby3g_ipc_close(arena);
+                else
+                    aby3g_free(arena);  // the receiver's mapping keeps it alive until it closes
+                arena = nullptr;
+            }
             // the peer process may still be copying out of a staging slot:
             // free each buffer once its last message is consumed -- within 10 s
             // in all (a live peer takes milliseconds; one that died, or a
@@ -381,6 +412,15 @@ struct Pipe {
         if (w.kind == 0) {
             m.host.resize(w.bytes);
             if (w.bytes) link->read(m.host.data(), w.bytes);
+        } else if (w.kind == 2) {
+            m.device = true;
+            m.link = true;
+            m.linkInKernel = true;
+            m.larena = w.gen;
+            m.lseq = w.seq;
+            m.ldevice = (int)w.device;
+        } else if (w.kind == 3) {
+            throw std::runtime_error("link: an arena announce after setup");
         } else {
             m.device = true;
             m.link = true;
@@ -512,6 +552,25 @@ std::shared_ptr<DeviceBuffer> RecvFuture::getShared() const {
     std::lock_guard<std::mutex> lk(st.mu);
     if (st.done) return st.out;
     Msg m = st.pipe->pop(st.ticket);
+    if (m.link && m.linkInKernel) {
+        // from another process on this GPU, handed over in-kernel: read in
+        // place from the sender's arena (this process's mapping)
+        if (m.bytes != st.bytes)
+            throw std::runtime_error("channel: message size mismatch (expected " + std::to_string(st.bytes) +
+                                     ", got " + std::to_string(m.bytes) + ")");
+        if (!st.handoff)
+            throw std::runtime_error("channel: a message published in-kernel must be received by a waiting kernel "
+                                     "(RecvFuture::getSharedHandoff)");
+        Pipe& p = *st.pipe;
+        if (!p.arena || m.larena + m.bytes > 2 * p.arenaSlot)
+            throw std::runtime_error("channel: in-kernel message outside the sender's arena");
+        st.out = DeviceBuffer::borrow(p.arenaSlots() + m.larena, std::max<size_t>(m.bytes, 8), st.gpu);
+        st.handoff->flags = p.arenaFlags();
+        st.handoff->seq = m.lseq;
+        st.handoff->wait_ticks = st.gpu->waitTicks();
+        st.done = true;
+        return st.out;
+    }
     if (m.link) {
         // from another process: the payload is copied out of the sender's
         // staging slot into a buffer of this party
@@ -572,10 +631,21 @@ bool Channel::handoffWouldPost(const Gpu& gpu, u64 rows, u64 producerBytes) cons
     return !(chunks > kHandoffChunks || (chunks > kHandoffMaxChunks && producerBytes > kHandoffLightBytes));
 }
 
-aby3g_handoff Channel::handoffPost(Gpu& gpu, u64 rows, u64 producerBytes) {
+aby3g_handoff Channel::handoffPost(Gpu& gpu, u64 rows, u64 producerBytes, const void* payload) {
     if (!mOut) throw std::runtime_error("channel not connected");
     Pipe& p = *mOut;
-    if (!p.kernelHandoff || p.link || p.signalDevice != gpu.device() || kernelsSerialized())
+    if (p.link) {
+        // between processes on one GPU: only a payload in this direction's arena
+        const u8* q = (const u8*)payload;
+        if (!p.arena || kernelsSerialized() || !q || q < p.arenaSlots() || q >= p.arenaSlots() + 2 * p.arenaSlot)
+            return aby3g_handoff{nullptr, 0, nullptr};
+        const u64 chunks = std::max<u64>(1, (rows + ABY3G_HANDOFF_ROWS - 1) / ABY3G_HANDOFF_ROWS);
+        if (!handoffResidencyOk(handoffResidency(gpu.device()), chunks) || chunks > kHandoffChunks ||
+            (chunks > kHandoffMaxChunks && producerBytes > kHandoffLightBytes))
+            return aby3g_handoff{nullptr, 0, nullptr};
+        return aby3g_handoff{p.arenaFlags(), ++p.hsSeq, nullptr};
+    }
+    if (!p.kernelHandoff || p.signalDevice != gpu.device() || kernelsSerialized())
         return aby3g_handoff{nullptr, 0, nullptr};
     if (!p.hsFlags) {
         // First message of this direction: the flags are zeroed on the
@@ -633,6 +703,13 @@ const HandoffResidency& handoffResidency(int device) {
     return byDevice.emplace(device, r).first->second;
 }
 
+std::shared_ptr<DeviceBuffer> Channel::evalSendBuffer(Gpu& gpu, size_t bytes) {
+    if (!mOut || !mOut->link || !mOut->arena || kernelsSerialized() || bytes > mOut->arenaSlot) return nullptr;
+    Pipe& p = *mOut;
+    const u64 slot = p.arenaNext++ & 1;
+    return DeviceBuffer::borrow(p.arenaSlots() + slot * p.arenaSlot, bytes, &gpu);
+}
+
 bool Channel::linkedConcurrent() const {
     return mOut && mIn && mOut->link && mIn->link && !kernelsSerialized();
 }
@@ -644,6 +721,22 @@ void Channel::asyncSendShared(std::shared_ptr<DeviceBuffer> buf, size_t bytes, G
     }
     if (!mOut) throw std::runtime_error("channel not connected");
     if (!buf || buf->bytes() < bytes) throw std::runtime_error("asyncSendShared: buffer smaller than the message");
+    if (mOut->link) {
+        Pipe& p = *mOut;
+        if (posted.flags != p.arenaFlags() || posted.seq != p.hsSeq)
+            throw std::runtime_error("asyncSendShared: the hand-off is not this channel's latest (handoffPost)");
+        std::lock_guard<std::mutex> lk(p.mu);
+        WireMsg w{};
+        w.bytes = bytes;
+        w.kind = 2;
+        w.slot = kNoSlot;
+        w.gen = (u64)((const u8*)buf->data() - p.arenaSlots());
+        w.seq = posted.seq;
+        w.device = gpu.device();
+        p.sent += bytes;
+        p.ringWrite(std::vector<u8>((const u8*)&w, (const u8*)&w + sizeof w));
+        return;
+    }
     if (posted.flags != mOut->hsFlags || posted.seq != mOut->hsSeq)
         throw std::runtime_error("asyncSendShared: the hand-off is not this channel's latest (handoffPost)");
     Msg m;
@@ -771,7 +864,7 @@ std::vector<CommPkg> makeLocalRing(const int* devices, bool kernelHandoff) {
     return c;
 }
 
-CommPkg makeProcessRing(int party, const std::string& link, int device) {
+CommPkg makeProcessRing(int party, const std::string& link, int device, bool sameDevice) {
     if (party < 0 || party > 2) throw std::runtime_error("makeProcessRing: party must be 0, 1 or 2");
     if (link.empty() || link.find('/') != std::string::npos)
         throw std::runtime_error("makeProcessRing: link name must be non-empty without '/'");
@@ -789,6 +882,39 @@ CommPkg makeProcessRing(int party, const std::string& link, int device) {
     for (int a = 0; a < 3; ++a)
         for (int b = 0; b < 3; ++b)
             if (a != b && (a == party || b == party)) pipes[a][b] = end(a, b);
+    if (sameDevice && !kernelsSerialized()) {
+        // the arenas of in-kernel hand-offs: each process announces its two
+        // outgoing ones (zeroed, then exported), then maps the two incoming
+        const char* e = getenv("ABY3_ARENA_MB");
+        const u64 slot = (u64)(e && atoi(e) > 0 ? atoi(e) : 32) << 20;
+        GPU_CALL(aby3g_set_device(device));
+        aby3g_stream tmp = nullptr;  // not the null stream (it would hold a hardware queue)
+        GPU_CALL(aby3g_stream_create(&tmp));
+        for (int to : {nx, pv}) {
+            Pipe& p = *pipes[party][to];
+            GPU_CALL(aby3g_malloc(&p.arena, kArenaFlagBytes + 2 * slot));
+            GPU_CALL(aby3g_memset(p.arena, 0, kArenaFlagBytes, tmp));
+            GPU_CALL(aby3g_stream_sync(tmp));
+            p.arenaSlot = slot;
+            WireMsg w{};
+            w.kind = 3;
+            w.slot = kNoSlot;
+            w.gen = slot;
+            w.device = device;
+            GPU_CALL(aby3g_ipc_get_handle(p.arena, &w.handle));
+            p.ringWrite(std::vector<u8>((const u8*)&w, (const u8*)&w + sizeof w));
+        }
+        GPU_CALL(aby3g_stream_destroy(tmp));
+        for (int from : {pv, nx}) {
+            Pipe& p = *pipes[from][party];
+            WireMsg w;
+            p.link->read(&w, sizeof w);
+            if (w.kind != 3) throw std::runtime_error("makeProcessRing: expected the peer's arena announce");
+            GPU_CALL(aby3g_ipc_open(&w.handle, &p.arena));
+            p.arenaSlot = w.gen;
+            p.arenaMapped = true;
+        }
+    }
     CommPkg c;
     c.mNext = Channel(pipes[party][nx], pipes[nx][party]);
     c.mPrev = Channel(pipes[party][pv], pipes[pv][party]);

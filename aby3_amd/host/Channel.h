@@ -84,7 +84,14 @@ public:
     // asyncSendShared(buf, bytes, gpu, posted): no stream operation.
     // producerBytes: HBM bytes of the producing launch (large messages go
     // in-kernel only from light producers)
-    aby3g_handoff handoffPost(Gpu& gpu, u64 rows, u64 producerBytes = 0);
+    // payload: the message's buffer; between processes it must lie in this
+    // direction's arena (evalSendBuffer) for an in-kernel hand-off
+    aby3g_handoff handoffPost(Gpu& gpu, u64 rows, u64 producerBytes = 0, const void* payload = nullptr);
+    // One party per process on one GPU: a buffer for an evaluation's messages
+    // inside this direction's IPC-mapped arena (two slots, alternating per
+    // call), which the receiver reads in place -- null when the direction has
+    // no arena or `bytes` exceeds a slot (the caller allocates its own).
+    std::shared_ptr<DeviceBuffer> evalSendBuffer(Gpu& gpu, size_t bytes);
     // Would handoffPost(gpu, rows, producerBytes) hand the next message over
     // in-kernel? (no side effects; the same answer handoffPost gives)
     bool handoffWouldPost(const Gpu& gpu, u64 rows, u64 producerBytes = 0) const;
@@ -164,6 +171,8 @@ std::vector<CommPkg> makeLocalRing(const int* devices = nullptr, bool kernelHand
 // Link.h). Blocks until the two other parties have attached. Device payloads
 // are staged in IPC-exported slots and copied out by the receiver; a
 // zero-copy send (asyncSendShared) becomes such a staged copy.
-CommPkg makeProcessRing(int party, const std::string& link, int device);
+// sameDevice: the three processes share this GPU; the binary engine's level
+// messages then go in-kernel through IPC-mapped arenas (one per direction).
+CommPkg makeProcessRing(int party, const std::string& link, int device, bool sameDevice = false);
 
 }  // namespace aby3

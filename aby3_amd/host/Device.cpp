@@ -264,6 +264,15 @@ std::shared_ptr<DeviceBuffer> DeviceBuffer::view(const std::shared_ptr<DeviceBuf
     return v;
 }
 
+std::shared_ptr<DeviceBuffer> DeviceBuffer::borrow(void* ptr, size_t bytes, Gpu* gpu) {
+    auto v = std::make_shared<DeviceBuffer>();
+    v->mGpu = gpu;
+    v->mPtr = ptr;
+    v->mBytes = bytes;
+    v->mFences = std::make_unique<Fences>();
+    return v;
+}
+
 void DeviceBuffer::fence(aby3g_stream s) {
     if (mParent) {
         mParent->fence(s);

@@ -164,6 +164,9 @@ public:
     // alive, and its fences are the parent's (one fence after the last use
     // of any view covers them all)
     static std::shared_ptr<DeviceBuffer> view(const std::shared_ptr<DeviceBuffer>& parent, size_t off, size_t bytes);
+    // memory this buffer does not own (e.g. a region of an IPC-mapped arena):
+    // fence() works, nothing is freed
+    static std::shared_ptr<DeviceBuffer> borrow(void* ptr, size_t bytes, Gpu* gpu);
 
 private:
     struct Fences {

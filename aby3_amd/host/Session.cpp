@@ -689,7 +689,7 @@ aby3h_session* aby3h_party_create(int job, const uint64_t* params, int nparams, 
         s.job = makeJob(job, params, nparams);
         s.locals = {party};
         s.comms.resize(3);
-        s.comms[(size_t)party] = makeProcessRing(party, link, device);
+        s.comms[(size_t)party] = makeProcessRing(party, link, device, colocated != 0);
         s.devices[party] = device;
         s.colocated = colocated != 0;
         s.turnNext = party;  // stream-creation turns: only this party's here

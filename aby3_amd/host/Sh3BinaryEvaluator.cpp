@@ -1,12 +1,14 @@
 #include "Sh3BinaryEvaluator.h"
 #include <cstring>
 #include <map>
+#include <mutex>
 
 namespace aby3 {
 
 // defaults of the binary engine's fused forms (A/B-measured)
-constexpr bool kFuseInputsDefault = false;
+constexpr bool kFuseInputsDefault = true;
 constexpr bool kMergeLevelsDefault = false;
+constexpr bool kFuseOutputDefault = false;
 
 void Sh3BinaryEvaluator::setCir(BetaCircuit* cir, u64 width, Sh3ShareGen& gen) {
     block p = gen.getPrevBlock();
@@ -443,6 +445,23 @@ static bool mergeLevelsEnabled() {
 // message from here on goes in-kernel: the parties' decisions agree (the same
 // circuit, rows and channel kinds), so the previous party hands over in-kernel
 // whatever this one receives after the first of these rounds.
+namespace {
+struct MergedResidency {
+    int cus = 0, perCuSmall = 0, perCuLarge = 0, smallMaxWgs = 0;
+};
+const MergedResidency& mergedResidency(int device) {
+    static std::mutex mu;
+    static std::map<int, MergedResidency> byDevice;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = byDevice.find(device);
+    if (it != byDevice.end()) return it->second;
+    MergedResidency r;
+    GPU_CALL(aby3g_set_device(device));
+    GPU_CALL(aby3g_bin_levels_residency(&r.cus, &r.perCuSmall, &r.perCuLarge, &r.smallMaxWgs));
+    return byDevice.emplace(device, r).first->second;
+}
+}  // namespace
+
 bool Sh3BinaryEvaluator::mergeRest(CommPkg& comm, Gpu& g) {
     const u64 n = mCir->mLevelCounts.size();
     if (!mergeLevelsEnabled() || mLevel == 0 || mLevel > n || !mPendingIn.empty()) return false;
@@ -458,12 +477,12 @@ bool Sh3BinaryEvaluator::mergeRest(CommPkg& comm, Gpu& g) {
     }
     if (launches < 2) return false;
     {
-        // every party's whole (persistent) grid must be resident at once: a
-        // workgroup per CU at most, three parties, besides the stream-op spinners
-        const HandoffResidency& r = handoffResidency(g.device());
-        const u64 chunks = mWords / 32, grid = std::min<u64>(chunks, (u64)r.cus);
+        // every party's whole grid (a workgroup per chunk) must be resident at
+        // once, besides the stream-op spinners
+        const MergedResidency& r = mergedResidency(g.device());
+        const u64 chunks = mWords / 32;
         const int perCu = chunks < (u64)r.smallMaxWgs ? r.perCuSmall : r.perCuLarge;
-        if (3 * grid + (u64)r.otherSpinners > (u64)r.cus * (u64)std::max(0, perCu)) return false;
+        if (3 * chunks + (u64)hwQueuesPerDevice() > (u64)r.cus * (u64)std::max(0, perCu)) return false;
     }
     const u64 rowBytes = mWords * 8;
     std::vector<aby3g_level_run> runs;
@@ -554,12 +573,17 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
     }
     std::shared_ptr<DeviceBuffer> send;
     if (nAnd) {
-        if (!mSendAll) mSendAll = std::make_shared<DeviceBuffer>(g, (u64)mCir->mAndCount * rowBytes);
+        if (!mSendAll) {
+            // between processes on one GPU, the evaluation's messages live in
+            // the channel's IPC-mapped arena, read in place by the receiver
+            mSendAll = comm.mNext.evalSendBuffer(g, (u64)mCir->mAndCount * rowBytes);
+            if (!mSendAll) mSendAll = std::make_shared<DeviceBuffer>(g, (u64)mCir->mAndCount * rowBytes);
+        }
         send = DeviceBuffer::view(mSendAll, mAndDone * rowBytes, nAnd * rowBytes);
     }
     mAndDone += nAnd;
     // this level's bytes (about 72 per gate and 64-row word)
-    if (nAnd) hp = comm.mNext.handoffPost(g, mRows, (u64)mCir->mLevelCounts[mLevel] * mWords * 72);
+    if (nAnd) hp = comm.mNext.handoffPost(g, mRows, (u64)mCir->mLevelCounts[mLevel] * mWords * 72, send->data());
     if (nb && mZPending) waitZ();
     // the first level with its inputs (aby3g_bin_level_in) when the held
     // sources make up every input wire (an input set another way lives in
@@ -630,10 +654,20 @@ Sh3Task Sh3BinaryEvaluator::asyncEvaluate(Sh3Task dep, BetaCircuit* cir, Sh3Shar
         });
 }
 
+// ABY3_FUSE_OUTPUT=1 / 0 turns the last launch's output read-out on / off (A/B runs)
+static bool fuseOutputEnabled() {
+    static const bool on = [] {
+        const char* e = getenv("ABY3_FUSE_OUTPUT");
+        return e ? e[0] == '1' : kFuseOutputDefault;
+    }();
+    return on;
+}
+
 void Sh3BinaryEvaluator::fuseOutput(u64 i, sbMatrix& out) {
     if (!mCir || i >= mCir->mOutputs.size()) throw RTE_LOC;
     mFuseOut = nullptr;
     mFuseOutDone = false;
+    if (!fuseOutputEnabled()) return;
     // the last launch must be a later level's (the first level's fused-input
     // form has no read-out), the output few-bit
     if (mCur->lastLaunchLevel == 0 || mCir->mOutputs[i].size() > 8) return;

@@ -163,6 +163,7 @@ _SIGS = {
     "aby3g_handoff_status": (c_int, [POINTER(ctypes.c_uint32)]),
     "aby3g_set_handoff_timeout_us": (c_int, [c_uint64]),
     "aby3g_bin_level_residency": (c_int, [POINTER(c_int), POINTER(c_int), POINTER(c_int), POINTER(c_int)]),
+    "aby3g_bin_levels_residency": (c_int, [POINTER(c_int), POINTER(c_int), POINTER(c_int), POINTER(c_int)]),
     "aby3g_stream_count": (c_int, [c_int, POINTER(c_int)]),
     "aby3g_malloc_uncached": (c_int, [POINTER(c_void_p), c_size_t]),
     "aby3g_device_uuid": (c_int, [c_int, c_void_p]),

@@ -444,6 +444,8 @@ typedef struct {
     uint64_t* send;
     uint64_t wait_seq, post_seq;
 } aby3g_level_run;
+/* residency of aby3g_bin_levels' two forms (workgroups per CU), as aby3g_bin_level_residency */
+int aby3g_bin_levels_residency(int* cus, int* per_cu_small, int* per_cu_large, int* small_max_wgs);
 int aby3g_bin_levels(const aby3g_level_run* runs, uint32_t nruns, const aby3g_gate* gates, const uint32_t* recv_rows,
                      const uint32_t* batch_ends, uint64_t* mem, uint64_t wires, uint64_t words, const uint64_t* z,
                      const aby3g_handoff* wait, uint64_t* post_flags, const uint32_t* out_wires, uint32_t nout,

@@ -71,7 +71,8 @@ def _party_rank(rank, world, port, exe, q):
     tag = torch.tensor([os.getpid() if rank == 0 else 0], dtype=torch.int64)
     dist.broadcast(tag, 0)
     name = f"g{int(tag.item())}"
-    env = dict(os.environ, ND_ARENA=f"/aby3nd.{name}", ABY3_LINK_TIMEOUT_S="60")
+    # (1 MiB hand-off arenas: the null device's shared memory is a 1 GiB bump allocator)
+    env = dict(os.environ, ND_ARENA=f"/aby3nd.{name}", ABY3_LINK_TIMEOUT_S="60", ABY3_ARENA_MB="1")
     dist.barrier()
     r = subprocess.run([exe, str(rank), name], capture_output=True, text=True, timeout=300, env=env)
     dist.barrier()

@@ -41,7 +41,8 @@ def test_party_processes_sanitized(tmp_path):
     """Three processes, one party each (aby3h_party_create): every job over
     the shared-memory links and IPC staging slots, under AddressSanitizer."""
     exe = _build(str(tmp_path), "address", "party_procs.cpp")
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1", ABY3_LINK_TIMEOUT_S="60")
+    # 1 MiB hand-off arenas: the null device's shared memory is a 1 GiB bump allocator
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1", ABY3_LINK_TIMEOUT_S="60", ABY3_ARENA_MB="1")
     r = subprocess.run([exe], capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
     assert "party_procs: ok" in r.stdout

@@ -19,3 +19,11 @@ for job, params, steps, warm in ((nt.JOB_MSB, [1<<20], 30, 50), (nt.JOB_MUL_TRUN
     ms, outs = bench.party_job(job, params, steps, warmup=warm)
     print(json.dumps(dict(job=job, party_ms=round(ms, 4))))
 " || exit 1
+# share GEMM with A's digit split inside (k_share_gemm16r): parity, then A/B on C2
+ABY3G_GEMM_RAWA=1 timeout -k 10 200 python -u -m pytest -x -q -p no:cacheprovider --timeout 120 --timeout-method thread \
+    tests/test_gpu_kernels.py -m gpu -k "mul_local or mul_trunc_local or digit_extremes or mul_sub" > gpurun_out/r04c_rawa.log 2>&1 \
+    || { tail -30 gpurun_out/r04c_rawa.log; exit 1; }
+tail -1 gpurun_out/r04c_rawa.log
+for i in 1 2 3; do
+  for r in 0 1; do ABY3G_GEMM_RAWA=$r AB_TAG=rawa$r timeout -k 10 120 python scripts/job_timing.py mul 200 || exit 1; done
+done

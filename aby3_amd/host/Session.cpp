@@ -7,6 +7,7 @@
 #include <cmath>
 #include <condition_variable>
 #include <cstdio>
+#include <deque>
 #include <fstream>
 #include <functional>
 #include <numeric>
@@ -45,6 +46,8 @@ struct Job {
     virtual void setup(PartyCtx& p) = 0;
     virtual void step(PartyCtx& p) = 0;
     virtual bool check(PartyCtx&) { return true; }
+    // completes every step issued so far (jobs that keep several in flight)
+    virtual void drain(PartyCtx&) {}
     virtual void info(double* out) = 0;
     // party i's result matrix of the last step (both shares), for digests
     virtual const SharedMat* result(int) const { return nullptr; }
@@ -57,9 +60,19 @@ struct MulJob : Job {
     u64 M, K, N, D;
     MulMode mode;
     bool trunc;
+    // products in flight per party: 1 = each step's product completes before
+    // the next is issued; 2 = step s issues product s, then waits for product
+    // s - 1 (independent products through the runtime's task graph, each
+    // into its own output matrix), so one product's reshare round overlaps
+    // the next one's share GEMM on the party's stream
+    u64 inflight;
     i64Matrix a, b;
-    si64Matrix A[3], B[3], C[3];
-    MulJob(u64 m, u64 k, u64 n, u64 d, MulMode md, bool t) : M(m), K(k), N(n), D(d), mode(md), trunc(t) {
+    si64Matrix A[3], B[3], C[3][2];
+    std::deque<Sh3Task> pending[3];
+    int slot[3] = {0, 0, 0};
+    int last[3] = {0, 0, 0};
+    MulJob(u64 m, u64 k, u64 n, u64 d, MulMode md, bool t, u64 inf = 1)
+        : M(m), K(k), N(n), D(d), mode(md), trunc(t), inflight(inf < 1 ? 1 : inf > 2 ? 2 : inf) {
         const u64 br = mode == MulMode::Gemm ? K : M, bc = mode == MulMode::Gemm ? N : K;
         // fixed-point operands in [-8, 8) * 2^D
         const i64 bound = trunc ? (8ll << D) : 0;
@@ -79,14 +92,28 @@ struct MulJob : Job {
         }
     }
     void step(PartyCtx& p) override {
-        if (trunc)
-            p.eval.asyncMul(p.rt, A[p.idx], B[p.idx], C[p.idx], D, mode).get();
-        else
-            p.eval.asyncMul(p.rt, A[p.idx], B[p.idx], C[p.idx], mode).get();
+        const int i = (int)p.idx;
+        si64Matrix& c = C[i][slot[i]];
+        last[i] = slot[i];
+        slot[i] = (slot[i] + 1) % (int)inflight;
+        pending[i].push_back(trunc ? p.eval.asyncMul(p.rt, A[i], B[i], c, D, mode)
+                                   : p.eval.asyncMul(p.rt, A[i], B[i], c, mode));
+        if (pending[i].size() >= inflight) {
+            pending[i].front().get();
+            pending[i].pop_front();
+        }
+    }
+    void drain(PartyCtx& p) override {
+        auto& q = pending[p.idx];
+        while (!q.empty()) {
+            q.front().get();
+            q.pop_front();
+        }
     }
     bool check(PartyCtx& p) override {
+        drain(p);
         i64Matrix r;
-        p.enc.revealAll(p.rt, C[p.idx], r).get();
+        p.enc.revealAll(p.rt, C[p.idx][last[p.idx]], r).get();
         if (p.idx != 0) return true;
         // spot-check 64 entries against the plaintext product
         u64 x = 99;
@@ -112,7 +139,7 @@ struct MulJob : Job {
         o[ABY3H_INFO_MULTS_PER_STEP] = mode == MulMode::Gemm ? (double)M * N * K : (double)M * N;
         o[ABY3H_INFO_GEMM_INT8_OPS] = mode == MulMode::Gemm ? 144.0 * M * N * K : 0;
     }
-    const SharedMat* result(int i) const override { return &C[i]; }
+    const SharedMat* result(int i) const override { return &C[i][last[i]]; }
 };
 
 // gate-kernel algorithmic bytes per padded word
@@ -548,6 +575,7 @@ struct Session {
                     uint64_t c0 = 0, c1 = 0;
                     aby3g_api_time(&a0, &c0);
                     for (u64 s = 0; s < n; ++s) job->step(p);
+                    job->drain(p);
                     aby3g_api_time(&a1, &c1);
                     hostRecvWaitUs[i] = n ? (recvWaitUs() - w0) / n : 0;
                     hostApiUs[i] = n ? (a1 - a0) / n : 0;
@@ -610,7 +638,7 @@ std::unique_ptr<Job> makeJob(int job, const uint64_t* params, int nparams) {
     switch (job) {
         case ABY3H_JOB_MUL_TRUNC:
             return std::make_unique<MulJob>(P(0, 1024), P(1, 1024), P(2, 1024), P(3, 16),
-                                            P(4, 1) ? MulMode::Gemm : MulMode::Hadamard, true);
+                                            P(4, 1) ? MulMode::Gemm : MulMode::Hadamard, true, P(5, 1));
         case ABY3H_JOB_MUL:
             return std::make_unique<MulJob>(P(0, 128), P(1, 128), P(2, 128), 0, P(3, 0) ? MulMode::Gemm : MulMode::Hadamard,
                                             false);

@@ -432,7 +432,7 @@ __device__ __forceinline__ void lr_predraw(const aby3g_lr_iter& it, const u32* T
 // loads), kLrHelperUnroll rows of a wave in flight.
 constexpr u32 kLrHelperUnroll = 4;
 __device__ __forceinline__ void lr_helper(const u32* T0g, const aby3g_lr_iter& it, const LrKeys& K,
-                                          const HsStatus& status, u64* part, u32* lds, u32* keys) {
+                                          const HsStatus& status, u64* part, u32* lds, u32* keys, bool keepRows) {
     const u32 B = it.B, d = it.d, G = lr_helpers(B), h = blockIdx.x - 1;
     const u32 tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const Layout L(B, d, it.cir);
@@ -446,6 +446,15 @@ __device__ __forceinline__ void lr_helper(const u32* T0g, const aby3g_lr_iter& i
     const u64* w0 = (const u64*)it.w;
     const u64* w1 = w0 + d;
     const u32 R = (B + G - 1) / G, r0 = h * R, r1 = min(B, r0 + R);
+
+    // Phase 4 reads the same rows and columns per lane as phase 1 when each
+    // takes one pass (d <= 128, at most kLrWaves * kLrHelperUnroll rows):
+    // phase 1's loads are then kept in registers for it instead of gathered
+    // from the dataset again after block 0's err arrives.
+    const bool keep = keepRows && d <= 128 && r1 - r0 <= kLrWaves * kLrHelperUnroll;
+    u64x2 k0r[kLrHelperUnroll], k1r[kLrHelperUnroll];
+#pragma unroll
+    for (u32 u = 0; u < kLrHelperUnroll; ++u) k0r[u] = k1r[u] = u64x2{0, 0};
 
     // ---- phase 1 ----
     for (u32 i0 = r0 + wave; i0 < r1; i0 += kLrWaves * kLrHelperUnroll) {
@@ -469,6 +478,13 @@ __device__ __forceinline__ void lr_helper(const u32* T0g, const aby3g_lr_iter& i
 #pragma unroll
             for (u32 u = 0; u < kLrHelperUnroll; ++u)
                 acc[u] += a0[u].x * ws0 + a0[u].y * ws1 + a1[u].x * wa0 + a1[u].y * wa1;
+            if (keep) {
+#pragma unroll
+                for (u32 u = 0; u < kLrHelperUnroll; ++u) {
+                    k0r[u] = a0[u];
+                    k1r[u] = a1[u];
+                }
+            }
         }
 #pragma unroll
         for (u32 u = 0; u < kLrHelperUnroll; ++u) {
@@ -521,9 +537,14 @@ __device__ __forceinline__ void lr_helper(const u32* T0g, const aby3g_lr_iter& i
             for (u32 u = 0; u < kLrHelperUnroll; ++u) {
                 const u32 i = i0 + u * kLrWaves;
                 const bool in = i < r1;
-                const u64 rw = it.batch[in ? i : r0];
-                a0[u] = kin && in ? load_pair(X0 + rw * d + k, pair) : u64x2{0, 0};
-                a1[u] = kin && in ? load_pair(X1 + rw * d + k, pair) : u64x2{0, 0};
+                if (keep) {
+                    a0[u] = kin && in ? k0r[u] : u64x2{0, 0};
+                    a1[u] = kin && in ? k1r[u] : u64x2{0, 0};
+                } else {
+                    const u64 rw = it.batch[in ? i : r0];
+                    a0[u] = kin && in ? load_pair(X0 + rw * d + k, pair) : u64x2{0, 0};
+                    a1[u] = kin && in ? load_pair(X1 + rw * d + k, pair) : u64x2{0, 0};
+                }
                 ev0[u] = in ? hs_load(e0 + i) : 0;  // written by block 0 on another CU
                 evs[u] = in ? ev0[u] + hs_load(e1 + i) : 0;
             }
@@ -985,13 +1006,13 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
 }
 
 __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict__ T0g, aby3g_lr_iter it, LrKeys K,
-                                                           HsStatus status, int memInLds) {
+                                                           HsStatus status, int memInLds, int keepRows) {
     __shared__ u32 lds[kAesLdsWords];
     __shared__ u64 part[kLrThreads];
     __shared__ __attribute__((aligned(16))) u32 keys[kLrKeys * kKeyWords];
     extern __shared__ __attribute__((aligned(16))) u64 dyn[];  // [2][wires][W] engine memory, then [nand][W] masks
     if (blockIdx.x > 0)
-        lr_helper(T0g, it, K, status, part, lds, keys);
+        lr_helper(T0g, it, K, status, part, lds, keys, keepRows != 0);
     else if (memInLds)
         lr_party<true>(T0g, it, K, status, lds, keys, dyn, part);
     else
@@ -1003,6 +1024,16 @@ __global__ void __launch_bounds__(kLrThreads, 1) k_lr_iter(const u32* __restrict
 }  // namespace aby3g
 
 using namespace aby3g;
+
+// ABY3G_LR_KEEP_ROWS=0: the helpers gather their batch rows again for the
+// XX^T err product (A/B runs); default: kept from the XX w product
+static bool keep_rows() {
+    static const bool on = [] {
+        const char* e = getenv("ABY3G_LR_KEEP_ROWS");
+        return !e || e[0] != '0';
+    }();
+    return on;
+}
 
 extern "C" {
 
@@ -1057,7 +1088,7 @@ int aby3g_lr_iteration(const aby3g_lr_iter* it, aby3g_stream stream) {
         ABY3G_REQUIRE(attr || !inLds, "could not raise the fused iteration's dynamic LDS limit");
         // block 0 runs the protocol, blocks 1..G help with the dataset products
         launch(PROBE_OTHER, k_lr_iter, dim3(1 + lr_helpers(it->B)), dim3(kLrThreads), inLds ? dynBytes : 0, S(stream),
-               aes_table(), *it, K, hs_status(), inLds);
+               aes_table(), *it, K, hs_status(), inLds, keep_rows() ? 1 : 0);
     });
 }
 

@@ -84,3 +84,20 @@ def test_lagging_party_many_steps(gpu):
     outs = run_parties(nt.JOB_MUL_TRUNC, [1024, 1024, 1024, 16, 1], 60, "lag", timeout=200, lag_ms=5)
     assert sorted(o["party"] for o in outs) == [0, 1, 2]
     assert all(o["ok"] for o in outs), outs
+
+
+@pytest.mark.parametrize("params", [[1024, 1024, 1024, 16, 1], [257, 200, 250, 8, 1]])
+def test_products_in_flight_share_exact(gpu, params):
+    """MulJob with two products in flight per party (the next product issued
+    before the previous one's reshare round completes, each into its own
+    output): every party's shares of the last product are those of the
+    one-at-a-time run, and the revealed result matches plaintext."""
+    ref = colocated_digests(nt.JOB_MUL_TRUNC, params, 5)
+    with nt.Session(nt.JOB_MUL_TRUNC, params + [2], probe=False) as s:
+        s.run(5)
+        got = [s.digest(p) for p in range(3)]
+        assert s.check()
+    assert got == ref
+    outs = run_parties(nt.JOB_MUL_TRUNC, params + [2], 4, f"inflight_{params[0]}")
+    assert all(o["ok"] for o in outs), outs
+    assert [o["digest"] for o in sorted(outs, key=lambda o: o["party"])] == ref

@@ -26,12 +26,25 @@ __global__ void k_lincomb(u64 n, u64 ca, const i64* __restrict__ a, u64 cb, cons
     }
 }
 
-// Sh3Evaluator.cpp:712-718: C[party] += (za + zb + zo) >> d
+// Sh3Evaluator.cpp:712-718: C[party] += (za + zb + zo) >> d. Two elements a
+// thread (16-byte accesses) when every pointer is 16-byte aligned.
 __global__ void k_trunc_finalize(u64 n, const i64* __restrict__ za, const i64* __restrict__ zb,
                                  const i64* __restrict__ zo, u32 d, i64* __restrict__ c) {
     GRID_STRIDE(i, n) {
         const i64 s = (i64)((u64)za[i] + (u64)zb[i] + (u64)zo[i]);
         c[i] = (i64)((u64)c[i] + (u64)(s >> d));
+    }
+}
+typedef i64 i64x2 __attribute__((ext_vector_type(2)));
+__global__ void k_trunc_finalize2(u64 n2, const i64x2* __restrict__ za, const i64x2* __restrict__ zb,
+                                  const i64x2* __restrict__ zo, u32 d, i64x2* __restrict__ c) {
+    GRID_STRIDE(i, n2) {
+        const i64x2 a = za[i], b = zb[i], o = zo[i];
+        i64x2 v = c[i];
+        const i64 s0 = (i64)((u64)a.x + (u64)b.x + (u64)o.x), s1 = (i64)((u64)a.y + (u64)b.y + (u64)o.y);
+        v.x = (i64)((u64)v.x + (u64)(s0 >> d));
+        v.y = (i64)((u64)v.y + (u64)(s1 >> d));
+        c[i] = v;
     }
 }
 
@@ -124,8 +137,14 @@ int aby3g_trunc_finalize(int party, const int64_t* z_a, const int64_t* z_b, cons
         ABY3G_REQUIRE(party >= 0 && party <= 2, "party out of range");
         ABY3G_REQUIRE(d < 64, "shift too large");
         if (party == 2 || !n) return;  // only P0 and P1 finalize (Sh3Evaluator.cpp:692)
-        launch(PROBE_EPILOGUE, k_trunc_finalize, dim3(ew_grid(n)), dim3(kB), 0, S(stream), n, z_a, z_b, z_own, (u32)d,
-               C + (u64)party * n);
+        i64* c = C + (u64)party * n;
+        auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+        if (n % 2 == 0 && a16(z_a) && a16(z_b) && a16(z_own) && a16(c))
+            launch(PROBE_EPILOGUE, k_trunc_finalize2, dim3(ew_grid(n / 2)), dim3(kB), 0, S(stream), n / 2,
+                   (const i64x2*)z_a, (const i64x2*)z_b, (const i64x2*)z_own, (u32)d, (i64x2*)c);
+        else
+            launch(PROBE_EPILOGUE, k_trunc_finalize, dim3(ew_grid(n)), dim3(kB), 0, S(stream), n, z_a, z_b, z_own,
+                   (u32)d, c);
     });
 }
 

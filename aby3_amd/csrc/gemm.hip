@@ -134,7 +134,7 @@ constexpr u64 kDigitBias = 0x8080808080808080ull;
 // 16 lanes per 256-byte record.
 constexpr u32 kDigitPitch = 272;  // LDS bytes per record image (256 + 16)
 constexpr u32 kDigitRows = 32;    // A rows per A-workgroup
-constexpr u32 kDigitCols = 64;    // B columns per B-workgroup
+constexpr u32 kDigitCols = 64;    // B columns per B-workgroup (the widest form)
 
 // digit-plane words of 4 values: word p = digit p of v0..v3, one byte each
 __device__ __forceinline__ void digit_words(const u64 (&v)[4], u32 (&w)[8]) {
@@ -161,6 +161,7 @@ __device__ __forceinline__ void digit_words(const u64 (&v)[4], u32 (&w)[8]) {
 // 64 columns of B0, B1) -> its records. t in [0, 256); img: 2 * 64 record
 // images. Every thread of the workgroup reaches the one barrier inside, also
 // when `valid` is false.
+template <u32 COLS>
 __device__ __forceinline__ void digit_group(bool valid, u64 gid, u32 t, u8* img, const i64* __restrict__ A0,
                                             const i64* __restrict__ A1, const i64* __restrict__ B0,
                                             const i64* __restrict__ B1, u64 M, u64 K, u64 N, u64 S2, u64 aGroups,
@@ -197,13 +198,13 @@ __device__ __forceinline__ void digit_group(bool valid, u64 gid, u32 t, u8* img,
         nrec = 2 * kDigitRows;
         out = Ad;
     } else {
-        // record (column, half) at image index half * 64 + column
-        r0 = (g / S2) * kDigitCols;
-        const u32 col = t & 63;
+        // record (column, half) at image index half * COLS + column
+        r0 = (g / S2) * COLS;
+        const u32 col = t & (COLS - 1);
         const u64 n = r0 + col;
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const u32 kq = (t >> 6) + 4 * e;
+        for (u32 e = 0; e < 8 * COLS / 256; ++e) {
+            const u32 kq = t / COLS + (256 / COLS) * e;
             u64 vs[4], vb[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -217,14 +218,14 @@ __device__ __forceinline__ void digit_group(bool valid, u64 gid, u32 t, u8* img,
             digit_words(vs, ws);
             digit_words(vb, wb);
             u32* i0 = reinterpret_cast<u32*>(img + col * kDigitPitch) + kq;
-            u32* i1 = reinterpret_cast<u32*>(img + (kDigitCols + col) * kDigitPitch) + kq;
+            u32* i1 = reinterpret_cast<u32*>(img + (COLS + col) * kDigitPitch) + kq;
 #pragma unroll
             for (int p = 0; p < 8; ++p) {
                 i0[8 * p] = ws[p];
                 i1[8 * p] = wb[p];
             }
         }
-        nrec = 2 * kDigitCols;
+        nrec = 2 * COLS;
         out = Bd;
     }
     __syncthreads();
@@ -232,19 +233,32 @@ __device__ __forceinline__ void digit_group(bool valid, u64 gid, u32 t, u8* img,
     // 16 chunks of 16 B per record; record (r, half) -> stage st + half * S2 of row / column r0 + r
     for (u32 c = t; c < nrec * 16; c += 256) {
         const u32 rec = c >> 4, ch = c & 15;
-        const u32 rr = isA ? rec >> 1 : rec & (kDigitCols - 1), half = isA ? rec & 1 : rec / kDigitCols;
+        const u32 rr = isA ? rec >> 1 : rec & (COLS - 1), half = isA ? rec & 1 : rec / COLS;
         const u64 r = r0 + rr, stg = st + half * S2;
         const v4i x = *reinterpret_cast<const v4i*>(img + rec * kDigitPitch + ch * 16);
         *reinterpret_cast<v4i*>(out + (r * stages + stg) * kRec + ch * 16) = x;
     }
 }
 
+// COLS = 32: 64 records per group on both sides (17 KiB of LDS, twice the
+// workgroups resident per CU of the 64-column form)
+template <u32 COLS>
 __global__ void __launch_bounds__(256) k_digits(const i64* __restrict__ A0, const i64* __restrict__ A1,
                                                 const i64* __restrict__ B0, const i64* __restrict__ B1, u64 M,
                                                 u64 K, u64 N, u64 S2, u64 aGroups, u64 stages, u8* __restrict__ Ad,
                                                 u8* __restrict__ Bd) {
-    __shared__ __attribute__((aligned(16))) u8 img[2 * kDigitCols * kDigitPitch];  // record images
-    digit_group(true, blockIdx.x, threadIdx.x, img, A0, A1, B0, B1, M, K, N, S2, aGroups, stages, Ad, Bd);
+    constexpr u32 kRecs = 2 * (COLS > kDigitRows ? COLS : kDigitRows);
+    __shared__ __attribute__((aligned(16))) u8 img[kRecs * kDigitPitch];  // record images
+    digit_group<COLS>(true, blockIdx.x, threadIdx.x, img, A0, A1, B0, B1, M, K, N, S2, aGroups, stages, Ad, Bd);
+}
+
+// ABY3G_DIGIT_COLS=64: the 64-column B-workgroups (A/B runs); default 32
+u32 digit_cols() {
+    static const u32 c = [] {
+        const char* e = getenv("ABY3G_DIGIT_COLS");
+        return e && atoi(e) == 64 ? 64u : 32u;
+    }();
+    return c;
 }
 
 // XCD-aware tile order. Workgroup ids are dealt round-robin to the 8 XCDs
@@ -712,7 +726,7 @@ DigitArgs digit_args(const GemmPlan& p, const i64* A, const i64* B, const Worksp
     da.stages = p.Kc / BK;
     da.S2 = p.Kp / 32;
     da.aGroups = (p.Mp / kDigitRows) * da.S2;
-    da.groups = da.aGroups + (p.Np / kDigitCols) * da.S2;
+    da.groups = da.aGroups + (p.Np / digit_cols()) * da.S2;
     da.Ad = w.Ad;
     da.Bd = w.Bd;
     return da;
@@ -753,8 +767,12 @@ void run_gemm(const GemmPlan& p, const i64* A, const i64* B, const Workspace& w,
     const DigitArgs da = digit_args(p, A, B, w);
     if (raw_a_enabled() && raw_a_fits(p)) {
         // digit pass over B only (aGroups 0), A converted in the GEMM
-        launch(PROBE_DIGITS, k_digits, dim3((u32)(da.groups - da.aGroups)), dim3(256), 0, s, da.A0, da.A1, da.B0,
-               da.B1, p.M, p.K, p.N, da.S2, (u64)0, da.stages, w.Ad, w.Bd);
+        if (digit_cols() == 32)
+            launch(PROBE_DIGITS, k_digits<32>, dim3((u32)(da.groups - da.aGroups)), dim3(256), 0, s, da.A0, da.A1,
+                   da.B0, da.B1, p.M, p.K, p.N, da.S2, (u64)0, da.stages, w.Ad, w.Bd);
+        else
+            launch(PROBE_DIGITS, k_digits<64>, dim3((u32)(da.groups - da.aGroups)), dim3(256), 0, s, da.A0, da.A1,
+                   da.B0, da.B1, p.M, p.K, p.N, da.S2, (u64)0, da.stages, w.Ad, w.Bd);
         const u64 stages = p.Kc / BK;
         const u32 TM = (u32)(p.Mp / p.tbm), TN = (u32)(p.Np / BN);
         const bool direct = p.splits == 1 && out != nullptr;
@@ -764,8 +782,12 @@ void run_gemm(const GemmPlan& p, const i64* A, const i64* B, const Workspace& w,
                p.N, stages, p.kPerSplit / BK, TM, TN, p.splits, direct ? out : w.P, direct ? sub : nullptr);
         return;
     }
-    launch(PROBE_DIGITS, k_digits, dim3((u32)da.groups), dim3(256), 0, s, da.A0, da.A1, da.B0, da.B1, p.M, p.K, p.N,
-           da.S2, da.aGroups, da.stages, w.Ad, w.Bd);
+    if (digit_cols() == 32)
+        launch(PROBE_DIGITS, k_digits<32>, dim3((u32)da.groups), dim3(256), 0, s, da.A0, da.A1, da.B0, da.B1, p.M, p.K,
+               p.N, da.S2, da.aGroups, da.stages, w.Ad, w.Bd);
+    else
+        launch(PROBE_DIGITS, k_digits<64>, dim3((u32)da.groups), dim3(256), 0, s, da.A0, da.A1, da.B0, da.B1, p.M, p.K,
+               p.N, da.S2, da.aGroups, da.stages, w.Ad, w.Bd);
     run_share_gemm(p, w, s, out, sub, subReady);
 }
 

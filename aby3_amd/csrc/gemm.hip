@@ -135,6 +135,7 @@ constexpr u64 kDigitBias = 0x8080808080808080ull;
 constexpr u32 kDigitPitch = 272;  // LDS bytes per record image (256 + 16)
 constexpr u32 kDigitRows = 32;    // A rows per A-workgroup
 constexpr u32 kDigitCols = 64;    // B columns per B-workgroup (the widest form)
+static_assert(BN % kDigitCols == 0, "padded columns are whole B-workgroups");
 
 // digit-plane words of 4 values: word p = digit p of v0..v3, one byte each
 __device__ __forceinline__ void digit_words(const u64 (&v)[4], u32 (&w)[8]) {

@@ -628,6 +628,11 @@ def main():
                                   "Co-located parties plan each GEMM for a third of the chip "
                                   "(aby3g_set_gemm_sharing(3): 128 workgroups of 128x64 tiles, one K split at "
                                   "1024^3), so a launch alone leaves half the CUs to the other parties' kernels",
+            # the launch's own CUs: one 128 x 64 tile per workgroup and CU
+            # (one K split at this size), so the peak it can reach alone is
+            # that share of the chip's
+            "cus_used": min(256, -(-M // 128) * -(-N // 64)),
+            "frac_of_cus_used": achieved_tops / (PEAK_INT8_TOPS * min(256, -(-M // 128) * -(-N // 64)) / 256),
             "job_mfma_rate": info["gemm_int8_ops"] * 3 / (dt / args.steps) / 1e12,
             "job_mfma_rate_unit": "TOP/s: the three parties' share-GEMM int8 ops per step / the whole step",
             "launch_span_ms_overlapped": ovl_ms / max(ovl_n, 1),

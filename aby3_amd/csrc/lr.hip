@@ -570,6 +570,20 @@ __device__ __forceinline__ void lr_helper(const u32* T0g, const aby3g_lr_iter& i
         __syncthreads();
     }
     lr_arrive(box, F_H2);
+    // the next iteration's rows into this XCD's L2 (its helper h is a
+    // workgroup of the same id, dealt to the same XCD)
+    if (it.next_batch) {
+        const u32 k = 2 * lane;
+        if (k < d) {
+            u64 sink = 0;
+            for (u32 i = r0 + wave; i < r1; i += kLrWaves) {
+                const u64 rw = it.next_batch[i];
+                const u64x2 a0 = load_pair(X0 + rw * d + k, k + 1 < d), a1 = load_pair(X1 + rw * d + k, k + 1 < d);
+                sink ^= a0.x ^ a1.x;
+            }
+            asm volatile("" ::"v"(sink));  // the loads are kept; nothing waits for them
+        }
+    }
 }
 
 // phase stamps for profiling (aby3g_lr_iter.phase_ticks): wall clock of slot s

@@ -290,6 +290,15 @@ struct BitInjJob : Job {
 // construction and kept resident (an iteration is the protocol alone);
 // sample = 1: every step draws its batch with getSubset inside the step
 // (DeviceBatchSampler), as SGD_Logistic's loop does (Regression.h:249-253).
+// ABY3_LR_PREFETCH=0: no prefetch of the next batch's rows (A/B runs)
+static bool nextBatchPrefetch() {
+    static const bool on = [] {
+        const char* e = getenv("ABY3_LR_PREFETCH");
+        return !e || e[0] != '0';
+    }();
+    return on;
+}
+
 struct LrJob : Job {
     static constexpr u64 kBatches = 8192;  // mini-batches precomputed (and resident) per session
     u64 n, d, B, D, aB, sample;
@@ -349,6 +358,8 @@ struct LrJob : Job {
         } else {
             if (t >= kBatches) throw std::runtime_error("lr job: more iterations than precomputed mini-batches");
             idx = dbatch[p.idx].as<u32>() + t * B;
+            // resident batches: the next one is known (its rows prefetched)
+            st[p.idx].nextBatch = t + 1 < kBatches && nextBatchPrefetch() ? idx + B : nullptr;
         }
         sgdLogisticStep(*ml[p.idx], sX[p.idx], sY[p.idx], sW[p.idx], idx, B, aB, st[p.idx]);
     }

@@ -240,7 +240,7 @@ struct FusedLr {
     }
 
     void step(aby3ML& ml, const si64Matrix& X, const si64Matrix& Y, si64Matrix& w, const u32* batchIdx, u64 aB,
-              u64* phaseTicks) {
+              u64* phaseTicks, const u32* nextBatch) {
         Gpu& g = ml.mRt.gpu();
         Sh3Evaluator& ev = ml.mEval;
         Sh3ShareGen& gen = ev.mShareGen;
@@ -256,6 +256,7 @@ struct FusedLr {
         it.Y = Y.data();
         it.w = w.data();
         it.batch = batchIdx;
+        it.next_batch = nextBatch;
         it.cir = cir;
         it.scratch = scratch.data();
         it.mailbox = ownBox ? ownBox : mailbox.data();
@@ -318,7 +319,7 @@ void sgdLogisticStep(aby3ML& ml, const si64Matrix& X, const si64Matrix& Y, si64M
         st.fusedChecked = true;
     }
     if (st.fused && st.fused->B == B && st.fused->d == X.cols()) {
-        st.fused->step(ml, X, Y, w, batchIdx, aB, st.phaseTicks);
+        st.fused->step(ml, X, Y, w, batchIdx, aB, st.phaseTicks, st.nextBatch);
         return;
     }
     sgdLogisticStepOps(ml, X, Y, w, batchIdx, B, aB, st);

@@ -40,6 +40,7 @@ struct SgdState {
     std::shared_ptr<FusedLr> fused;
     bool fusedChecked = false;
     u64* phaseTicks = nullptr;  // optional device [32]: the fused launch's phase stamps (profiling)
+    const u32* nextBatch = nullptr;  // optional: the next iteration's batch (its rows prefetched into L2)
 };
 
 // One SGD_Logistic iteration on the batch of B row indices at device pointer

@@ -634,6 +634,10 @@ typedef struct {
      * one runs. */
     uint32_t pre_have, pre_next;
     aby3g_lr_rand next_rand;
+    /* optional: the next iteration's batch (B row ids). The helpers touch its
+     * dataset rows after their last product, so that the next launch's
+     * helpers (the same workgroup ids, so the same XCDs) find them in L2. */
+    const uint32_t* next_batch;
 } aby3g_lr_iter;
 uint64_t aby3g_lr_mailbox_bytes(uint32_t B, uint32_t d, const aby3g_lr_circuit* cir);
 uint64_t aby3g_lr_scratch_bytes(uint32_t B, uint32_t d, const aby3g_lr_circuit* cir);

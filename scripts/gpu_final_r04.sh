@@ -2,7 +2,7 @@
 # round-4 final evidence on the final tree: pytest -m gpu, smoke, the
 # driver's bench command and the default one, kernel trace + PMC passes
 R=$GRAFT_REPO_ROOT
-TAG=r04b
+TAG=${1:-r04c}
 cd $R && mkdir -p gpurun_out/$TAG
 timeout -k 10 500 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/$TAG/pytest_gpu.log 2>&1 || { grep -E "FAILED|Error" gpurun_out/$TAG/pytest_gpu.log | head -20; tail -3 gpurun_out/$TAG/pytest_gpu.log; exit 1; }
 tail -1 gpurun_out/$TAG/pytest_gpu.log

@@ -25,8 +25,11 @@ extern "C" {
 typedef struct aby3h_session aby3h_session;
 
 enum {
-    /* params: M, K, N, D, mode (1 GEMM, 0 Hadamard). One step = one
-     * Sh3Evaluator::asyncMul(A, B, C, D) with truncation (Sh3Evaluator.cpp:651-730). */
+    /* params: M, K, N, D, mode (1 GEMM, 0 Hadamard)[, inflight]. One step = one
+     * Sh3Evaluator::asyncMul(A, B, C, D) with truncation (Sh3Evaluator.cpp:651-730).
+     * inflight 2: step s issues product s (into one of two output matrices)
+     * and then waits for product s - 1, so the runtime holds two independent
+     * products; the run's last one completes when the run ends. */
     ABY3H_JOB_MUL_TRUNC = 0,
     /* params: M, K, N, mode. One step = asyncMul without truncation (:92-116). */
     ABY3H_JOB_MUL = 1,

@@ -69,3 +69,45 @@ def test_rocprof_summary_agrees_with_bench_launch_time():
             avg_ms = float(row["AverageNs"]) / 1e6
     assert avg_ms is not None, "no share-GEMM row in " + stats
     assert avg_ms == pytest.approx(d["roofline"]["launch_ms"], rel=0.1)
+
+
+def _pmc_summary():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("pmc_summary", os.path.join(ROOT, "scripts", "pmc_summary.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def _latest_with(pattern):
+    files = [f for f in glob.glob(os.path.join(PROFILES, pattern))
+             if re.search(r"r(\d+)([a-z]?)", os.path.basename(f))]
+    if not files:
+        pytest.skip("no " + pattern)
+    key = lambda f: (lambda m: (int(m.group(1)), m.group(2)))(re.search(r"r(\d+)([a-z]?)", os.path.basename(f)))
+    return max(files, key=key)
+
+
+def test_binary_traffic_sums_every_level_kernel():
+    """The binary roofline's traffic (pmc_*.json bin_gates) is the sum of every
+    gate-level kernel's PMC bytes: each k_bin_* kernel the committed kernel
+    stats name is counted by pmc_summary.py and present in the PMC table."""
+    ps = _pmc_summary()
+    pmc_path = _latest_with("pmc_r*.json")
+    pmc = json.load(open(pmc_path))
+    if "msb" not in pmc.get("kernels", {}):
+        pytest.skip("no msb kernel table in " + pmc_path)
+    table = pmc["kernels"]["msb"]
+    tag = re.search(r"pmc_(r\d+[a-z]?)\.json", os.path.basename(pmc_path)).group(1)
+    stats = os.path.join(PROFILES, tag + "_kernel_stats.csv")
+    if os.path.exists(stats):
+        for row in csv.DictReader(open(stats)):
+            m = re.search(r"\b(k_bin_[A-Za-z0-9_]+)", row["Name"])
+            if m:
+                assert ps.is_level_kernel(m.group(1)), m.group(1) + " is a gate kernel the traffic sum leaves out"
+                assert m.group(1) in table, m.group(1) + " has no PMC bytes in " + pmc_path
+    want = sum(v["read_bytes"] + v["write_bytes"] for k, v in table.items() if k.startswith("k_bin_"))
+    assert want > 0
+    # 4 profiled steps of three parties (scripts/gpu_profile.sh)
+    assert pmc["bin_gates"]["hbm_bytes_per_step_per_party"] == pytest.approx(want / 12, rel=1e-9)
+    assert ps.bin_level_bytes(table) == pytest.approx(want, rel=1e-12)

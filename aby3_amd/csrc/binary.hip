@@ -147,16 +147,6 @@ constexpr u32 kLevelUnroll = 4;
 // publishes its own send rows for the next party's same workgroup (hp) --
 // the levels of the three parties pipeline chunk by chunk.
 static_assert(kLevelWords * 64 == ABY3G_HANDOFF_ROWS, "a level workgroup is one hand-off chunk");
-// The circuit's few-bit output fused into its last level (aby3g_bin_level_out):
-// after the gates, a thread per (share, row) of the workgroup's chunk gathers
-// bit (row & 63) of each output wire's word, as k_w2b_few does.
-struct OutFuse {
-    const u32* wires;  // nbits output wires; nbits == 0: none
-    u32 nbits;
-    i64* out;          // [2][rows] (one column)
-    u64 rows;
-};
-
 template <u32 SLOTS, bool HS>
 __global__ void __launch_bounds__(SLOTS * 32) k_bin_level(const aby3g_gate* __restrict__ gates,
                                                          const uint2* __restrict__ rrows,
@@ -165,7 +155,7 @@ __global__ void __launch_bounds__(SLOTS * 32) k_bin_level(const aby3g_gate* __re
                                                          const u32* __restrict__ unpack_wires, u32 nunpack,
                                                          u64* __restrict__ mem, u64 wires, u64 words,
                                                          const u64* __restrict__ z, u64* __restrict__ sendbuf,
-                                                         HsWait hw, HsPost hp, OutFuse of) {
+                                                         HsWait hw, HsPost hp) {
     // HS: the in-kernel hand-off instantiation (sc1 payload accesses, waits
     // and posts); the other is the plain streaming kernel
     if (HS && !hs_wait(hw, blockIdx.x, blockIdx.x + 1)) return;
@@ -200,114 +190,6 @@ __global__ void __launch_bounds__(SLOTS * 32) k_bin_level(const aby3g_gate* __re
         begin = end;
     }
     if (HS) hs_post(hp, blockIdx.x, blockIdx.x + 1);
-    if (of.nbits) {
-        __syncthreads();
-        for (u32 k = threadIdx.x; k < 2 * kLevelWords * 64; k += SLOTS * 32) {
-            const u32 sh = k / (kLevelWords * 64);
-            const u64 r = (u64)blockIdx.x * kLevelWords * 64 + (k % (kLevelWords * 64));
-            if (r >= of.rows) continue;
-            const u64* m = sh ? s1 : s0;
-            const u64 wr = r >> 6;
-            const u32 bit = (u32)(r & 63);
-            u64 v = 0;
-            for (u32 j = 0; j < of.nbits; ++j) v |= ((m[(u64)of.wires[j] * words + wr] >> bit) & 1ull) << j;
-            of.out[(u64)sh * of.rows + r] = (i64)v;
-        }
-    }
-}
-
-// Several consecutive levels in one launch (aby3g_bin_levels), every message
-// between them handed over in-kernel: a workgroup carries its chunk through
-// the levels -- wait for the previous party's same chunk of the previous
-// level, unpack, this level's batches, publish its send rows -- so the three
-// parties' launches pipeline chunk by chunk and level by level with no launch
-// boundary between levels. Level descriptors are kernel arguments.
-struct LevelRun {
-    u32 first_gate, batch_off, nbatches, nunpack;
-    const u32* unpack_wires;
-    const u64* recv;  // the previous level's AND shares, or null
-    u64* send;        // this level's send rows, or null
-    u64 wait_seq;     // 0: nothing to wait for (none received, or a stream hand-off before the launch)
-    u64 post_seq;     // 0: nothing sent
-};
-constexpr u32 kMaxRuns = ABY3G_LEVELS_MAX;
-struct LevelRuns {
-    LevelRun l[kMaxRuns];
-};
-
-// A persistent grid: at most one workgroup per CU per party (the three
-// parties' grids are then resident together whatever else runs, so no
-// workgroup spins waiting for a peer's workgroup that has no slot); each
-// carries its chunks c = blockIdx.x + k gridDim.x level by level.
-template <u32 SLOTS>
-__global__ void __launch_bounds__(SLOTS * 32) k_bin_levels(LevelRuns runs, u32 nruns, u32 nchunks,
-                                                          const aby3g_gate* __restrict__ gates,
-                                                          const uint2* __restrict__ rrows,
-                                                          const u32* __restrict__ batch_ends, u64* __restrict__ mem,
-                                                          u64 wires, u64 words, const u64* __restrict__ z, HsWait hw,
-                                                          u64* postFlags, OutFuse of) {
-    const u32 lane = threadIdx.x & 31, slot = threadIdx.x >> 5;
-    u64* s0 = mem;
-    u64* s1 = mem + wires * words;
-#pragma unroll 1
-    for (u32 li = 0; li < nruns; ++li) {
-        const LevelRun& L = runs.l[li];
-        const u64* __restrict__ recv = L.recv;
-        const uint2* rr0 = (rrows && recv) ? rrows + L.first_gate : nullptr;
-        const aby3g_gate* gl = gates + L.first_gate;
-        const u32* be = batch_ends + L.batch_off;
-#pragma unroll 1
-        for (u32 c = blockIdx.x; c < nchunks; c += gridDim.x) {
-            const u64 w = (u64)c * kLevelWords + lane;
-            if (L.wait_seq) {
-                HsWait h = hw;
-                h.seq = L.wait_seq;
-                if (!hs_wait(h, c, c + 1)) return;
-            }
-#pragma unroll 4
-            for (u32 j = slot; j < L.nunpack; j += SLOTS)
-                s1[(u64)L.unpack_wires[j] * words + w] = hs_load(recv + (u64)j * words + w);
-            u32 begin = 0;
-            for (u32 b = 0; b < L.nbatches; ++b) {
-                if (b || !rr0) __syncthreads();
-                const u32 end = be[b];
-                for (u32 g0 = begin + slot; g0 < end; g0 += kLevelUnroll * SLOTS) {
-                    aby3g_gate g[kLevelUnroll];
-                    uint2 rr[kLevelUnroll];
-                    GateOps o[kLevelUnroll];
-#pragma unroll
-                    for (u32 k = 0; k < kLevelUnroll; ++k)
-                        if (g0 + k * SLOTS < end) {
-                            g[k] = gl[g0 + k * SLOTS];
-                            rr[k] = rr0 ? rr0[g0 + k * SLOTS] : make_uint2(~0u, ~0u);
-                        }
-#pragma unroll
-                    for (u32 k = 0; k < kLevelUnroll; ++k)
-                        if (g0 + k * SLOTS < end) gate_load(g[k], rr[k], s0, s1, recv, words, w, z, o[k], true);
-#pragma unroll
-                    for (u32 k = 0; k < kLevelUnroll; ++k)
-                        if (g0 + k * SLOTS < end) gate_eval(g[k], o[k], s0, s1, words, w, L.send, true);
-                }
-                begin = end;
-            }
-            if (L.post_seq) hs_post(HsPost{postFlags, L.post_seq}, c, c + 1);
-            __syncthreads();  // the next chunk / level: this one's words are done
-        }
-    }
-    if (of.nbits) {
-        for (u32 c = blockIdx.x; c < nchunks; c += gridDim.x)
-            for (u32 k = threadIdx.x; k < 2 * kLevelWords * 64; k += SLOTS * 32) {
-                const u32 sh = k / (kLevelWords * 64);
-                const u64 r = (u64)c * kLevelWords * 64 + (k % (kLevelWords * 64));
-                if (r >= of.rows) continue;
-                const u64* m = sh ? s1 : s0;
-                const u64 wr = r >> 6;
-                const u32 bit = (u32)(r & 63);
-                u64 v = 0;
-                for (u32 j = 0; j < of.nbits; ++j) v |= ((m[(u64)of.wires[j] * words + wr] >> bit) & 1ull) << j;
-                of.out[(u64)sh * of.rows + r] = (i64)v;
-            }
-    }
 }
 
 __global__ void __launch_bounds__(kGateBlock) k_bin_unpack(const u64* __restrict__ recv, const u32* __restrict__ outw,
@@ -897,16 +779,14 @@ int aby3g_bin_level_rr(const aby3g_gate* gates, const uint32_t* recv_rows, const
 static int bin_level(const aby3g_gate* gates, const uint32_t* recv_rows, const uint32_t* batch_ends,
                      uint32_t nbatches, const uint64_t* recvbuf, const uint32_t* unpack_wires, uint32_t nunpack,
                      uint64_t* mem, uint64_t wires, uint64_t words, const uint64_t* z, uint64_t* sendbuf,
-                     const aby3g_handoff* wait, const aby3g_handoff* post, const OutFuse& of, aby3g_stream stream) {
+                     const aby3g_handoff* wait, const aby3g_handoff* post, aby3g_stream stream) {
     const uint2* rrows = reinterpret_cast<const uint2*>(recv_rows);
     return guarded([&] {
-        ABY3G_REQUIRE(of.nbits <= 64 && (!of.nbits || (of.wires && of.out && of.rows <= words * 64)),
-                      "fused output: at most 64 wires, rows within the engine's words");
         ABY3G_REQUIRE(!rrows || recvbuf, "recv_rows without a recv buffer");
         ABY3G_REQUIRE(words % kLevelWords == 0, "words must be padded to a multiple of 32 (2048 rows)");
         ABY3G_REQUIRE(!(wait && wait->flags) || nunpack, "a hand-off wait without received shares");
         ABY3G_REQUIRE(!(post && post->flags) || sendbuf, "a hand-off post without a send buffer");
-        if ((!nbatches && !nunpack && !of.nbits) || !words) return;
+        if ((!nbatches && !nunpack) || !words) return;
         // one workgroup per chunk; in-kernel hand-offs are used only for
         // launches of at most 64 chunks, or 512 from a light producer
         // (Channel::handoffPost), so the spinning workgroups of two parties'
@@ -922,17 +802,17 @@ static int bin_level(const aby3g_gate* gates, const uint32_t* recv_rows, const u
         if (wgs < kLevelSmallMaxWgs) {
             if (hs)
                 launch(PROBE_BINARY, k_bin_level<32, true>, dim3(wgs), dim3(32 * 32), 0, S(stream), gates, rrows,
-                       batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp, of);
+                       batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp);
             else
                 launch(PROBE_BINARY, k_bin_level<32, false>, dim3(wgs), dim3(32 * 32), 0, S(stream), gates, rrows,
-                       batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp, of);
+                       batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp);
         } else {
             if (hs)
                 launch(PROBE_BINARY, k_bin_level<8, true>, dim3(wgs), dim3(8 * 32), 0, S(stream), gates, rrows,
-                       batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp, of);
+                       batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp);
             else
                 launch(PROBE_BINARY, k_bin_level<8, false>, dim3(wgs), dim3(8 * 32), 0, S(stream), gates, rrows,
-                       batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp, of);
+                       batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp);
         }
     });
 }
@@ -942,79 +822,7 @@ int aby3g_bin_level_hs(const aby3g_gate* gates, const uint32_t* recv_rows, const
                        uint64_t* mem, uint64_t wires, uint64_t words, const uint64_t* z, uint64_t* sendbuf,
                        const aby3g_handoff* wait, const aby3g_handoff* post, aby3g_stream stream) {
     return bin_level(gates, recv_rows, batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z,
-                     sendbuf, wait, post, OutFuse{nullptr, 0, nullptr, 0}, stream);
-}
-
-int aby3g_bin_level_out(const aby3g_gate* gates, const uint32_t* recv_rows, const uint32_t* batch_ends,
-                        uint32_t nbatches, const uint64_t* recvbuf, const uint32_t* unpack_wires, uint32_t nunpack,
-                        uint64_t* mem, uint64_t wires, uint64_t words, const uint64_t* z, uint64_t* sendbuf,
-                        const aby3g_handoff* wait, const aby3g_handoff* post, const uint32_t* out_wires,
-                        uint32_t nout, int64_t* out, uint64_t rows, aby3g_stream stream) {
-    return bin_level(gates, recv_rows, batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z,
-                     sendbuf, wait, post, OutFuse{out_wires, nout, out, rows}, stream);
-}
-
-int aby3g_bin_levels(const aby3g_level_run* runs, uint32_t nruns, const aby3g_gate* gates, const uint32_t* recv_rows,
-                     const uint32_t* batch_ends, uint64_t* mem, uint64_t wires, uint64_t words, const uint64_t* z,
-                     const aby3g_handoff* wait, uint64_t* post_flags, const uint32_t* out_wires, uint32_t nout,
-                     int64_t* out, uint64_t rows, aby3g_stream stream) {
-    return guarded([&] {
-        ABY3G_REQUIRE(nruns <= kMaxRuns, "too many levels for one launch");
-        ABY3G_REQUIRE(words % kLevelWords == 0, "words must be padded to a multiple of 32 (2048 rows)");
-        ABY3G_REQUIRE(nout <= 64 && (!nout || (out_wires && out && rows <= words * 64)), "fused output");
-        if (!nruns || !words) return;
-        LevelRuns lr{};
-        bool waits = false;
-        for (u32 i = 0; i < nruns; ++i) {
-            const aby3g_level_run& r = runs[i];
-            ABY3G_REQUIRE(!r.nunpack || r.recv, "received shares without a buffer");
-            ABY3G_REQUIRE(!r.post_seq || (r.send && post_flags), "a post without a send buffer or flags");
-            ABY3G_REQUIRE(!r.wait_seq || (r.nunpack && wait && wait->flags), "a wait without received shares");
-            ABY3G_REQUIRE(!r.wait_seq || i == 0 || r.wait_seq > runs[i - 1].wait_seq, "wait sequence numbers");
-            // a level after the first receives only in-kernel (a stream wait
-            // cannot sit inside the launch)
-            ABY3G_REQUIRE(i == 0 || !r.nunpack || r.wait_seq, "a later level's shares must be handed over in-kernel");
-            LevelRun& d = lr.l[i];
-            d.first_gate = r.first_gate;
-            d.batch_off = r.batch_off;
-            d.nbatches = r.nbatches;
-            d.nunpack = r.nunpack;
-            d.unpack_wires = r.unpack_wires;
-            d.recv = r.recv;
-            d.send = r.send;
-            d.wait_seq = r.wait_seq;
-            d.post_seq = r.post_seq;
-            waits = waits || r.wait_seq;
-        }
-        const HsWait hw = waits ? hs_wait_arg(wait) : HsWait{nullptr, 0, nullptr, HsStatus{nullptr, 0, 0}};
-        const u32 chunks = (u32)(words / kLevelWords);
-        const OutFuse of{out_wires, nout, out, rows};
-        const uint2* rr = reinterpret_cast<const uint2*>(recv_rows);
-        static thread_local int cus = 0;
-        if (!cus) ABY3G_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, current_device()));
-        // one workgroup per chunk: the levels merged are light (few gates per
-        // level), so 4 gate slots (two waves) suffice and the three parties'
-        // grids fit the device together (mergeRest checks it)
-        (void)cus;
-        if (chunks < kLevelSmallMaxWgs)
-            launch(PROBE_BINARY, k_bin_levels<32>, dim3(chunks), dim3(32 * 32), 0, S(stream), lr, nruns, chunks, gates,
-                   rr, batch_ends, mem, wires, words, z, hw, post_flags, of);
-        else
-            launch(PROBE_BINARY, k_bin_levels<4>, dim3(chunks), dim3(4 * 32), 0, S(stream), lr, nruns, chunks, gates,
-                   rr, batch_ends, mem, wires, words, z, hw, post_flags, of);
-    });
-}
-
-int aby3g_bin_levels_residency(int* cus, int* per_cu_small, int* per_cu_large, int* small_max_wgs) {
-    return guarded([&] {
-        ABY3G_REQUIRE(cus && per_cu_small && per_cu_large && small_max_wgs, "null argument");
-        ABY3G_CHECK_HIP(hipDeviceGetAttribute(cus, hipDeviceAttributeMultiprocessorCount, current_device()));
-        ABY3G_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            per_cu_small, reinterpret_cast<const void*>(k_bin_levels<32>), 32 * 32, 0));
-        ABY3G_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            per_cu_large, reinterpret_cast<const void*>(k_bin_levels<4>), 4 * 32, 0));
-        *small_max_wgs = (int)kLevelSmallMaxWgs;
-    });
+                     sendbuf, wait, post, stream);
 }
 
 int aby3g_bin_level_residency(int* cus, int* per_cu_small, int* per_cu_large, int* small_max_wgs) {
@@ -1022,14 +830,13 @@ int aby3g_bin_level_residency(int* cus, int* per_cu_small, int* per_cu_large, in
         ABY3G_REQUIRE(cus && per_cu_small && per_cu_large && small_max_wgs, "null argument");
         const int dev = current_device();
         ABY3G_CHECK_HIP(hipDeviceGetAttribute(cus, hipDeviceAttributeMultiprocessorCount, dev));
-        // the consumers that spin: the hand-off level kernel and the
-        // multi-level one (the smaller residency of the two)
-        int a = 0, b = 0;
+        // the consumers that spin: the hand-off instantiations of the level
+        // kernel, one chunk per workgroup (the only in-kernel waiters of the
+        // binary engine)
+        int a = 0;
         ABY3G_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &a, reinterpret_cast<const void*>(k_bin_level<32, true>), 32 * 32, 0));
-        ABY3G_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &b, reinterpret_cast<const void*>(k_bin_levels<32>), 32 * 32, 0));
-        *per_cu_small = std::min(a, b);
+        *per_cu_small = a;
         ABY3G_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &a, reinterpret_cast<const void*>(k_bin_level<8, true>), 8 * 32, 0));
         *per_cu_large = a;
@@ -1139,7 +946,12 @@ int aby3g_bin_level_in(const aby3g_wire_src* srcs, uint32_t nsrc, uint64_t rows,
             ABY3G_REQUIRE(s.copy_out == nullptr, "copy_out: call aby3g_lin_copy_out first");
             const u64 off = (u64)(s.wire_rows - mem);
             ABY3G_REQUIRE(s.wire_rows >= mem && off % words == 0 && off / words < 2 * wires, "wire_rows outside mem");
-            if (!s.term[0] && !s.term[1] && !s.term[2] && !s.term[3]) continue;  // all zero: no LDS
+            if (!s.term[0] && !s.term[1] && !s.term[2] && !s.term[3]) {
+                // all zero: no LDS (aby3g_bits_to_wires_lin applies a constant
+                // even without terms; this form does not)
+                ABY3G_REQUIRE(s.constant == 0, "a source without terms must have a zero constant here");
+                continue;
+            }
             LevelInSrc& d = ls.s[nl++];
             for (int t = 0; t < 4; ++t) {
                 d.term[t] = (const u64*)s.term[t];

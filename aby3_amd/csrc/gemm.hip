@@ -253,14 +253,9 @@ __global__ void __launch_bounds__(256) k_digits(const i64* __restrict__ A0, cons
     digit_group<COLS>(true, blockIdx.x, threadIdx.x, img, A0, A1, B0, B1, M, K, N, S2, aGroups, stages, Ad, Bd);
 }
 
-// ABY3G_DIGIT_COLS=64: the 64-column B-workgroups (A/B runs); default 32
-u32 digit_cols() {
-    static const u32 c = [] {
-        const char* e = getenv("ABY3G_DIGIT_COLS");
-        return e && atoi(e) == 64 ? 64u : 32u;
-    }();
-    return c;
-}
+// B-workgroups of 32 columns: 64 records per group on both sides (17 KiB of
+// LDS; measured ahead of 64-column groups at half the occupancy, round 4)
+constexpr u32 kBGroupCols = 32;
 
 // XCD-aware tile order. Workgroup ids are dealt round-robin to the 8 XCDs
 // (id % 8), each with its own 4 MiB L2. Remap so every XCD gets one
@@ -455,197 +450,6 @@ __global__ void __launch_bounds__(512, 1)
             }
 }
 
-// k_share_gemm16r: k_share_gemm16s with the A operand's digit split done in
-// the GEMM itself (the digit pass then covers B only). A's stage records are
-// DMA'd raw -- row m's 32 i64 of the stage, 256 contiguous bytes of A0 (first
-// K half) or A1 (second half) -- into the same swizzled LDS image, and every
-// wave converts the rows it DMA'd in place into the 8 digit planes
-// (digit_words: the v_perm_b32 4 x 8 byte transpose) one phase before the
-// stage is read: in the read phase of stage it a group first waits for its
-// own DMA pieces of stage it + 1 (issued two phases earlier), converts them,
-// then issues stage it + 2 and reads stage it's fragments. A wave DMAs 16 A
-// rows (4 pieces) and 8 B columns (2 pieces); a lane converts 4 consecutive k
-// of two rows (8 lanes per 256-byte record, all in one wave, so every read of
-// a record precedes its writes). K must be a multiple of 32 (no partial
-// record reaches past its row).
-__global__ void __launch_bounds__(512, 1)
-    k_share_gemm16r(const i64* __restrict__ A, const u8* __restrict__ Bd, u64 M, u64 K, u64 N, u64 stagesTotal,
-                    u64 stagesPerSplit, u32 TM, u32 TN, u32 splits, i64* __restrict__ P, const i64* __restrict__ sub) {
-    constexpr u32 NBUF = 3, kT = 512;
-    constexpr u32 kStageA = TBM * kRec, kStageB = BN * kRec, kStage = kStageA + kStageB;
-    constexpr u32 kPerWave = 6;  // 4 A pieces (16 rows) + 2 B pieces (8 columns)
-    __shared__ __attribute__((aligned(16))) u8 lds[NBUF * kStage];
-    const u32 tid = threadIdx.x, lane = tid & 63;
-    const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const bool Y = wave >= 4;
-    const TileCoord tc = tile_of(blockIdx.x, TM, TN, splits);
-    const u64 m0 = (u64)tc.tm * TBM, n0 = (u64)tc.tn * BN;
-    const u64 s0 = (u64)tc.split * stagesPerSplit;
-    const u64 s1 = min(stagesTotal, s0 + stagesPerSplit);
-    i64* dst = P + (splits > 1 ? (u64)tc.split * M * N : 0);
-    if (s0 >= s1) {
-        for (u32 i = tid; i < TBM * BN; i += kT) {
-            u64 m = m0 + i / BN, n = n0 + i % BN;
-            if (m < M && n < N) dst[m * N + n] = 0;
-        }
-        return;
-    }
-    const u32 nst = (u32)(s1 - s0);
-    const u64 S2 = stagesTotal / 2;  // stages per K half
-    const u8* A0 = (const u8*)A;
-    const u8* A1 = (const u8*)(A + M * K);
-
-    const u32 lrow = lane >> 4, lslot = lane & 15;
-    // A pieces: rows 16 wave + 4 j + lrow (clamped below M: rows past M are never stored)
-    u32 aRow[4];  // byte offsets into A0 / A1 (M K 8 < 2^32, checked by the launcher)
-    u32 aLds[4];
-#pragma unroll
-    for (u32 j = 0; j < 4; ++j) {
-        const u32 r = 16 * wave + 4 * j + lrow;
-        const u32 g = lslot ^ (r & 15);
-        aRow[j] = (u32)(min(m0 + r, M - 1) * K * 8 + g * 16);
-        aLds[j] = (16 * wave + 4 * j) * kRec;
-    }
-    const u8* bSrc[2];
-    u32 bLds[2];
-#pragma unroll
-    for (u32 j = 0; j < 2; ++j) {
-        const u32 r = 8 * wave + 4 * j + lrow;
-        const u32 g = lslot ^ (r & 15);
-        bSrc[j] = Bd + (n0 + r) * stagesTotal * kRec + g * 16;
-        bLds[j] = kStageA + (8 * wave + 4 * j) * kRec;
-    }
-    auto issue = [&](u64 st, u32 b) {
-        const u8* ab = st < S2 ? A0 + st * 256 : A1 + (st - S2) * 256;
-#pragma unroll
-        for (u32 j = 0; j < 4; ++j)
-            __builtin_amdgcn_global_load_lds((glb_void*)(ab + aRow[j]), (lds_void*)(lds + b * kStage + aLds[j]), 16, 0,
-                                             0);
-#pragma unroll
-        for (u32 j = 0; j < 2; ++j)
-            __builtin_amdgcn_global_load_lds((glb_void*)(bSrc[j] + st * kRec), (lds_void*)(lds + b * kStage + bLds[j]),
-                                             16, 0, 0);
-    };
-    // in place: the wave's 16 A rows of buffer b, raw -> digit records
-    auto convert = [&](u32 b) {
-        u8* base = lds + b * kStage;
-        // the lane id through an opaque move: the conversion's ~18 lane
-        // addresses are recomputed here rather than hoisted out of the stage
-        // loop and held in registers (they spilled the accumulators)
-        u32 ln;
-        asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
-        const u32 ct = ln & 7;
-#pragma unroll
-        for (u32 h = 0; h < 2; ++h) {
-            const u32 r = 16 * wave + 8 * h + (ln >> 3);
-            u8* rec = base + r * kRec;
-            const v4i x0 = *reinterpret_cast<const v4i*>(rec + (((2 * ct) ^ (r & 15)) * 16));
-            const v4i x1 = *reinterpret_cast<const v4i*>(rec + (((2 * ct + 1) ^ (r & 15)) * 16));
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the record's reads before its writes
-            const u64 v[4] = {(u64)(u32)x0.x | ((u64)(u32)x0.y << 32), (u64)(u32)x0.z | ((u64)(u32)x0.w << 32),
-                              (u64)(u32)x1.x | ((u64)(u32)x1.y << 32), (u64)(u32)x1.z | ((u64)(u32)x1.w << 32)};
-            u32 w[8];
-            digit_words(v, w);
-#pragma unroll
-            for (u32 p = 0; p < 8; ++p)
-                *reinterpret_cast<u32*>(rec + (((2 * p + (ct >> 2)) ^ (r & 15)) * 16) + 4 * (ct & 3)) = w[p];
-        }
-    };
-
-    v4i acc[8][2][2];
-#pragma unroll
-    for (int s = 0; s < 8; ++s)
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) acc[s][i][j] = v4i{0};
-
-    const u32 wr = (wave >> 1 & 1) * 32 + (wave >> 2) * 64, wc = (wave & 1) * 32;
-    const u32 r16 = lane & 15, g4 = lane >> 4, hi = g4 >> 1;
-    const bool zhalf = hi != 0;
-
-    {
-        issue(s0, 0);
-        issue(min(s0 + 1, s1 - 1), 1);
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPerWave) : "memory");
-        convert(0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();      // barrier 0: stage 0 converted and visible
-    if (Y) __builtin_amdgcn_s_barrier();  // Y starts one phase late
-
-    u32 buf = 0;
-    for (u32 it = 0; it < nst; ++it) {
-        // ---- read phase: convert own rows of stage it + 1, DMA of stage it + 2, this stage's fragments
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // own pieces of stage it + 1 landed
-        convert(buf == 2 ? 0 : buf + 1);
-        __builtin_amdgcn_sched_barrier(0);
-        issue(min(s0 + it + 2, s1 - 1), buf == 0 ? 2 : buf - 1);
-        const u8* ls = lds + buf * kStage;
-        v4i a[4][2], b[8][2];
-        {
-            // fragment offsets recomputed per stage from an opaque lane id (held
-            // across the loop they would cost 24 registers the conversion needs)
-            u32 ln;
-            asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
-            const u32 q16 = ln & 15, qh = (ln >> 5) & 1, qf = (ln >> 4) & 1;
-#pragma unroll
-            for (int f = 0; f < 8; ++f)
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const u32 gg = 2 * (f == 0 ? 0 : (qh ? f - 1 : f)) + qf;
-                    b[f][j] = *reinterpret_cast<const v4i*>(ls + kStageA + (wc + 16 * j + q16) * kRec + ((gg ^ q16) * 16));
-                }
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-                for (int i = 0; i < 2; ++i)
-                    a[e][i] = *reinterpret_cast<const v4i*>(ls + (wr + 16 * i + q16) * kRec +
-                                                            (((2 * (2 * e + qh) + qf) ^ q16) * 16));
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        // ---- MFMA phase
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-            if (zhalf) b[0][j] = v4i{0};
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-#pragma unroll
-                    for (int f = 0; f + 2 * e < 8; ++f)
-                        acc[2 * e + f][i][j] =
-                            __builtin_amdgcn_mfma_i32_16x16x64_i8(a[e][i], b[f][j], acc[2 * e + f][i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_s_barrier();
-        buf = buf == 2 ? 0 : buf + 1;
-    }
-    if (!Y) __builtin_amdgcn_s_barrier();  // equal barrier counts
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                u64 v = 0;
-#pragma unroll
-                for (int s = 0; s < 8; ++s) v += (u64)(i64)acc[s][i][j][r] << (8 * s);
-                const u64 m = m0 + wr + 16 * i + 4 * g4 + r;
-                const u64 n = n0 + wc + 16 * j + r16;
-                if (m < M && n < N) {
-                    const u64 x = m * N + n;
-                    if (sub) v -= (u64)sub[x];
-                    dst[x] = (i64)v;
-                }
-            }
-}
-
 // Optional turn-taking of share-GEMM launches on one device (in issue order,
 // whichever stream issues them) through a device-wide event chain (stream
 // waits on the previous GEMM's completion event; no host sync): bench.py's
@@ -727,7 +531,7 @@ DigitArgs digit_args(const GemmPlan& p, const i64* A, const i64* B, const Worksp
     da.stages = p.Kc / BK;
     da.S2 = p.Kp / 32;
     da.aGroups = (p.Mp / kDigitRows) * da.S2;
-    da.groups = da.aGroups + (p.Np / digit_cols()) * da.S2;
+    da.groups = da.aGroups + (p.Np / kBGroupCols) * da.S2;
     da.Ad = w.Ad;
     da.Bd = w.Bd;
     return da;
@@ -751,44 +555,12 @@ void run_share_gemm(const GemmPlan& p, const Workspace& w, hipStream_t s, i64* o
            TM, TN, p.splits, dst, sb);
 }
 
-// A's digit split inside the GEMM (k_share_gemm16r): ABY3G_GEMM_RAWA=1. Needs
-// K a whole number of 32-wide stages and A's byte offsets within 32 bits.
-bool raw_a_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("ABY3G_GEMM_RAWA");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
-bool raw_a_fits(const GemmPlan& p) { return p.Kp == p.K && p.tbm == TBM && p.M * p.K * 8 < (1ull << 32); }
-
 // Runs the digit split and the MFMA GEMM.
 void run_gemm(const GemmPlan& p, const i64* A, const i64* B, const Workspace& w, hipStream_t s, i64* out = nullptr,
               const i64* sub = nullptr, hipEvent_t subReady = nullptr) {
     const DigitArgs da = digit_args(p, A, B, w);
-    if (raw_a_enabled() && raw_a_fits(p)) {
-        // digit pass over B only (aGroups 0), A converted in the GEMM
-        if (digit_cols() == 32)
-            launch(PROBE_DIGITS, k_digits<32>, dim3((u32)(da.groups - da.aGroups)), dim3(256), 0, s, da.A0, da.A1,
-                   da.B0, da.B1, p.M, p.K, p.N, da.S2, (u64)0, da.stages, w.Ad, w.Bd);
-        else
-            launch(PROBE_DIGITS, k_digits<64>, dim3((u32)(da.groups - da.aGroups)), dim3(256), 0, s, da.A0, da.A1,
-                   da.B0, da.B1, p.M, p.K, p.N, da.S2, (u64)0, da.stages, w.Ad, w.Bd);
-        const u64 stages = p.Kc / BK;
-        const u32 TM = (u32)(p.Mp / p.tbm), TN = (u32)(p.Np / BN);
-        const bool direct = p.splits == 1 && out != nullptr;
-        if (direct && sub && subReady) ABY3G_CHECK_HIP(hipStreamWaitEvent(s, subReady, 0));
-        MfmaTurn turn(s);
-        launch(PROBE_GEMM, k_share_gemm16r, dim3(TM * TN * p.splits), dim3(512), 0, s, A, (const u8*)w.Bd, p.M, p.K,
-               p.N, stages, p.kPerSplit / BK, TM, TN, p.splits, direct ? out : w.P, direct ? sub : nullptr);
-        return;
-    }
-    if (digit_cols() == 32)
-        launch(PROBE_DIGITS, k_digits<32>, dim3((u32)da.groups), dim3(256), 0, s, da.A0, da.A1, da.B0, da.B1, p.M, p.K,
-               p.N, da.S2, da.aGroups, da.stages, w.Ad, w.Bd);
-    else
-        launch(PROBE_DIGITS, k_digits<64>, dim3((u32)da.groups), dim3(256), 0, s, da.A0, da.A1, da.B0, da.B1, p.M, p.K,
-               p.N, da.S2, da.aGroups, da.stages, w.Ad, w.Bd);
+    launch(PROBE_DIGITS, k_digits<kBGroupCols>, dim3((u32)da.groups), dim3(256), 0, s, da.A0, da.A1, da.B0, da.B1, p.M,
+           p.K, p.N, da.S2, da.aGroups, da.stages, w.Ad, w.Bd);
     run_share_gemm(p, w, s, out, sub, subReady);
 }
 

@@ -32,7 +32,6 @@ static void evalTwoInput(BetaCircuit* cir, int pIdx, const std::vector<std::pair
     Sh3BinaryEvaluator binEng;
     binEng.setCir(cir, x[0].first->size(), eval.mShareGen);
     setTwoInputSharing(binEng, pIdx, x, sign, {0}, {0}, 1, rt.mComm, rt.gpu());
-    binEng.fuseOutput(0, res);  // the last level writes res (one comparison bit)
     binEng.asyncEvaluate(rt.noDependencies())
         .then([&](Sh3Task&) { binEng.getOutput(0, res); })
         .get();

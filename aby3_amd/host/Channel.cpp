@@ -1,5 +1,6 @@
 #include "Channel.h"
 #include "Link.h"
+#include <cstring>
 #include <chrono>
 #include <cstdlib>
 #include <atomic>
@@ -50,7 +51,8 @@ struct Msg {
 // a message descriptor on a link's ring (host payloads follow it)
 struct WireMsg {
     u64 bytes;
-    u32 kind;  // 0 host payload, 1 device payload (staged), 2 in-kernel (arena), 3 arena announce
+    u32 kind;  // 0 host payload, 1 device payload (staged), 2 in-kernel (arena), 3 arena announce,
+               // 4 device identity (the sender's device UUID in handle.bytes[0..15])
     u32 slot;
     u64 gen, seq;  // kind 2: gen = offset in the arena's slots; kind 3: gen = slot bytes
     i64 device;    // the sender's device
@@ -109,7 +111,11 @@ struct Pipe {
     // sender and receiver on this device (-1: unknown / different): device
     // payloads are then signalled through a stream-ordered word
     int signalDevice = -1;
-    u64* word = nullptr;  // allocated by the sender on first use
+    // allocated and zeroed when the ring is built (makeLocalRing), never
+    // mid-run: zeroing needs a device-wide wait, and a party host blocked in
+    // one cannot enqueue the producer another party's waiting kernel needs
+    // (the round-4 hand-off timeouts)
+    u64* word = nullptr;
     u64 devSeq = 0;       // device payloads signalled so far (sender thread only)
     // in-kernel hand-offs (Channel::handoffPost): one flag per chunk of
     // ABY3G_HANDOFF_ROWS rows, reused by every message with increasing seq
@@ -143,6 +149,7 @@ struct Pipe {
     void* arena = nullptr;
     u64 arenaSlot = 0;   // bytes per evaluation slot
     u64 arenaNext = 0;   // sender: slots handed out
+    int arenaOpen = 0;   // sender: an evaluation holds a slot (evalSendBuffer .. evalSendEnd)
     bool arenaMapped = false;
     u64* arenaFlags() const { return (u64*)arena; }
     u8* arenaSlots() const { return (u8*)arena + kArenaFlagBytes; }
@@ -199,7 +206,7 @@ struct Pipe {
     // readiness of a device payload enqueued so far on `gpu`'s stream
     void signalReady(Msg& m, Gpu& gpu, Event* fallback) {
         if (signalDevice >= 0 && signalDevice == gpu.device()) {
-            if (!word) GPU_CALL(aby3g_signal_alloc(&word));
+            if (!word) throw std::runtime_error("channel: signal word not allocated at ring construction");
             m.sigWord = word;
             m.sigValue = ++devSeq;
             GPU_CALL(aby3g_stream_write_value(gpu.stream(), word, m.sigValue));
@@ -640,7 +647,8 @@ aby3g_handoff Channel::handoffPost(Gpu& gpu, u64 rows, u64 producerBytes, const 
         if (!p.arena || kernelsSerialized() || !q || q < p.arenaSlots() || q >= p.arenaSlots() + 2 * p.arenaSlot)
             return aby3g_handoff{nullptr, 0, nullptr};
         const u64 chunks = std::max<u64>(1, (rows + ABY3G_HANDOFF_ROWS - 1) / ABY3G_HANDOFF_ROWS);
-        if (!handoffResidencyOk(handoffResidency(gpu.device()), chunks) || chunks > kHandoffChunks ||
+        // three processes on the device: each brings its own queues' stream-op waits
+        if (!handoffResidencyOk(handoffResidency(gpu.device()), chunks, 3) || chunks > kHandoffChunks ||
             (chunks > kHandoffMaxChunks && producerBytes > kHandoffLightBytes))
             return aby3g_handoff{nullptr, 0, nullptr};
         return aby3g_handoff{p.arenaFlags(), ++p.hsSeq, nullptr};
@@ -681,11 +689,11 @@ bool Channel::handoffCapable(const Gpu& gpu) const {
     return true;
 }
 
-bool handoffResidencyOk(const HandoffResidency& r, u64 chunks) {
+bool handoffResidencyOk(const HandoffResidency& r, u64 chunks, int processes) {
     const int per = chunks < (u64)std::max(0, r.smallMaxWgs) ? r.perCuSmall : r.perCuLarge;
-    if (per <= 0 || r.cus <= 0 || !chunks) return false;
+    if (per <= 0 || r.cus <= 0 || !chunks || processes < 1) return false;
     const u64 cusHeld = (chunks + (u64)per - 1) / (u64)per;
-    return 2 * cusHeld + (u64)std::max(0, r.otherSpinners) + 1 <= (u64)r.cus;
+    return 2 * cusHeld + (u64)processes * (u64)std::max(0, r.otherSpinners) + 1 <= (u64)r.cus;
 }
 
 const HandoffResidency& handoffResidency(int device) {
@@ -703,11 +711,17 @@ const HandoffResidency& handoffResidency(int device) {
     return byDevice.emplace(device, r).first->second;
 }
 
-std::shared_ptr<DeviceBuffer> Channel::evalSendBuffer(Gpu& gpu, size_t bytes) {
+std::shared_ptr<DeviceBuffer> Channel::evalSendBuffer(Gpu& gpu, size_t bytes, u64 andLevels) {
     if (!mOut || !mOut->link || !mOut->arena || kernelsSerialized() || bytes > mOut->arenaSlot) return nullptr;
     Pipe& p = *mOut;
+    if (andLevels < 2 || p.arenaOpen) return nullptr;
+    p.arenaOpen = 1;
     const u64 slot = p.arenaNext++ & 1;
     return DeviceBuffer::borrow(p.arenaSlots() + slot * p.arenaSlot, bytes, &gpu);
+}
+
+void Channel::evalSendEnd() {
+    if (mOut) mOut->arenaOpen = 0;
 }
 
 bool Channel::linkedConcurrent() const {
@@ -855,6 +869,19 @@ std::vector<CommPkg> makeLocalRing(const int* devices, bool kernelHandoff) {
                     p[i][j]->kernelHandoff = kernelHandoff;
                 }
             }
+    // every same-device direction's signal word, zeroed now, before any
+    // party's work is enqueued (aby3g_signal_alloc waits for the device)
+    if (devices) {
+        int cur = 0;
+        GPU_CALL(aby3g_get_device(&cur));
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                if (i != j && p[i][j]->signalDevice >= 0) {
+                    GPU_CALL(aby3g_set_device(p[i][j]->signalDevice));
+                    GPU_CALL(aby3g_signal_alloc(&p[i][j]->word));
+                }
+        GPU_CALL(aby3g_set_device(cur));
+    }
     std::vector<CommPkg> c(3);
     for (int i = 0; i < 3; ++i) {
         int nx = (i + 1) % 3, pv = (i + 2) % 3;
@@ -882,6 +909,33 @@ CommPkg makeProcessRing(int party, const std::string& link, int device, bool sam
     for (int a = 0; a < 3; ++a)
         for (int b = 0; b < 3; ++b)
             if (a != b && (a == party || b == party)) pipes[a][b] = end(a, b);
+    {
+        // `sameDevice` is the caller's claim; the arenas need all three
+        // parties on ONE GPU (their level kernels poll agent-scope flags and
+        // read coarse-grained payloads). Each process sends its claim and its
+        // device UUID to both neighbours and checks both: every process then
+        // reaches the same answer (all three claim it and their UUIDs are
+        // equal, or not), so they all take the arenas or none do -- a mixed
+        // layout (two parties on one GPU, one on another) or a disagreeing
+        // claim falls back to the staged copies.
+        u8 own[16];
+        GPU_CALL(aby3g_device_uuid(device, own));
+        for (int to : {nx, pv}) {
+            WireMsg w{};
+            w.kind = 4;
+            w.slot = kNoSlot;
+            w.seq = sameDevice ? 1 : 0;
+            w.device = device;
+            std::memcpy(w.handle.bytes, own, 16);
+            pipes[party][to]->ringWrite(std::vector<u8>((const u8*)&w, (const u8*)&w + sizeof w));
+        }
+        for (int from : {pv, nx}) {
+            WireMsg w;
+            pipes[from][party]->link->read(&w, sizeof w);
+            if (w.kind != 4) throw std::runtime_error("makeProcessRing: expected the peer's device identity");
+            if (w.seq != 1 || std::memcmp(w.handle.bytes, own, 16) != 0) sameDevice = false;
+        }
+    }
     if (sameDevice && !kernelsSerialized()) {
         // the arenas of in-kernel hand-offs: each process announces its two
         // outgoing ones (zeroed, then exported), then maps the two incoming

@@ -90,8 +90,16 @@ public:
     // One party per process on one GPU: a buffer for an evaluation's messages
     // inside this direction's IPC-mapped arena (two slots, alternating per
     // call), which the receiver reads in place -- null when the direction has
-    // no arena or `bytes` exceeds a slot (the caller allocates its own).
-    std::shared_ptr<DeviceBuffer> evalSendBuffer(Gpu& gpu, size_t bytes);
+    // no arena, `bytes` exceeds a slot, the circuit has fewer than two AND
+    // levels, or another evaluation's lease on the arena is still open (the
+    // caller then allocates its own). A slot is rewritten two evaluations
+    // later; that is safe only when the evaluations run one after another on
+    // the party's stream and each has two or more AND levels (the receiver's
+    // reads of evaluation e precede, in its stream, its first message of e+1,
+    // which the sender's e+1 needs before it starts e+2). The caller ends its
+    // lease with evalSendEnd() once the evaluation's last message is sent.
+    std::shared_ptr<DeviceBuffer> evalSendBuffer(Gpu& gpu, size_t bytes, u64 andLevels);
+    void evalSendEnd();
     // Would handoffPost(gpu, rows, producerBytes) hand the next message over
     // in-kernel? (no side effects; the same answer handoffPost gives)
     bool handoffWouldPost(const Gpu& gpu, u64 rows, u64 producerBytes = 0) const;
@@ -138,19 +146,23 @@ int hwQueuesPerDevice();
 // slot: at most two parties' consumer launches spin at once (a party's next
 // level waits behind its own current one on its stream, so one of the three
 // is always the producer), besides at most `otherSpinners` stream-operation
-// wait kernels (one per stream on the device). Counted in whole CUs, since
+// wait kernels (one per hardware queue of each process on the device: three
+// processes sharing one GPU bring three sets). Counted in whole CUs, since
 // the dispatcher may spread a launch over every CU: a consumer of c chunks
 // (c workgroups of the small form when c < smallMaxWgs, else of the large
 // one) holds at most ceil(c / perCu) CUs' worth of its kernel's slots, and
-//     2 ceil(c / perCu) + otherSpinners + 1 <= cus
-// leaves the producer a CU.
+//     2 ceil(c / perCu) + processes * otherSpinners + 1 <= cus
+// leaves the producer a CU. The rule holds for consumers of ONE chunk per
+// workgroup (the level kernel's hand-off instantiations): a workgroup that
+// looped over several chunks would hold its slot across waits on different
+// producers' chunks, and would need every party's whole grid co-resident.
 struct HandoffResidency {
     int cus = 0;
     int perCuSmall = 0, perCuLarge = 0;  // level-kernel workgroups resident per CU
     int smallMaxWgs = 0;
     int otherSpinners = 0;
 };
-bool handoffResidencyOk(const HandoffResidency& r, u64 chunks);
+bool handoffResidencyOk(const HandoffResidency& r, u64 chunks, int processes = 1);
 // the current device's figures (aby3g_bin_level_residency, computed once per
 // device; otherSpinners = GPU_MAX_HW_QUEUES)
 const HandoffResidency& handoffResidency(int device);

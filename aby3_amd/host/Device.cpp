@@ -192,12 +192,19 @@ void* Gpu::alloc(size_t bytes) {
     }
     void* p = nullptr;
     GPU_CALL(aby3g_set_device(mDevice));
-    int rc = aby3g_malloc(&p, cls);
-    if (rc != 0) {
-        // out of memory: drop the cache (after the streams drain) and retry once
-        sync();
-        trim();
-        GPU_CALL(aby3g_malloc(&p, cls));
+    if (aby3g_malloc(&p, cls) != 0) {
+        // Out of memory. No recovery here: returning the cache to the driver
+        // (hipFree) waits for the whole device, and mid-protocol that wait can
+        // block on a peer's kernel that waits for this party's next launch.
+        // Callers trim() at a quiescent point (between runs) instead.
+        size_t cached;
+        {
+            std::lock_guard<std::mutex> lk(mPool->mu);
+            cached = mPool->cached;
+        }
+        throw std::runtime_error(std::string("device out of memory allocating ") + std::to_string(cls) +
+                                 " bytes (" + std::to_string(cached) + " bytes cached by this party's pool; " +
+                                 "Gpu::trim() between runs returns them): " + aby3g_last_error());
     }
     return p;
 }

@@ -7,8 +7,6 @@ namespace aby3 {
 
 // defaults of the binary engine's fused forms (A/B-measured)
 constexpr bool kFuseInputsDefault = true;
-constexpr bool kMergeLevelsDefault = false;
-constexpr bool kFuseOutputDefault = false;
 
 void Sh3BinaryEvaluator::setCir(BetaCircuit* cir, u64 width, Sh3ShareGen& gen) {
     block p = gen.getPrevBlock();
@@ -124,8 +122,7 @@ void Sh3BinaryEvaluator::setCir(BetaCircuit* cir, u64 width, block prevSeed, blo
     mKeyPrev = prevSeed;
     mKeyNext = nextSeed;
     mPendingIn.clear();  // held inputs belong to the previous circuit
-    mFuseOut = nullptr;
-    mFuseOutDone = false;
+    mPendingHold.clear();
     Gpu& g = Gpu::current();
     mGpu = &g;
     upload(g);
@@ -258,10 +255,22 @@ static bool fuseInputsEnabled() {
     return on;
 }
 
-void Sh3BinaryEvaluator::flushPendingInputs() {
+void Sh3BinaryEvaluator::flushPendingInputs(bool dropHolds) {
     if (mPendingIn.empty()) return;
     GPU_CALL(aby3g_bits_to_wires_lin(mPendingIn.data(), (u32)mPendingIn.size(), mRows, mWords, mGpu->stream()));
     mPendingIn.clear();
+    readHeld(dropHolds);
+}
+
+void Sh3BinaryEvaluator::holdForInputs(std::shared_ptr<DeviceBuffer> b) {
+    if (b) mPendingHold.push_back(std::move(b));
+}
+
+void Sh3BinaryEvaluator::readHeld(bool drop) {
+    // the launch that reads the held sources is enqueued: fence each buffer
+    // behind it (a no-op for this party's own pool, reused in stream order)
+    for (auto& b : mPendingHold) b->fence(mGpu->stream());
+    if (drop) mPendingHold.clear();
 }
 
 bool Sh3BinaryEvaluator::pendingCoversInputs() const {
@@ -290,8 +299,11 @@ void Sh3BinaryEvaluator::setInputs(const std::vector<WireInput>& in) {
     // source is one 64-bit column: the copy-outs (a message, e.g. P0's
     // reshared value) are made now, the transposes inside that launch.
     bool defer = fuseInputsEnabled() && mCur->fuseInputs;
-    for (const WireInput& w : in)
+    for (const WireInput& w : in) {
         if (w.input >= mCir->mInputs.size() || mCir->mInputs[w.input].size() > 64) defer = false;
+        // a constant without terms: the separate transpose applies it, the fused level does not
+        if (!w.term[0] && !w.term[1] && !w.term[2] && !w.term[3] && w.constant) defer = false;
+    }
     auto flush = [&] {
         if (srcs.empty()) return;
         if (defer) {
@@ -304,7 +316,7 @@ void Sh3BinaryEvaluator::setInputs(const std::vector<WireInput>& in) {
                     for (int t = 1; t < 4; ++t) s.term[t] = nullptr, s.coef[t] = 0;
                 }
                 s.copy_out = nullptr;
-                if (mPendingIn.size() == ABY3G_WIRE_SRC_MAX) flushPendingInputs();
+                if (mPendingIn.size() == ABY3G_WIRE_SRC_MAX) flushPendingInputs(false);  // more sources follow
                 mPendingIn.push_back(s);
             }
         } else {
@@ -374,6 +386,9 @@ void setTwoInputSharing(Sh3BinaryEvaluator& eng, int pIdx, const std::vector<std
         }
         zero(in1, 0);
         zero(in1, 1);
+        // the first level may read the copy-out v later (fused inputs): keep
+        // it out of the pool until that launch is enqueued
+        eng.holdForInputs(v);
         eng.setInputs(w);
         comm.mNext.asyncSendShared(v, b8, g);
     } else if (pIdx == 1) {
@@ -395,8 +410,11 @@ void setTwoInputSharing(Sh3BinaryEvaluator& eng, int pIdx, const std::vector<std
             d.constant = offsets[k];
             w.push_back(d);
         }
+        // v is P0's buffer, read in place by the first level's launch (fused
+        // inputs, enqueued later in roundCallback) or by the transpose now:
+        // held until that launch is enqueued, then fenced behind it
+        eng.holdForInputs(v);
         eng.setInputs(w);
-        v->fence(g.stream());
     } else {
         // in0 = (0, 0), in1 = (0, x1)
         for (size_t k = 0; k < in0.size(); ++k) {
@@ -432,121 +450,10 @@ void Sh3BinaryEvaluator::setReplicatedInput(u64 i, const sbMatrix& in) {
     mLevel = 0;
 }
 
-// ABY3_MERGE_LEVELS=1 / 0 turns the merged light levels on / off (A/B runs)
-static bool mergeLevelsEnabled() {
-    static const bool on = [] {
-        const char* e = getenv("ABY3_MERGE_LEVELS");
-        return e ? e[0] == '1' : kMergeLevelsDefault;
-    }();
-    return on;
-}
-
-// The rest of the evaluation as one launch (aby3g_bin_levels) when every
-// message from here on goes in-kernel: the parties' decisions agree (the same
-// circuit, rows and channel kinds), so the previous party hands over in-kernel
-// whatever this one receives after the first of these rounds.
-namespace {
-struct MergedResidency {
-    int cus = 0, perCuSmall = 0, perCuLarge = 0, smallMaxWgs = 0;
-};
-const MergedResidency& mergedResidency(int device) {
-    static std::mutex mu;
-    static std::map<int, MergedResidency> byDevice;
-    std::lock_guard<std::mutex> lk(mu);
-    auto it = byDevice.find(device);
-    if (it != byDevice.end()) return it->second;
-    MergedResidency r;
-    GPU_CALL(aby3g_set_device(device));
-    GPU_CALL(aby3g_bin_levels_residency(&r.cus, &r.perCuSmall, &r.perCuLarge, &r.smallMaxWgs));
-    return byDevice.emplace(device, r).first->second;
-}
-}  // namespace
-
-bool Sh3BinaryEvaluator::mergeRest(CommPkg& comm, Gpu& g) {
-    const u64 n = mCir->mLevelCounts.size();
-    if (!mergeLevelsEnabled() || mLevel == 0 || mLevel > n || !mPendingIn.empty()) return false;
-    if (n + 1 - mLevel > ABY3G_LEVELS_MAX) return false;
-    u32 launches = 0;
-    for (u64 L = mLevel; L <= n; ++L) {
-        const bool gates = L < n && mCur->levelBatches[L];
-        const bool unpack = mCir->mLevelAndCounts[L - 1] != 0;
-        launches += gates || unpack;
-        if (L < n && mCir->mLevelAndCounts[L] &&
-            !comm.mNext.handoffWouldPost(g, mRows, (u64)mCir->mLevelCounts[L] * mWords * 72))
-            return false;
-    }
-    if (launches < 2) return false;
-    {
-        // every party's whole grid (a workgroup per chunk) must be resident at
-        // once, besides the stream-op spinners
-        const MergedResidency& r = mergedResidency(g.device());
-        const u64 chunks = mWords / 32;
-        const int perCu = chunks < (u64)r.smallMaxWgs ? r.perCuSmall : r.perCuLarge;
-        if (3 * chunks + (u64)hwQueuesPerDevice() > (u64)r.cus * (u64)std::max(0, perCu)) return false;
-    }
-    const u64 rowBytes = mWords * 8;
-    std::vector<aby3g_level_run> runs;
-    std::vector<std::shared_ptr<DeviceBuffer>> recvs;
-    aby3g_handoff hw{nullptr, 0, nullptr};
-    u64* postFlags = nullptr;
-    for (u64 L = mLevel; L <= n; ++L) {
-        aby3g_level_run r{};
-        const u32 nUnpack = mCir->mLevelAndCounts[L - 1];
-        if (nUnpack) {
-            aby3g_handoff h{nullptr, 0, nullptr};
-            auto recv = mRecvFutr.getSharedHandoff(h);
-            if (h.flags) {
-                if (hw.flags && hw.flags != h.flags) throw std::runtime_error("merged levels: hand-off flags differ");
-                hw = h;
-                r.wait_seq = h.seq;
-            } else if (L != mLevel) {
-                throw std::runtime_error("merged levels: a later level's shares arrived by a stream hand-off");
-            }
-            r.nunpack = nUnpack;
-            r.unpack_wires = mCur->outWires[L - 1];
-            r.recv = recv->as<u64>();
-            recvs.push_back(std::move(recv));
-        }
-        if (L < n) {
-            r.first_gate = mCur->levelFirstGate[L];
-            r.batch_off = mCur->levelBatchOffset[L];
-            r.nbatches = mCur->levelBatches[L];
-            const u32 nAnd = mCir->mLevelAndCounts[L];
-            if (nAnd) {
-                if (!mSendAll) mSendAll = std::make_shared<DeviceBuffer>(g, (u64)mCir->mAndCount * rowBytes);
-                auto send = DeviceBuffer::view(mSendAll, mAndDone * rowBytes, nAnd * rowBytes);
-                const aby3g_handoff hp = comm.mNext.handoffPost(g, mRows, (u64)mCir->mLevelCounts[L] * mWords * 72);
-                if (!hp.flags) throw std::runtime_error("merged levels: the post went by a stream hand-off");
-                if (postFlags && postFlags != hp.flags) throw std::runtime_error("merged levels: post flags differ");
-                postFlags = hp.flags;
-                r.send = send->as<u64>();
-                r.post_seq = hp.seq;
-                // in-kernel posts need no stream operation: sent before the launch
-                comm.mNext.asyncSendShared(send, nAnd * rowBytes, g, hp);
-                mRecvFutr = comm.mPrev.asyncRecvShared(nAnd * rowBytes, g);
-                mAndDone += nAnd;
-            }
-        }
-        runs.push_back(r);
-    }
-    if (mZPending) waitZ();
-    const bool out = mFuseOut != nullptr;
-    const u32 nout = out ? (u32)mCir->mOutputs[mFuseOutIdx].size() : 0;
-    GPU_CALL(aby3g_bin_levels(runs.data(), (u32)runs.size(), mCur->gates, mCur->recvRows, mCur->batchEnds,
-                              mMem.as<u64>(), mCir->mWireCount, mWords, mZPtr, hw.flags ? &hw : nullptr, postFlags,
-                              out ? mCur->allOutputWires + mCur->outputOffsets[mFuseOutIdx] : nullptr, nout,
-                              out ? mFuseOut->data() : nullptr, mRows, g.stream()));
-    if (out) mFuseOutDone = true;
-    for (auto& r : recvs) r->fence(g.stream());
-    mLevel = n + 1;
-    return true;
-}
-
 void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
     if (mLevel > mCir->mLevelCounts.size())
         throw std::runtime_error("evaluateRound() was called but no rounds remain... " LOCATION);
     Gpu& g = task.getRuntime().gpu();
-    if (mergeRest(comm, g)) return;  // no rounds left
     const u64 W = mCir->mWireCount;
     const u64 rowBytes = mWords * 8;
     // share 1 of last level's AND outputs arrived from prev (:555-573); they
@@ -576,7 +483,10 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
         if (!mSendAll) {
             // between processes on one GPU, the evaluation's messages live in
             // the channel's IPC-mapped arena, read in place by the receiver
-            mSendAll = comm.mNext.evalSendBuffer(g, (u64)mCir->mAndCount * rowBytes);
+            u64 andLevels = 0;
+            for (u32 c : mCir->mLevelAndCounts) andLevels += c != 0;
+            mSendAll = comm.mNext.evalSendBuffer(g, (u64)mCir->mAndCount * rowBytes, andLevels);
+            mArenaLease = mSendAll != nullptr;
             if (!mSendAll) mSendAll = std::make_shared<DeviceBuffer>(g, (u64)mCir->mAndCount * rowBytes);
         }
         send = DeviceBuffer::view(mSendAll, mAndDone * rowBytes, nAnd * rowBytes);
@@ -596,24 +506,14 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
                                     mCur->batchEnds + mCur->levelBatchOffset[0], nb, mMem.as<u64>(), W, mWords, mZPtr,
                                     send ? send->as<u64>() : nullptr, &hp, g.stream()));
         mPendingIn.clear();
+        readHeld(true);
     } else if (nb || nUnpack) {
         const aby3g_gate* gl = nb ? mCur->gates + mCur->levelFirstGate[mLevel] : nullptr;
         const u32* be = nb ? mCur->batchEnds + mCur->levelBatchOffset[mLevel] : nullptr;
         const u32* rr = (nb && recv) ? mCur->recvRows + 2 * (u64)mCur->levelFirstGate[mLevel] : nullptr;
-        if (mFuseOut && mLevel == mCur->lastLaunchLevel) {
-            // the last launch also reads the few-bit output out (getOutput)
-            const u32 nout = (u32)mCir->mOutputs[mFuseOutIdx].size();
-            GPU_CALL(aby3g_bin_level_out(gl, rr, be, nb, recv ? recv->as<u64>() : nullptr,
-                                         nUnpack ? mCur->outWires[mLevel - 1] : nullptr, nUnpack, mMem.as<u64>(), W,
-                                         mWords, mZPtr, send ? send->as<u64>() : nullptr, &hw, &hp,
-                                         mCur->allOutputWires + mCur->outputOffsets[mFuseOutIdx], nout,
-                                         mFuseOut->data(), mRows, g.stream()));
-            mFuseOutDone = true;
-        } else {
-            GPU_CALL(aby3g_bin_level_hs(gl, rr, be, nb, recv ? recv->as<u64>() : nullptr,
-                                        nUnpack ? mCur->outWires[mLevel - 1] : nullptr, nUnpack, mMem.as<u64>(), W,
-                                        mWords, mZPtr, send ? send->as<u64>() : nullptr, &hw, &hp, g.stream()));
-        }
+        GPU_CALL(aby3g_bin_level_hs(gl, rr, be, nb, recv ? recv->as<u64>() : nullptr,
+                                    nUnpack ? mCur->outWires[mLevel - 1] : nullptr, nUnpack, mMem.as<u64>(), W, mWords,
+                                    mZPtr, send ? send->as<u64>() : nullptr, &hw, &hp, g.stream()));
     }
 
     if (recv) {
@@ -625,6 +525,11 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
     if (nAnd) {
         comm.mNext.asyncSendShared(send, nAnd * rowBytes, g, hp);
         mRecvFutr = comm.mPrev.asyncRecvShared(nAnd * rowBytes, g);
+        if (mArenaLease && mAndDone == mCir->mAndCount) {
+            // the evaluation's last message is sent: the arena may serve the next one
+            comm.mNext.evalSendEnd();
+            mArenaLease = false;
+        }
     }
     ++mLevel;
     if (hasMoreRounds()) task.then([this](CommPkg& c, Sh3Task& t) { roundCallback(c, t); }, "callback");
@@ -654,31 +559,8 @@ Sh3Task Sh3BinaryEvaluator::asyncEvaluate(Sh3Task dep, BetaCircuit* cir, Sh3Shar
         });
 }
 
-// ABY3_FUSE_OUTPUT=1 / 0 turns the last launch's output read-out on / off (A/B runs)
-static bool fuseOutputEnabled() {
-    static const bool on = [] {
-        const char* e = getenv("ABY3_FUSE_OUTPUT");
-        return e ? e[0] == '1' : kFuseOutputDefault;
-    }();
-    return on;
-}
-
-void Sh3BinaryEvaluator::fuseOutput(u64 i, sbMatrix& out) {
-    if (!mCir || i >= mCir->mOutputs.size()) throw RTE_LOC;
-    mFuseOut = nullptr;
-    mFuseOutDone = false;
-    if (!fuseOutputEnabled()) return;
-    // the last launch must be a later level's (the first level's fused-input
-    // form has no read-out), the output few-bit
-    if (mCur->lastLaunchLevel == 0 || mCir->mOutputs[i].size() > 8) return;
-    out.resize(mRows, mCir->mOutputs[i].size());
-    mFuseOut = &out;
-    mFuseOutIdx = i;
-}
-
 void Sh3BinaryEvaluator::getOutput(u64 i, sbMatrix& out) {
     if (i >= mCir->mOutputs.size()) throw RTE_LOC;
-    if (mFuseOutDone && i == mFuseOutIdx && &out == mFuseOut) return;  // read out by the last level
     const auto& wires = mCir->mOutputs[i];
     out.resize(mRows, wires.size());
     Gpu& g = *mGpu;

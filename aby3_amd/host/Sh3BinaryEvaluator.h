@@ -54,16 +54,16 @@ public:
         i64 constant = 0;
         i64* copyOut = nullptr;  // optional: receives sum_t coef[t] * term[t][.]
     };
+    // The terms are raw pointers and may be read by the first level's launch
+    // (fused inputs), which roundCallback enqueues later: a caller whose
+    // term buffer could go back to a pool before then hands it to
+    // holdForInputs first (kept until that launch is enqueued, then fenced).
     void setInputs(const std::vector<WireInput>& in);
+    void holdForInputs(std::shared_ptr<DeviceBuffer> b);
     Sh3Task asyncEvaluate(Sh3Task dep);
     Sh3Task asyncEvaluate(Sh3Task dep, BetaCircuit* cir, Sh3ShareGen& gen, std::vector<const sbMatrix*> inputs,
                           std::vector<sbMatrix*> outputs);
     void getOutput(u64 i, sbMatrix& out);
-    // getOutput(i, out) done by the evaluation's last level launch itself
-    // (outputs of at most 8 wires): call before asyncEvaluate; the later
-    // getOutput(i, out) then has nothing left to do. Falls back to the
-    // separate read-out when the circuit does not allow it.
-    void fuseOutput(u64 i, sbMatrix& out);
     // getOutput into mapped rows of an existing `out` (row map(p) <- circuit
     // row p; other rows untouched): the round's scatter
     void getOutput(u64 i, sbMatrix& out, const aby3g_rowmap& map);
@@ -102,8 +102,7 @@ private:
         bool fuseInputs = false;
         u32 inLo = 0, inHi = 0;
         bool inputsReadLater = false;
-        // the round whose launch is the evaluation's last (a few-bit output
-        // can be read out by it: aby3g_bin_level_out)
+        // the round whose launch is the evaluation's last
         u64 lastLaunchLevel = 0;
     };
     std::shared_ptr<DevCircuit> mCur;
@@ -129,14 +128,17 @@ private:
     // last level, instead of per level
     std::shared_ptr<DeviceBuffer> mSendAll;
     u64 mAndDone = 0;  // AND outputs of the levels already run (their rows in mSendAll)
+    bool mArenaLease = false;  // mSendAll is the channel's arena slot (Channel::evalSendBuffer)
     // setInputs' sources held for the first level's launch (DevCircuit::fuseInputs)
     std::vector<aby3g_wire_src> mPendingIn;
-    sbMatrix* mFuseOut = nullptr;  // fuseOutput's target, output mFuseOutIdx
-    u64 mFuseOutIdx = 0;
-    bool mFuseOutDone = false;
-    void flushPendingInputs();  // writes them to mMem the separate way
+    // buffers the held sources read (e.g. a received message): kept alive
+    // until the launch that reads them is enqueued (holdForInputs)
+    std::vector<std::shared_ptr<DeviceBuffer>> mPendingHold;
+    void readHeld(bool drop);
+    // writes them to mMem the separate way (dropHolds false: more held
+    // sources that read the same buffers follow)
+    void flushPendingInputs(bool dropHolds = true);
     bool pendingCoversInputs() const;
-    bool mergeRest(CommPkg& comm, Gpu& g);  // the remaining rounds as one launch (aby3g_bin_levels)
     int mZSlot = -1;
     aby3g_stream mZStream = nullptr;     // the stream the masks are drawn on
     std::unique_ptr<Event> mZEv, mZFresh; // draws done / main stream's position for fresh memory

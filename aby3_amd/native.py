@@ -163,7 +163,6 @@ _SIGS = {
     "aby3g_handoff_status": (c_int, [POINTER(ctypes.c_uint32)]),
     "aby3g_set_handoff_timeout_us": (c_int, [c_uint64]),
     "aby3g_bin_level_residency": (c_int, [POINTER(c_int), POINTER(c_int), POINTER(c_int), POINTER(c_int)]),
-    "aby3g_bin_levels_residency": (c_int, [POINTER(c_int), POINTER(c_int), POINTER(c_int), POINTER(c_int)]),
     "aby3g_stream_count": (c_int, [c_int, POINTER(c_int)]),
     "aby3g_malloc_uncached": (c_int, [POINTER(c_void_p), c_size_t]),
     "aby3g_device_uuid": (c_int, [c_int, c_void_p]),
@@ -188,11 +187,6 @@ _SIGS = {
     "aby3g_lin_copy_out": (c_int, [c_void_p, c_uint32, c_uint64, c_void_p]),
     "aby3g_bin_level_in": (c_int, [c_void_p, c_uint32, c_uint64, c_uint32, c_uint32, c_int, c_void_p, c_void_p,
                                    c_uint32, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "aby3g_bin_level_out": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_uint32, c_void_p,
-                                    c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint32,
-                                    c_void_p, c_uint64, c_void_p]),
-    "aby3g_bin_levels": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64,
-                                 c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_void_p, c_uint64, c_void_p]),
     "aby3g_bits_to_wires_lin": (c_int, [c_void_p, c_uint32, c_uint64, c_uint64, c_void_p]),
     "aby3g_bits_to_wires": (c_int, [c_void_p, c_uint64, c_uint64, c_uint32, c_void_p, c_uint64, c_void_p]),
     "aby3g_wires_to_bits": (c_int, [c_void_p, c_void_p, c_uint32, c_uint64, c_void_p, c_uint64, c_void_p]),

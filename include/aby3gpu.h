@@ -415,41 +415,6 @@ int aby3g_bin_level_hs(const aby3g_gate* gates, const uint32_t* recv_rows, const
  * (hipOccupancyMaxActiveBlocksPerMultiprocessor) -- the small-grid form
  * (launches of fewer than *small_max_wgs workgroups) and the large one. */
 int aby3g_bin_level_residency(int* cus, int* per_cu_small, int* per_cu_large, int* small_max_wgs);
-/* aby3g_bin_level_hs, then getOutput of a few-bit output (<= 8 wires, one
- * column; :1198-1404) fused into the same launch: out [2][rows] i64 receives
- * bit j of each row from out_wires[j], both shares, as aby3g_wires_to_bits2
- * would after this level -- for the last level of a circuit. */
-int aby3g_bin_level_out(const aby3g_gate* gates, const uint32_t* recv_rows, const uint32_t* batch_ends,
-                        uint32_t nbatches, const uint64_t* recvbuf, const uint32_t* unpack_wires, uint32_t nunpack,
-                        uint64_t* mem, uint64_t wires, uint64_t words, const uint64_t* z, uint64_t* sendbuf,
-                        const aby3g_handoff* wait, const aby3g_handoff* post, const uint32_t* out_wires,
-                        uint32_t nout, int64_t* out, uint64_t rows, aby3g_stream stream);
-/* Several consecutive levels in ONE launch (:539-1196, round after round),
- * for co-located parties whose messages all go in-kernel: each workgroup
- * carries its ABY3G_HANDOFF_ROWS chunk through the levels -- waits for the
- * previous party's same chunk of the previous level (wait->flags, seq
- * wait_seq of the level), unpacks, runs the level's batches, publishes its
- * send rows (post_flags, seq post_seq). Only the first level may receive by
- * a stream hand-off made before the launch (wait_seq 0). first_gate /
- * batch_off index gates (and recv_rows, 2 per gate) / batch_ends as for
- * aby3g_bin_level_rr; the optional few-bit output is read out at the end as
- * in aby3g_bin_level_out. At most ABY3G_LEVELS_MAX levels. The residency
- * rule of the hand-offs (a spinning consumer launch) applies to the whole
- * launch. */
-#define ABY3G_LEVELS_MAX 8
-typedef struct {
-    uint32_t first_gate, batch_off, nbatches, nunpack;
-    const uint32_t* unpack_wires;
-    const uint64_t* recv;
-    uint64_t* send;
-    uint64_t wait_seq, post_seq;
-} aby3g_level_run;
-/* residency of aby3g_bin_levels' two forms (workgroups per CU), as aby3g_bin_level_residency */
-int aby3g_bin_levels_residency(int* cus, int* per_cu_small, int* per_cu_large, int* small_max_wgs);
-int aby3g_bin_levels(const aby3g_level_run* runs, uint32_t nruns, const aby3g_gate* gates, const uint32_t* recv_rows,
-                     const uint32_t* batch_ends, uint64_t* mem, uint64_t wires, uint64_t words, const uint64_t* z,
-                     const aby3g_handoff* wait, uint64_t* post_flags, const uint32_t* out_wires, uint32_t nout,
-                     int64_t* out, uint64_t rows, aby3g_stream stream);
 int aby3g_bin_unpack(const uint64_t* recvbuf, const uint32_t* out_wires, uint32_t n, uint64_t* mem, uint64_t wires,
                      uint64_t words, aby3g_stream stream);
 /* setInput (:200-276): bit-transpose a [rows][cols64] i64 share matrix into
@@ -536,7 +501,8 @@ int aby3g_lin_copy_out(const aby3g_wire_src* srcs, uint32_t nsrc, uint64_t rows,
  * ABY3G_LEVEL_IN_MAX_WIRES) from LDS and every other wire from mem. The
  * input wires reach mem only when write_inputs != 0 (a later level reads
  * them). Sources' wire_rows name their wires in mem as for
- * aby3g_bits_to_wires_lin. post: the level's AND shares handed over
+ * aby3g_bits_to_wires_lin; a source without terms is all zero and must have
+ * constant 0 (rejected otherwise). post: the level's AND shares handed over
  * in-kernel (aby3g_handoff), or NULL. */
 #define ABY3G_LEVEL_IN_MAX_WIRES 128
 int aby3g_bin_level_in(const aby3g_wire_src* srcs, uint32_t nsrc, uint64_t rows, uint32_t in_lo, uint32_t in_hi,

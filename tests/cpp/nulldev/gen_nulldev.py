@@ -22,7 +22,8 @@ OVERRIDES = {
     "aby3g_malloc": "*ptr = nd_alloc(bytes); return *ptr ? 0 : 1;",
     "aby3g_malloc_uncached": "*ptr = nd_alloc(bytes); return *ptr ? 0 : 1;",
     "aby3g_device_uuid": "memset(uuid, 0, 16); uuid[0] = (uint8_t)device; return 0;",
-    "aby3g_free": "nd_free(ptr); return 0;",
+    "aby3g_free": "g_blocking.fetch_add(1); nd_free(ptr); return 0;",
+    "aby3g_device_sync": "g_blocking.fetch_add(1); return 0;",
     "aby3g_host_malloc": "*ptr = calloc(1, bytes ? bytes : 1); return *ptr ? 0 : 1;",
     "aby3g_host_free": "free(ptr); return 0;",
     "aby3g_memcpy": "if (kind == 3) g_kind3.fetch_add(1); if (bytes) memmove(dst, src, bytes); return 0;",
@@ -35,7 +36,7 @@ OVERRIDES = {
     "aby3g_event_record": "*(int*)ev = 1; return 0;",
     "aby3g_event_elapsed_ms": "*ms = 0; return 0;",
     "aby3g_event_query": "*done = 1; return 0;",
-    "aby3g_signal_alloc": "*word = (uint64_t*)calloc(1, 8); return *word ? 0 : 1;",
+    "aby3g_signal_alloc": "g_blocking.fetch_add(1); *word = (uint64_t*)calloc(1, 8); return *word ? 0 : 1;",
     "aby3g_stream_write_value": "__atomic_store_n(word, value, __ATOMIC_RELEASE); return 0;",
     "aby3g_stream_wait_value": "return nd_wait(word, value);",
     "aby3g_ipc_get_handle": "memset(handle, 0, sizeof *handle); memcpy(handle->bytes, &ptr, sizeof ptr); return 0;",
@@ -45,7 +46,6 @@ OVERRIDES = {
     "aby3g_handoff_status": "*timeouts = 0; return 0;",
     "aby3g_stream_count": "*n = 0; return 0;",
     "aby3g_bin_level_residency": "*cus = 256; *per_cu_small = 1; *per_cu_large = 5; *small_max_wgs = 128; return 0;",
-    "aby3g_bin_levels_residency": "*cus = 256; *per_cu_small = 1; *per_cu_large = 10; *small_max_wgs = 128; return 0;",
     "aby3g_aes_block_host": "for (int i = 0; i < 16; ++i) out[i] = key[i] ^ (uint8_t)(ctr >> (8 * (i & 7))); return 0;",
     "aby3g_lr_mailbox_bytes": "return 4096;",
     "aby3g_lr_scratch_bytes": "return 4096;",
@@ -73,6 +73,12 @@ constexpr int ND_DEVICES = 3;
 static thread_local int t_device = 0;
 static std::atomic<unsigned> g_peer{0};       // bit 3 * device + peer: access enabled
 static std::atomic<unsigned long> g_kind3{0}; // copies between devices (kind 3)
+// calls that wait for the whole device on real hardware (hipDeviceSynchronize,
+// hipFree, the synchronous zeroing of a signal word): none may happen while a
+// party's protocol runs -- a host blocked in one cannot enqueue the producer
+// that another party's spinning consumer waits for
+static std::atomic<unsigned long> g_blocking{0};
+extern "C" unsigned long nulldev_blocking_calls() { return g_blocking.load(); }
 static int nd_peer(int device, int peer) {
     if (device < 0 || peer < 0 || device >= ND_DEVICES || peer >= ND_DEVICES || device == peer) return 1;
     g_peer.fetch_or(1u << (3 * device + peer));

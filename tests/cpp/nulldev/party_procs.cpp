@@ -14,6 +14,7 @@
 
 extern "C" int nulldev_shared_arena(size_t bytes);
 extern "C" void nulldev_stats(unsigned* peer_bits, unsigned long* kind3_copies);
+extern "C" unsigned long nulldev_blocking_calls();
 
 // ownDevice: party p on device p (the north-star layout, three GPUs): the
 // receiver's copy out of the sender's staging slot is then a peer copy
@@ -37,7 +38,19 @@ static int party_main(int party, const std::string& tag, bool ownDevice) {
             std::printf("FAIL party %d create job %d: %s\n", party, j.job, aby3h_last_error());
             return 1;
         }
-        if (aby3h_session_run(s, j.steps) || aby3h_session_check(s) == 2) {
+        const unsigned long b0 = nulldev_blocking_calls();
+        if (aby3h_session_run(s, j.steps)) {
+            std::printf("FAIL party %d job %d: %s\n", party, j.job, aby3h_last_error());
+            return 1;
+        }
+        // no device-wide wait while the parties run (a host blocked in one
+        // cannot enqueue what a peer's waiting kernel needs)
+        if (nulldev_blocking_calls() != b0) {
+            std::printf("FAIL party %d job %d: %lu device-wide waits inside session_run\n", party, j.job,
+                        nulldev_blocking_calls() - b0);
+            return 1;
+        }
+        if (aby3h_session_check(s) == 2) {
             std::printf("FAIL party %d job %d: %s\n", party, j.job, aby3h_last_error());
             return 1;
         }

@@ -8,6 +8,7 @@
 #include <vector>
 
 extern "C" void nulldev_stats(unsigned* peer_bits, unsigned long* kind3_copies);
+extern "C" unsigned long nulldev_blocking_calls();
 
 static int fail(const char* what) {
     std::printf("FAIL %s: %s\n", what, aby3h_last_error());
@@ -35,7 +36,15 @@ int main() {
             aby3h_session* s =
                 aby3h_session_create(j.job, j.p.data(), (int)j.p.size(), round == 2 ? dev3 : dev, round == 1);
             if (!s) return fail("create");
+            // no device-wide wait while the parties run (the r04h
+            // hand-off timeouts): setup may synchronise, a step may not
+            const unsigned long b0 = nulldev_blocking_calls();
             if (aby3h_session_run(s, j.steps)) return fail("run");
+            if (nulldev_blocking_calls() != b0) {
+                std::printf("FAIL job %d round %d: %lu device-wide waits (sync / free / signal-word zeroing) "
+                            "inside session_run\n", j.job, round, nulldev_blocking_calls() - b0);
+                return 1;
+            }
             if (aby3h_session_check(s) == 2) return fail("check");
             double ms;
             uint64_t n;

@@ -159,6 +159,19 @@ static void handoff_residency_test() {
     CHECK(!handoffResidencyOk(s, 38));
     CHECK(!handoffResidencyOk(s, 100));  // small form (16-wave workgroups), 2 * 100 + 5 > 80
     CHECK(handoffResidencyOk(s, 185));   // large form: 2 * 37 + 5 = 79
+    // three processes on one GPU (the IPC arenas): three processes' queues of
+    // stream-op waits, 2 * 103 + 12 + 1 = 219 CUs for 2^20-row messages
+    r = HandoffResidency{256, 1, 5, 128, 4};
+    CHECK(handoffResidencyOk(r, 512, 3));
+    CHECK(handoffResidencyOk(r, 500, 3));
+    CHECK(handoffResidencyOk(r, 605, 3));   // 2 * 121 + 13 = 255
+    CHECK(!handoffResidencyOk(r, 606, 3));
+    r.perCuLarge = 4;
+    CHECK(!handoffResidencyOk(r, 500, 3));  // 2 * 125 + 13 > 256
+    CHECK(handoffResidencyOk(r, 484, 3));   // 2 * 121 + 13 = 255
+    CHECK(!handoffResidencyOk(r, 485, 3));
+    r.perCuLarge = 5;
+    CHECK(!handoffResidencyOk(r, 512, 0));  // no process count, no hand-off
     // a kernel that cannot be resident at all never hands off in-kernel
     HandoffResidency z{256, 0, 0, 128, 4};
     CHECK(!handoffResidencyOk(z, 1));

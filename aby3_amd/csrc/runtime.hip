@@ -51,45 +51,63 @@ struct Probe {
 };
 thread_local Probe t_probe;
 
-// FIPS-197 S-box from its definition (inverse in GF(2^8), then the affine map).
+// FIPS-197 S-box from its definition (inverse in GF(2^8), then the affine
+// map), evaluated at compile time: the host keeps a copy and the T-table is a
+// device global initialised by the code object's loader, so no copy -- and no
+// null-stream operation -- is needed to get it onto a device (a null-stream
+// memcpy at the first AES launch would create the null stream's hardware
+// queue mid-run and could block behind a spinning kernel).
+constexpr u8 gf_mul(u8 a, u8 b) {
+    u8 p = 0;
+    for (int i = 0; i < 8; ++i) {
+        if (b & 1) p ^= a;
+        const bool hi = a & 0x80;
+        a = (u8)(a << 1);
+        if (hi) a ^= 0x1b;
+        b >>= 1;
+    }
+    return p;
+}
+constexpr u8 gf_inv(u8 x) {  // x^254 (0 -> 0)
+    u8 r = 1, base = x;
+    for (unsigned e = 254; e; e >>= 1) {
+        if (e & 1) r = gf_mul(r, base);
+        base = gf_mul(base, base);
+    }
+    return x ? r : 0;
+}
 struct Tables {
     u8 sbox[256];
     u32 T0[256];
-    Tables() {
-        auto gmul = [](u8 a, u8 b) {
-            u8 p = 0;
-            for (int i = 0; i < 8; ++i) {
-                if (b & 1) p ^= a;
-                bool hi = a & 0x80;
-                a = (u8)(a << 1);
-                if (hi) a ^= 0x1b;
-                b >>= 1;
-            }
-            return p;
-        };
-        for (int x = 0; x < 256; ++x) {
-            u8 inv = 0;
-            for (int y = 1; x && y < 256; ++y)
-                if (gmul((u8)x, (u8)y) == 1) {
-                    inv = (u8)y;
-                    break;
-                }
-            u8 r = 0x63;
-            for (int i = 0; i < 8; ++i) {
-                int bit = ((inv >> i) ^ (inv >> ((i + 4) & 7)) ^ (inv >> ((i + 5) & 7)) ^ (inv >> ((i + 6) & 7)) ^
-                           (inv >> ((i + 7) & 7))) & 1;
-                r ^= (u8)(bit << i);
-            }
-            sbox[x] = r;
-            u8 s = r, s2 = gmul(r, 2), s3 = gmul(r, 3);
-            T0[x] = (u32)s2 | ((u32)s << 8) | ((u32)s << 16) | ((u32)s3 << 24);
-        }
-    }
 };
-const Tables& tables() {
-    static Tables t;
+constexpr Tables make_tables() {
+    Tables t{};
+    for (int x = 0; x < 256; ++x) {
+        const u8 inv = gf_inv((u8)x);
+        u8 r = 0x63;
+        for (int i = 0; i < 8; ++i) {
+            const int bit = ((inv >> i) ^ (inv >> ((i + 4) & 7)) ^ (inv >> ((i + 5) & 7)) ^ (inv >> ((i + 6) & 7)) ^
+                             (inv >> ((i + 7) & 7))) & 1;
+            r ^= (u8)(bit << i);
+        }
+        t.sbox[x] = r;
+        const u8 s2 = gf_mul(r, 2), s3 = gf_mul(r, 3);
+        t.T0[x] = (u32)s2 | ((u32)r << 8) | ((u32)r << 16) | ((u32)s3 << 24);
+    }
     return t;
 }
+constexpr Tables kTables = make_tables();
+static_assert(kTables.sbox[0] == 0x63 && kTables.sbox[1] == 0x7c && kTables.sbox[0x53] == 0xed, "FIPS-197 S-box");
+const Tables& tables() { return kTables; }
+struct T0Table {
+    u32 v[256];
+};
+constexpr T0Table make_t0() {
+    T0Table t{};
+    for (int i = 0; i < 256; ++i) t.v[i] = kTables.T0[i];
+    return t;
+}
+__device__ const T0Table g_aes_t0 = make_t0();
 
 std::mutex g_tab_mu;
 std::map<int, u32*> g_tab_dev;
@@ -162,11 +180,10 @@ const u32* aes_table() {
     std::lock_guard<std::mutex> lk(g_tab_mu);
     auto it = g_tab_dev.find(dev);
     if (it != g_tab_dev.end()) return it->second;
-    u32* p = nullptr;
-    ABY3G_CHECK_HIP(hipMalloc(&p, sizeof(tables().T0)));
-    ABY3G_CHECK_HIP(hipMemcpy(p, tables().T0, sizeof(tables().T0), hipMemcpyHostToDevice));
-    g_tab_dev[dev] = p;
-    return p;
+    void* p = nullptr;
+    ABY3G_CHECK_HIP(hipGetSymbolAddress(&p, HIP_SYMBOL(g_aes_t0)));
+    g_tab_dev[dev] = (u32*)p;
+    return (u32*)p;
 }
 
 namespace {
@@ -342,8 +359,15 @@ int aby3g_signal_alloc(uint64_t** word) {
     return guarded([&] {
         ABY3G_REQUIRE(word != nullptr, "null word");
         ABY3G_CHECK_HIP(hipMalloc(word, sizeof(uint64_t)));
-        ABY3G_CHECK_HIP(hipMemset(*word, 0, sizeof(uint64_t)));
-        ABY3G_CHECK_HIP(hipDeviceSynchronize());
+        // zeroed on a stream of its own and waited for, not on the null
+        // stream (whose hardware queue would be created here and shared with
+        // a party's stream)
+        hipStream_t s;
+        ABY3G_CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        const hipError_t e1 = hipMemsetAsync(*word, 0, sizeof(uint64_t), s);
+        const hipError_t e2 = e1 == hipSuccess ? hipStreamSynchronize(s) : e1;
+        (void)hipStreamDestroy(s);
+        ABY3G_CHECK_HIP(e2);
     });
 }
 int aby3g_stream_write_value(aby3g_stream stream, uint64_t* word, uint64_t value) {

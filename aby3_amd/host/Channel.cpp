@@ -870,7 +870,10 @@ std::vector<CommPkg> makeLocalRing(const int* devices, bool kernelHandoff) {
                 }
             }
     // every same-device direction's signal word, zeroed now, before any
-    // party's work is enqueued (aby3g_signal_alloc waits for the device)
+    // party's work is enqueued (aby3g_signal_alloc zeroes it on a stream of
+    // its own: a null-stream memset here created the null stream's hardware
+    // queue ahead of the parties' streams and shifted which streams share a
+    // queue -- C3 0.41 against 0.334 ms in a same-box A/B)
     if (devices) {
         int cur = 0;
         GPU_CALL(aby3g_get_device(&cur));
@@ -891,7 +894,8 @@ std::vector<CommPkg> makeLocalRing(const int* devices, bool kernelHandoff) {
     return c;
 }
 
-CommPkg makeProcessRing(int party, const std::string& link, int device, bool sameDevice) {
+CommPkg makeProcessRing(int party, const std::string& link, int device, bool sameDevice, bool forceRemote) {
+    if (forceRemote) sameDevice = false;  // no arenas: staged copies, as between GPUs
     if (party < 0 || party > 2) throw std::runtime_error("makeProcessRing: party must be 0, 1 or 2");
     if (link.empty() || link.find('/') != std::string::npos)
         throw std::runtime_error("makeProcessRing: link name must be non-empty without '/'");
@@ -972,6 +976,7 @@ CommPkg makeProcessRing(int party, const std::string& link, int device, bool sam
     CommPkg c;
     c.mNext = Channel(pipes[party][nx], pipes[nx][party]);
     c.mPrev = Channel(pipes[party][pv], pipes[pv][party]);
+    c.forceRemote = forceRemote;
     return c;
 }
 

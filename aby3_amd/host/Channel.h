@@ -126,6 +126,12 @@ private:
 
 struct CommPkg {
     Channel mPrev, mNext;
+    // one party per process, all three on one GPU, but every branch taken as
+    // if each party had a GPU of its own (makeProcessRing's forceRemote): the
+    // staged IPC copies for every device message and the fused LR
+    // iteration's system-scope mailboxes -- the north-star layout's code
+    // paths, run on a one-GPU box
+    bool forceRemote = false;
 };
 
 // Host time this thread has spent inside receives waiting for messages (us).
@@ -185,6 +191,7 @@ std::vector<CommPkg> makeLocalRing(const int* devices = nullptr, bool kernelHand
 // zero-copy send (asyncSendShared) becomes such a staged copy.
 // sameDevice: the three processes share this GPU; the binary engine's level
 // messages then go in-kernel through IPC-mapped arenas (one per direction).
-CommPkg makeProcessRing(int party, const std::string& link, int device, bool sameDevice = false);
+CommPkg makeProcessRing(int party, const std::string& link, int device, bool sameDevice = false,
+                        bool forceRemote = false);
 
 }  // namespace aby3

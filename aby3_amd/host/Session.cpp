@@ -414,6 +414,7 @@ struct LrJob : Job {
     void info(double* o) override {
         o[ABY3H_INFO_MULTS_PER_STEP] = 2.0 * B * d;
         o[ABY3H_INFO_LR_FUSED] = (st[0].fused || st[1].fused || st[2].fused) ? 1 : 0;
+        o[ABY3H_INFO_LR_SYS_SCOPE] = (st[0].fusedSysScope || st[1].fusedSysScope || st[2].fusedSysScope) ? 1 : 0;
     }
     const SharedMat* result(int i) const override { return &sW[i]; }
 };
@@ -424,7 +425,8 @@ struct SortJob : Job {
     i64Matrix k;
     sbMatrix S[3], R[3];
     CircuitLibrary lib;
-    explicit SortJob(u64 keys) : n(keys) {
+    MergeOrder order;
+    explicit SortJob(u64 keys, u64 ord = 0) : n(keys), order(ord ? MergeOrder::Sequential : MergeOrder::Batched) {
         if (!n || n > (1ull << 20)) throw std::runtime_error("sort job: 1 .. 2^20 keys");
         // distinct keys below 2^63, the low 20 bits an index tag (tag_append,
         // BoolBasic.cpp:992-1004): signed and unsigned order agree
@@ -439,7 +441,9 @@ struct SortJob : Job {
         else
             p.enc.remoteBinMatrix(p.rt, S[p.idx]).get();
     }
-    void step(PartyCtx& p) override { odd_even_merge_sort(S[p.idx], R[p.idx], p.idx, p.eval, p.rt); }
+    void step(PartyCtx& p) override {
+        odd_even_multi_merge(S[p.idx], std::vector<u64>(n, 1), R[p.idx], p.idx, p.eval, p.rt, order);
+    }
     const SharedMat* result(int i) const override { return &R[i]; }
     // every key, in order: the revealed output equals std::sort of the input
     bool check(PartyCtx& p) override {
@@ -453,7 +457,7 @@ struct SortJob : Job {
     void info(double* o) override {
         BetaCircuit* c = lib.cmp_swap(64);
         double andW = 0, gateW = 0, bytes = 0;
-        for (u64 rows : multiMergeEvalRows(std::vector<u64>(n, 1))) {
+        for (u64 rows : multiMergeEvalRows(std::vector<u64>(n, 1), order == MergeOrder::Sequential)) {
             const double words = std::ceil(rows / 64.0), padded = 32.0 * ((rows + 2047) / 2048);
             andW += c->mAndCount * words;
             gateW += c->mGates.size() * words;
@@ -656,7 +660,7 @@ std::unique_ptr<Job> makeJob(int job, const uint64_t* params, int nparams) {
         case ABY3H_JOB_MSB: return std::make_unique<MsbJob>(P(0, 1 << 20));
         case ABY3H_JOB_LR:
             return std::make_unique<LrJob>(P(0, 1000000), P(1, 128), P(2, 256), P(3, 16), P(4, 11), P(5, 0));
-        case ABY3H_JOB_SORT: return std::make_unique<SortJob>(P(0, 1 << 20));
+        case ABY3H_JOB_SORT: return std::make_unique<SortJob>(P(0, 1 << 20), P(1, 0));
         case ABY3H_JOB_A2B: return std::make_unique<A2bJob>(P(0, 1 << 20));
         case ABY3H_JOB_BITINJ: return std::make_unique<BitInjJob>(P(0, 1 << 16), P(1, 64));
         default: throw std::runtime_error("unknown job");
@@ -728,7 +732,8 @@ aby3h_session* aby3h_party_create(int job, const uint64_t* params, int nparams, 
         s.job = makeJob(job, params, nparams);
         s.locals = {party};
         s.comms.resize(3);
-        s.comms[(size_t)party] = makeProcessRing(party, link, device, colocated != 0);
+        if (colocated < 0 || colocated > 2) throw std::runtime_error("colocated must be 0, 1 or 2");
+        s.comms[(size_t)party] = makeProcessRing(party, link, device, colocated == 1, colocated == 2);
         s.devices[party] = device;
         s.colocated = colocated != 0;
         s.turnNext = party;  // stream-creation turns: only this party's here

@@ -115,7 +115,7 @@ std::vector<u64> mergeBatchEvalRows(const std::vector<MergeSpec>& ms) {
     return rows;
 }
 
-std::vector<u64> multiMergeEvalRows(std::vector<u64> lens) {
+std::vector<u64> multiMergeEvalRows(std::vector<u64> lens, bool sequential) {
     std::vector<u64> rows;
     while (lens.size() > 1) {
         const size_t k = lens.size();
@@ -134,7 +134,11 @@ std::vector<u64> multiMergeEvalRows(std::vector<u64> lens) {
             }
             lens = std::move(next);
         }
-        for (u64 r : mergeBatchEvalRows(ms)) rows.push_back(r);
+        if (sequential)  // one merge after the other: each its own evaluations
+            for (const MergeSpec& m : ms)
+                for (u64 r : mergeBatchEvalRows({m})) rows.push_back(r);
+        else
+            for (u64 r : mergeBatchEvalRows(ms)) rows.push_back(r);
     }
     return rows;
 }

@@ -48,7 +48,7 @@ struct MergeSpec {
 // Rows of each cmp_swap evaluation a batch / a multi-merge runs (chunks of
 // kMaxSendingSize counted separately): the work accounting of bench jobs.
 std::vector<u64> mergeBatchEvalRows(const std::vector<MergeSpec>& merges);
-std::vector<u64> multiMergeEvalRows(std::vector<u64> lens);
+std::vector<u64> multiMergeEvalRows(std::vector<u64> lens, bool sequential = false);
 // Run a batch of merges over the 64-bit sbMatrix `data` (one word per row).
 void mergeBatch(sbMatrix& data, const std::vector<MergeSpec>& merges, int pIdx, Sh3Evaluator& eval,
                 Sh3Runtime& runtime);

@@ -119,7 +119,9 @@ struct FusedLr {
         comm.mPrev.asyncSendCopy(uuid, 16);
         comm.mNext.recv(un, 16);
         comm.mPrev.recv(up, 16);
-        f->sysScope = std::memcmp(un, uuid, 16) != 0 || std::memcmp(up, uuid, 16) != 0;
+        // (forceRemote: the three-GPU branch on one GPU, for tests and the
+        // bench -- uncached mailboxes and system-scope messages)
+        f->sysScope = comm.forceRemote || std::memcmp(un, uuid, 16) != 0 || std::memcmp(up, uuid, 16) != 0;
         GPU_CALL(aby3g_set_device(g.device()));
         GPU_CALL(f->sysScope ? aby3g_malloc_uncached(&f->ownBox, mb) : aby3g_malloc(&f->ownBox, mb));
         GPU_CALL(aby3g_memset(f->ownBox, 0, mb, g.stream()));
@@ -317,6 +319,7 @@ void sgdLogisticStep(aby3ML& ml, const si64Matrix& X, const si64Matrix& Y, si64M
     if (!st.fusedChecked) {
         st.fused = FusedLr::make(ml, X.cols(), B);
         st.fusedChecked = true;
+        st.fusedSysScope = st.fused && st.fused->sysScope;
     }
     if (st.fused && st.fused->B == B && st.fused->d == X.cols()) {
         st.fused->step(ml, X, Y, w, batchIdx, aB, st.phaseTicks, st.nextBatch);

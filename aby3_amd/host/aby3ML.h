@@ -39,6 +39,7 @@ struct SgdState {
     // parties take together.
     std::shared_ptr<FusedLr> fused;
     bool fusedChecked = false;
+    bool fusedSysScope = false;  // the fused iteration's messages are system-scope (parties on other GPUs)
     u64* phaseTicks = nullptr;  // optional device [32]: the fused launch's phase stamps (profiling)
     const u32* nextBatch = nullptr;  // optional: the next iteration's batch (its rows prefetched into L2)
 };

@@ -235,7 +235,7 @@ class _Lib:
 JOB_MUL_TRUNC, JOB_MUL, JOB_MSB, JOB_LR, JOB_SORT, JOB_A2B, JOB_BITINJ = range(7)
 INFO = dict(mults_per_step=0, gemm_int8_ops=1, and_words=2, gate_words=3, gate_bytes=4, bytes_sent=5,
             host_enqueue_us=6, host_drain_us=7, host_recv_wait_us=8, host_api_us=9, host_api_calls=10,
-            device_wait_us=11, lr_fused=12)
+            device_wait_us=11, lr_fused=12, lr_sys_scope=13)
 
 _HOST_SIGS = {
     "aby3h_last_error": (c_char_p, []),
@@ -301,10 +301,12 @@ class Session:
         self.host = h
 
     @classmethod
-    def party(cls, job: int, params, party: int, link: str, device: int = 0, colocated: bool = True,
+    def party(cls, job: int, params, party: int, link: str, device: int = 0, colocated: int = 1,
               probe=False):
         """One party of a session in this process (aby3h_party_create): the
-        three processes pass the same job, params and link name."""
+        three processes pass the same job, params and link name. colocated:
+        0 parties on different GPUs, 1 on this one, 2 on this one taking the
+        cross-GPU branches (aby3.h)."""
         self = cls.__new__(cls)
         h = host()
         p = (c_uint64 * len(params))(*params)

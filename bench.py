@@ -192,6 +192,20 @@ def timed(sess, steps, pg, secs=0.0, warmup=0):
     return allmax(pg, t1 - t0)
 
 
+def cpu_mul_procs_s(mode, reps):
+    """Seconds per C1 multiplication of the oracle as BASELINE configs[0]
+    states it: three CPU processes, one party each, the reshare crossing
+    between them (oracle/src/orc_c1_procs.cpp; cpu_baseline leg only)."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "oracle", "build", "orc_c1_procs")
+    r = subprocess.run([exe, str(mode), "128", "128", "128", str(reps)], capture_output=True, text=True,
+                       timeout=600)
+    if r.returncode != 0:
+        raise SystemExit(f"bench: oracle C1 process baseline failed ({r.returncode}): {r.stderr[-500:]}")
+    return json.loads(r.stdout.strip().splitlines()[-1])["secs"] / reps
+
+
 def cpu_mul_s(mode, reps):
     """Seconds per C1 multiplication of the oracle (cpu_baseline leg only)."""
     import ctypes
@@ -204,7 +218,7 @@ def cpu_mul_s(mode, reps):
     return secs / reps
 
 
-def party_job(job, params, steps, warmup=0):
+def party_job(job, params, steps, warmup=0, layout=1):
     """A job in the north_star's process layout: three processes, one party
     each (aby3h_party_create), on this node's GPU 0 (the driver's boxes have
     one GPU, so the three share it), messages over the shared-memory links
@@ -215,7 +229,8 @@ def party_job(job, params, steps, warmup=0):
     link = f"bench{os.getpid()}.{job}.{len(params)}"
     env = dict(os.environ, ABY3_LINK_TIMEOUT_S="120", ABY3_WARMUP_STEPS=str(warmup))
     procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "party_worker.py"), str(job), str(p),
-                               str(steps), link, "0", ",".join(str(x) for x in params)], stdout=subprocess.PIPE,
+                               str(steps), link, "0", ",".join(str(x) for x in params), str(layout)],
+                              stdout=subprocess.PIPE,
                               stderr=subprocess.PIPE, text=True, env=env)
              for p in range(3)]
     outs = []
@@ -404,6 +419,26 @@ def extras(args, nt, dev, world, pg):
                 "est_full_sort_s": info["and_words"] / rate,
             }
             res["merge_sort"]["speedup_vs_cpu_baseline"] = res["merge_sort"]["and_word_gates_per_s"] / rate
+    # The reference's own merge order (Sort.cpp:413-437: odd_even_multi_merge
+    # calls odd_even_merge for one pair after the other), whose randomness
+    # draws -- and so shares -- the batched form does not reproduce: priced at
+    # 2^14 keys, beside the batched order at the same size.
+    seq_keys = 1 << 14
+    seq = {"workload": f"odd_even_merge_sort of {seq_keys} 64-bit keys in the reference's order "
+                       "(MergeOrder::Sequential: every pairwise merge its own cmp_swap evaluations, one after "
+                       "the other), 3 parties; beside it the batched order at the same size", "keys": seq_keys}
+    for order, name in ((1, "sequential"), (0, "batched")):
+        with nt.Session(nt.JOB_SORT, [seq_keys, order], devices=(dev,) * 3, probe=False) as s:
+            s.run(1)
+            reps = 1 if order else 20
+            dt = timed(s, reps, pg)
+            if not s.check():
+                raise SystemExit(f"bench: {name} merge sort output differs from std::sort of the keys")
+            info = s.info()
+            seq[name] = {"ms_per_sort": dt / reps * 1e3, "and_words_per_sort": info["and_words"],
+                         "and_word_gates_per_s": world * reps * info["and_words"] / dt}
+    seq["sequential_over_batched"] = seq["sequential"]["ms_per_sort"] / seq["batched"]["ms_per_sort"]
+    res["merge_sort"]["sequential"] = seq
     # C1: asyncMul 128x128, both modes, no truncation
     res["c1_mul"] = {}
     for mode, name in ((0, "hadamard"), (1, "gemm")):
@@ -417,11 +452,17 @@ def extras(args, nt, dev, world, pg):
             e = {"workload": f"asyncMul 128x128 si64 ({name}{', 128x128x128' if mode else ''}), 3 parties",
                  "ms_per_mul": dt / reps * 1e3, "mults_per_s": world * reps * mults / dt}
             if world == 1 and not args.no_cpu_baseline:
-                cpu_s = cpu_mul_s(mode, 2000 if mode == 0 else 300)
+                n_cpu = 2000 if mode == 0 else 300
+                cpu_s = cpu_mul_procs_s(mode, n_cpu)
                 e["cpu_baseline"] = {
                     "value": mults / cpu_s, "unit": "mults/s", "cores": 3, "kind": "port",
-                    "sample": f"{2000 if mode == 0 else 300} x asyncMul 128x128 ({name}): the oracle's local share "
-                              "product + zero-share per party (3 party threads), ring reshare as a copy"}
+                    "sample": f"{n_cpu} x asyncMul 128x128 ({name}) as configs[0] states it: three CPU processes, one "
+                              "party each (oracle/build/orc_c1_procs), each computing its local share product + "
+                              "zero-share and sending it to the next party through a shared-memory mailbox (a copy "
+                              "in and a copy out, as through a localhost socket)"}
+                e["cpu_baseline_threads"] = {
+                    "value": mults / cpu_mul_s(mode, n_cpu), "unit": "mults/s", "cores": 3,
+                    "sample": "the same with the parties as three threads of one process, the reshare a copy"}
                 e["speedup_vs_cpu_baseline"] = e["mults_per_s"] / e["cpu_baseline"]["value"]
             res["c1_mul"][name] = e
     # share conversions, each checked on its revealed output
@@ -723,6 +764,21 @@ def main():
                                     "(the fused launch over IPC-mapped mailboxes)",
                         "ms_per_iteration": ms,
                         "fused": all(o["lr_fused"] == 1 for o in outs)}
+            # the three-GPU layout's branches on this GPU (aby3h_party_create
+            # colocated = 2): uncached mailboxes + system-scope messages for the
+            # fused iteration, staged IPC copies for every C2 device message
+            ms, outs = party_job(nt.JOB_LR, [args.lr_rows, 128, 256, 16, 11], LR_ITERS, warmup=1000, layout=2)
+            pp["c4_remote_branches"] = {
+                "workload": f"SGD_Logistic iteration, {args.lr_rows}x128, batch 256, one party per process, the "
+                            "cross-GPU branches forced on GPU 0 (uncached mailboxes, system-scope messages)",
+                "ms_per_iteration": ms,
+                "fused": all(o["lr_fused"] == 1 for o in outs),
+                "sys_scope": all(o["lr_sys_scope"] == 1 for o in outs)}
+            ms, outs = party_job(nt.JOB_MUL_TRUNC, [M, K, N, D, 1], 30, warmup=100, layout=2)
+            pp["c2_remote_branches"] = {
+                "workload": "the C2 multiplication, one party per process, the cross-GPU branches forced on GPU 0 "
+                            "(every z message a staged copy out of the sender's IPC slot, no arenas)",
+                "ms_per_step": ms}
             out["extras"]["party_processes"] = pp
             # the verdict's flat keys
             pp["ms_per_step"] = pp["c2"]["ms_per_step"]

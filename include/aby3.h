@@ -43,9 +43,12 @@ enum {
      * kept in HBM; 1: each step draws its batch with getSubset
      * (DeviceBatchSampler, the pool resident in HBM) inside the step. */
     ABY3H_JOB_LR = 3,
-    /* params: keys. One step = odd_even_merge_sort of `keys` 64-bit keys
-     * (distinct, (U[0, 2^43) << 20) | i): the multi-merge of singleton lists,
-     * every round of every level one cmp_swap evaluation (Sort.cpp:413-628). */
+    /* params: keys, order. One step = odd_even_merge_sort of `keys` 64-bit
+     * keys (distinct, (U[0, 2^43) << 20) | i): the multi-merge of singleton
+     * lists (Sort.cpp:413-628). order 0 (default): batched, every round of
+     * every level one cmp_swap evaluation; 1: sequential, the reference's
+     * loop of one odd_even_merge after another (Sort.cpp:423-429), so the
+     * reference's order of randomness draws and shares (MergeOrder). */
     ABY3H_JOB_SORT = 4,
     /* params: rows. One step = Sh3Converter::toBinaryMatrix of rows x 1
      * 64-bit values (resharing + 64-bit adder, Sh3Converter.cpp:61-207). */
@@ -70,7 +73,8 @@ enum {
     ABY3H_INFO_HOST_API_CALLS = 10,   /* last run: aby3g_* calls per step (party 0) */
     ABY3H_INFO_DEVICE_WAIT_US = 11,   /* last run: in-kernel wait for peers per step and party (us, mean of the local parties) */
     ABY3H_INFO_LR_FUSED = 12,         /* JOB_LR: 1 when the iterations ran as the fused launch (aby3g_lr_iteration) */
-    ABY3H_INFO_COUNT = 13
+    ABY3H_INFO_LR_SYS_SCOPE = 13,     /* JOB_LR: 1 when that launch's messages were system-scope (uncached mailboxes) */
+    ABY3H_INFO_COUNT = 14
 };
 
 const char* aby3h_last_error(void);
@@ -85,8 +89,12 @@ aby3h_session* aby3h_session_create(int job, const uint64_t* params, int nparams
  * its own party 0..2 and device; the call returns once the session is set up
  * in all three. The parties' messages travel over shared-memory links (host
  * control words) and IPC-exported device staging slots (payloads; peer reads
- * over xGMI between GPUs). colocated != 0: other parties share this party's
- * GPU (one stream per party). Every aby3h_session_* call below must then be
+ * over xGMI between GPUs). colocated: 0 = the parties run on different GPUs;
+ * 1 = other parties share this party's GPU (one stream per party, in-kernel
+ * hand-offs through IPC-mapped arenas); 2 = they share it, but every
+ * cross-GPU branch is taken as if they did not (staged copies for every
+ * device message, the fused LR iteration's uncached mailboxes and
+ * system-scope messages) -- the north-star layout's code on one GPU. Every aby3h_session_* call below must then be
  * made by all three processes in the same order; info and probe report this
  * process's party, check reports party 0's verdict in party 0's process (the
  * others return 0 when their part succeeded). */

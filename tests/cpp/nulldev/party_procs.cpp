@@ -18,7 +18,8 @@ extern "C" unsigned long nulldev_blocking_calls();
 
 // ownDevice: party p on device p (the north-star layout, three GPUs): the
 // receiver's copy out of the sender's staging slot is then a peer copy
-static int party_main(int party, const std::string& tag, bool ownDevice) {
+// forceRemote: one device, every cross-GPU branch taken (colocated = 2)
+static int party_main(int party, const std::string& tag, bool ownDevice, bool forceRemote = false) {
     struct J {
         int job;
         std::vector<uint64_t> p;
@@ -33,7 +34,7 @@ static int party_main(int party, const std::string& tag, bool ownDevice) {
     for (auto& j : jobs) {
         const std::string link = tag + "." + std::to_string(k++);
         aby3h_session* s = aby3h_party_create(j.job, j.p.data(), (int)j.p.size(), party, ownDevice ? party : 0,
-                                              link.c_str(), ownDevice ? 0 : 1, 0);
+                                              link.c_str(), ownDevice ? 0 : (forceRemote ? 2 : 1), 0);
         if (!s) {
             std::printf("FAIL party %d create job %d: %s\n", party, j.job, aby3h_last_error());
             return 1;
@@ -77,18 +78,19 @@ int main(int argc, char** argv) {
     // named arena ND_ARENA)
     if (argc == 3) return party_main(atoi(argv[1]), argv[2], false);
     int bad = 0;
-    for (int own = 0; own < 2 && !bad; ++own) {  // one device, then a device per party
+    // one device, a device per party, one device with the cross-GPU branches
+    for (int own = 0; own < 3 && !bad; ++own) {
         const std::string tag = "t" + std::to_string(getpid()) + "d" + std::to_string(own);
         pid_t kids[3];
         for (int p = 0; p < 3; ++p) {
             kids[p] = fork();
-            if (kids[p] == 0) _exit(party_main(p, tag, own != 0));
+            if (kids[p] == 0) _exit(party_main(p, tag, own == 1, own == 2));
         }
         for (int p = 0; p < 3; ++p) {
             int st = 0;
             waitpid(kids[p], &st, 0);
             if (!WIFEXITED(st) || WEXITSTATUS(st) != 0) {
-                std::printf("party %d exited with status %d (%s)\n", p, st, own ? "own devices" : "one device");
+                std::printf("party %d exited with status %d (%s)\n", p, st, own == 1 ? "own devices" : own == 2 ? "one device, remote branches" : "one device");
                 bad = 1;
             }
         }

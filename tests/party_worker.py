@@ -14,7 +14,10 @@ def main():
     job, party, steps = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
     link, device = sys.argv[4], int(sys.argv[5])
     params = [int(x) for x in sys.argv[6].split(",")] if len(sys.argv) > 6 and sys.argv[6] else []
-    s = native.Session.party(job, params, party, link, device=device, colocated=True)
+    # layout (aby3h_party_create's colocated): 1 the three on one GPU with
+    # in-kernel hand-offs, 2 on one GPU taking the cross-GPU branches
+    layout = int(sys.argv[7]) if len(sys.argv) > 7 else 1
+    s = native.Session.party(job, params, party, link, device=device, colocated=layout)
     # a lagging party (tests): its host sleeps between steps, so the others run ahead
     lag = float(os.environ.get("ABY3_TEST_LAG_MS", "0")) / 1e3
     try:
@@ -38,7 +41,7 @@ def main():
         s.close()
     print(json.dumps({"party": party, "ok": ok, "ms_per_step": 1e3 * dt / steps,
                       "recv_wait_us": info["host_recv_wait_us"], "digest": digest,
-                      "lr_fused": info["lr_fused"]}), flush=True)
+                      "lr_fused": info["lr_fused"], "lr_sys_scope": info["lr_sys_scope"]}), flush=True)
 
 
 if __name__ == "__main__":

@@ -18,10 +18,10 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def run_parties(job, params, steps, tag, timeout=150, lag_ms=0):
+def run_parties(job, params, steps, tag, timeout=150, lag_ms=0, layout=1):
     link = f"gt{os.getpid()}.{tag}"
     env = dict(os.environ, ABY3_LINK_TIMEOUT_S="100")
-    args = [str(job), None, str(steps), link, "0", ",".join(str(p) for p in params)]
+    args = [str(job), None, str(steps), link, "0", ",".join(str(p) for p in params), str(layout)]
     procs = []
     for party in range(3):
         a = list(args)
@@ -72,6 +72,30 @@ def test_three_party_processes(gpu, job, params, steps):
         # the fused iteration runs across the processes (IPC-mapped mailboxes)
         assert all(o["lr_fused"] == 1 for o in outs), outs
     ref = colocated_digests(job, params, steps + 1)  # the worker's warm-up step + steps
+    got = [o["digest"] for o in sorted(outs, key=lambda o: o["party"])]
+    assert got == ref
+
+
+@pytest.mark.parametrize("job,params,steps", [
+    (nt.JOB_LR, [20000, 128, 256, 16, 11], 5),          # C4: the fused iteration's system-scope mailboxes
+    (nt.JOB_LR, [20000, 128, 256, 16, 11, 1], 40),      # C4 with getSubset in every step
+    (nt.JOB_MUL_TRUNC, [1024, 1024, 1024, 16, 1], 3),   # C2: every z message as a staged IPC copy
+    (nt.JOB_MSB, [1 << 16], 2),                         # C3: every level's AND shares staged
+    (nt.JOB_SORT, [4096], 1),                           # C5
+])
+def test_three_party_processes_remote_branches(gpu, job, params, steps):
+    """The north-star layout's cross-GPU branches, run on the one GPU
+    (aby3h_party_create colocated = 2): no IPC arenas, every device message a
+    staged copy read out of the sender's exported slot, and the fused LR
+    iteration with uncached mailboxes and system-scope stores and loads
+    (aby3ML.cpp FusedLr::make, lr.hip sys_scope). Share-exact against the
+    same job in one process."""
+    outs = run_parties(job, params, steps, f"remote{job}_{params[0]}_{len(params)}", layout=2)
+    assert sorted(o["party"] for o in outs) == [0, 1, 2]
+    assert all(o["ok"] for o in outs), outs
+    if job == nt.JOB_LR:
+        assert all(o["lr_fused"] == 1 and o["lr_sys_scope"] == 1 for o in outs), outs
+    ref = colocated_digests(job, params, steps + 1)
     got = [o["digest"] for o in sorted(outs, key=lambda o: o["party"])]
     assert got == ref
 

@@ -162,6 +162,8 @@ def test_merge_vs_oracle(gpu, mode, dim, lens):
     (nt.JOB_LR, [1000000, 128, 256, 16, 11, 1], 40),    # C4 with getSubset inside every step
     (nt.JOB_SORT, [1 << 20], 1),                        # C5 the whole 2^20-key sort, every key checked
     (nt.JOB_SORT, [777], 2),                            # sort of a ragged count
+    (nt.JOB_SORT, [777, 1], 1),                         # the reference's sequential merge order
+    (nt.JOB_SORT, [1 << 12, 1], 1),
     (nt.JOB_A2B, [1 << 20], 2),                         # toBinaryMatrix, every value checked
     (nt.JOB_A2B, [1000], 3),                            # ragged rows
     (nt.JOB_BITINJ, [1 << 16, 64], 2),                  # bitInjection, every bit checked

@@ -413,10 +413,8 @@ void setTwoInputSharing(Sh3BinaryEvaluator& eng, int pIdx, const std::vector<std
         // v is P0's buffer, read in place by the first level's launch (fused
         // inputs, enqueued later in roundCallback) or by the transpose now:
         // held until that launch is enqueued, then fenced behind it
-        static const bool early = getenv("ABY3_TMP_FENCE_EARLY") && getenv("ABY3_TMP_FENCE_EARLY")[0] == '1';
-        if (!early) eng.holdForInputs(v);
+        eng.holdForInputs(v);
         eng.setInputs(w);
-        if (early) v->fence(g.stream());  // TMP A/B: the round-4 placement
     } else {
         // in0 = (0, 0), in1 = (0, x1)
         for (size_t k = 0; k < in0.size(); ++k) {

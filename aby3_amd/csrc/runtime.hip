@@ -99,20 +99,25 @@ constexpr Tables make_tables() {
 constexpr Tables kTables = make_tables();
 static_assert(kTables.sbox[0] == 0x63 && kTables.sbox[1] == 0x7c && kTables.sbox[0x53] == 0xed, "FIPS-197 S-box");
 const Tables& tables() { return kTables; }
-struct T0Table {
-    u32 v[256];
-};
-constexpr T0Table make_t0() {
-    T0Table t{};
-    for (int i = 0; i < 256; ++i) t.v[i] = kTables.T0[i];
-    return t;
-}
-__device__ const T0Table g_aes_t0 = make_t0();
 
 std::mutex g_tab_mu;
 std::map<int, u32*> g_tab_dev;
 std::map<int, u32*> g_status_dev;  // per device: in-kernel hand-off timeouts (under g_tab_mu)
 }  // namespace
+
+// The AES T-table as a device global, initialised by the code object's loader
+// from the compile-time table (externally linked and writable: the runtime
+// registers such a variable; a const one in an anonymous namespace was folded
+// into read-only data and could not be found by hipGetSymbolAddress).
+struct AesT0Table {
+    u32 v[256];
+};
+constexpr AesT0Table make_aes_t0() {
+    AesT0Table t{};
+    for (int i = 0; i < 256; ++i) t.v[i] = kTables.T0[i];
+    return t;
+}
+__device__ AesT0Table aby3g_aes_t0_dev = make_aes_t0();
 
 // Pinned host memory, so neither the kernels' timeout path nor the host's
 // reads need a stream: HIP's null stream is never touched (it would take one
@@ -181,7 +186,7 @@ const u32* aes_table() {
     auto it = g_tab_dev.find(dev);
     if (it != g_tab_dev.end()) return it->second;
     void* p = nullptr;
-    ABY3G_CHECK_HIP(hipGetSymbolAddress(&p, HIP_SYMBOL(g_aes_t0)));
+    ABY3G_CHECK_HIP(hipGetSymbolAddress(&p, HIP_SYMBOL(aby3g_aes_t0_dev)));
     g_tab_dev[dev] = (u32*)p;
     return (u32*)p;
 }

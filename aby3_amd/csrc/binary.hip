@@ -133,47 +133,6 @@ __device__ __forceinline__ void gate_eval(const aby3g_gate& g, const GateOps& o,
     s1[g.out * words + w] = o1;
 }
 
-// Rows p, p + S, p + 2S, ... (S = stride, 64 by default) of a merge round's
-// compare-exchange list -> rows of the merge array (aby3g_rowmap), without a
-// division per row (a 32- or 64-bit division is ~20-40 VALU ops, 16 of them
-// per thread made the mapped transposes VALU-bound): one division at the
-// start, then each step adds S / per_rep reps and S % per_rep positions with
-// one carry.
-struct MapWalk {
-    u64 q, rep, k, qd, qm;
-};
-__device__ __forceinline__ MapWalk map_walk(const aby3g_rowmap& m, u64 p, u32 stride = 64) {
-    MapWalk w;
-    w.q = m.first + p;
-    if (m.idx) return w;
-    if (((w.q | m.per_rep) >> 32) == 0) {
-        const u32 qq = (u32)w.q, pr = (u32)m.per_rep, r32 = qq / pr;
-        w.rep = r32;
-        w.k = qq - r32 * pr;
-        w.qd = stride / pr;
-        w.qm = stride - (u32)w.qd * pr;
-    } else {
-        w.rep = w.q / m.per_rep;
-        w.k = w.q - w.rep * m.per_rep;
-        w.qd = stride / m.per_rep;
-        w.qm = stride - w.qd * m.per_rep;
-    }
-    return w;
-}
-__device__ __forceinline__ u64 map_walk_row(const aby3g_rowmap& m, const MapWalk& w) {
-    return m.idx ? m.idx[w.q] : m.start + w.rep * m.rep_stride + w.k * m.step;
-}
-__device__ __forceinline__ void map_walk_next(const aby3g_rowmap& m, MapWalk& w, u32 stride = 64) {
-    w.q += stride;
-    if (m.idx) return;
-    w.k += w.qm;
-    w.rep += w.qd;
-    if (w.k >= m.per_rep) {
-        w.k -= m.per_rep;
-        ++w.rep;
-    }
-}
-
 // SLOTS gate slots x 32 word lanes. Each slot takes kLevelUnroll gates of a
 // batch per iteration, all their loads issued before any evaluation (the
 // gates of a batch are independent), so a batch of G gates costs about
@@ -188,21 +147,7 @@ constexpr u32 kLevelUnroll = 4;
 // publishes its own send rows for the next party's same workgroup (hp) --
 // the levels of the three parties pipeline chunk by chunk.
 static_assert(kLevelWords * 64 == ABY3G_HANDOFF_ROWS, "a level workgroup is one hand-off chunk");
-// OUT: the circuit's outputs read out by the last launch into mapped rows
-// (aby3g_bin_level_out; the scatters of a merge round): after the gates, per
-// (output, share) the workgroup's 64 x 32 wire words -- written by its own
-// gates a moment ago, so from L2 -- are staged in an LDS tile, a wave per
-// word bit-transposes them (lane b: wire b -> lane r: row 64 w + r), and
-// each row goes to its mapped destination.
-struct MapOut {
-    const u32* wires[2];
-    aby3g_rowmap map[2];
-    u32 nbits;
-    i64* out;
-    u64 outRows, rows;
-};
-constexpr u32 kOutPitch = kLevelWords + 1;  // u64 per tile row (+1: bank spread)
-template <u32 SLOTS, bool HS, bool OUT>
+template <u32 SLOTS, bool HS>
 __global__ void __launch_bounds__(SLOTS * 32) k_bin_level(const aby3g_gate* __restrict__ gates,
                                                          const uint2* __restrict__ rrows,
                                                          const u32* __restrict__ batch_ends, u32 nbatches,
@@ -210,7 +155,7 @@ __global__ void __launch_bounds__(SLOTS * 32) k_bin_level(const aby3g_gate* __re
                                                          const u32* __restrict__ unpack_wires, u32 nunpack,
                                                          u64* __restrict__ mem, u64 wires, u64 words,
                                                          const u64* __restrict__ z, u64* __restrict__ sendbuf,
-                                                         HsWait hw, HsPost hp, MapOut om) {
+                                                         HsWait hw, HsPost hp) {
     // HS: the in-kernel hand-off instantiation (sc1 payload accesses, waits
     // and posts); the other is the plain streaming kernel
     if (HS && !hs_wait(hw, blockIdx.x, blockIdx.x + 1)) return;
@@ -245,37 +190,6 @@ __global__ void __launch_bounds__(SLOTS * 32) k_bin_level(const aby3g_gate* __re
         begin = end;
     }
     if (HS) hs_post(hp, blockIdx.x, blockIdx.x + 1);
-    if constexpr (OUT) {
-        __shared__ u64 tile[64 * kOutPitch];
-        constexpr u32 kT = SLOTS * 32, kWaves = kT / 64;
-        const u32 tid = threadIdx.x, lane64 = tid & 63, wave = tid >> 6;
-        const u64 w0 = (u64)blockIdx.x * kLevelWords;
-#pragma unroll 1
-        for (u32 o = 0; o < 2; ++o) {
-            if (!om.wires[o]) continue;
-#pragma unroll 1
-            for (u32 sh = 0; sh < 2; ++sh) {
-                __syncthreads();  // the gates' words written (first pass) / the previous tile read
-                const u64* ms = sh ? s1 : s0;
-                for (u32 i = tid; i < 64 * kLevelWords; i += kT) {
-                    const u32 b = i / kLevelWords, wl = i % kLevelWords;
-                    tile[b * kOutPitch + wl] = b < om.nbits ? ms[(u64)om.wires[o][b] * words + w0 + wl] : 0;
-                }
-                __syncthreads();
-                i64* dst = om.out + (u64)sh * om.outRows;
-                MapWalk mw = map_walk(om.map[o], (w0 + wave) * 64 + lane64, kWaves * 64);
-                for (u32 wl = wave; wl < kLevelWords; wl += kWaves) {
-                    const u64 row = transpose64(tile[lane64 * kOutPitch + wl], lane64);
-                    const u64 p = (w0 + wl) * 64 + lane64;
-                    if (p < om.rows) {
-                        const u64 d = map_walk_row(om.map[o], mw);
-                        if (d < om.outRows) dst[d] = (i64)row;
-                    }
-                    map_walk_next(om.map[o], mw, kWaves * 64);
-                }
-            }
-        }
-    }
 }
 
 __global__ void __launch_bounds__(kGateBlock) k_bin_unpack(const u64* __restrict__ recv, const u32* __restrict__ outw,
@@ -544,15 +458,12 @@ __global__ void __launch_bounds__(256) k_lin_copy(WireSrcs ws, u32 nsrc, u64 row
 
 // The first level with its inputs (aby3g_bin_level_in). A source: one 64-bit
 // input (at most 64 wires from `wire` on) of one share, the sum of its terms
-// plus the constant on rows < rows; mapRows != 0: row r of the terms is row
-// map(r) (a merge round's gather), rows mapped at or past mapRows zero.
+// plus the constant on rows < rows.
 struct LevelInSrc {
     const u64* term[4];
     u64 coef[4];
     u64 constant;
     u32 wire, share, nbits, pad;
-    aby3g_rowmap map;
-    u64 mapRows;
 };
 struct LevelInSrcs {
     LevelInSrc s[ABY3G_WIRE_SRC_MAX];
@@ -627,28 +538,7 @@ __global__ void __launch_bounds__(SLOTS * 32) k_bin_level_in(LevelInSrcs srcs, u
     for (u32 k = 0; k < ABY3G_WIRE_SRC_MAX; ++k) {
         if (k >= nsrc) break;
         const LevelInSrc& src = srcs.s[k];
-        u64 v[kPer], at[kPer];
-        // the term row of each of the thread's rows (the source's own rows,
-        // or the gather map's; ~0: none)
-        if (src.mapRows) {
-            MapWalk mw = map_walk(src.map, (w0 + wave) * 64 + lane64, kWaves * 64);
-#pragma unroll
-            for (u32 i = 0; i < kPer; ++i) {
-                const u64 r = (w0 + wave + i * kWaves) * 64 + lane64;
-                at[i] = ~0ull;
-                if (r < rows) {  // an index map holds entries for rows < rows only
-                    const u64 m = map_walk_row(src.map, mw);
-                    if (m < src.mapRows) at[i] = m;
-                }
-                map_walk_next(src.map, mw, kWaves * 64);
-            }
-        } else {
-#pragma unroll
-            for (u32 i = 0; i < kPer; ++i) {
-                const u64 r = (w0 + wave + i * kWaves) * 64 + lane64;
-                at[i] = r < rows ? r : ~0ull;
-            }
-        }
+        u64 v[kPer];
 #pragma unroll
         for (u32 i = 0; i < kPer; ++i) v[i] = 0;
 #pragma unroll
@@ -657,8 +547,10 @@ __global__ void __launch_bounds__(SLOTS * 32) k_bin_level_in(LevelInSrcs srcs, u
             if (!p) continue;
             const u64 cf = src.coef[t];
 #pragma unroll
-            for (u32 i = 0; i < kPer; ++i)
-                if (at[i] != ~0ull) v[i] += cf * p[at[i]];
+            for (u32 i = 0; i < kPer; ++i) {
+                const u64 r = (w0 + wave + i * kWaves) * 64 + lane64;
+                if (r < rows) v[i] += cf * p[r];
+            }
         }
 #pragma unroll
         for (u32 i = 0; i < kPer; ++i) {
@@ -699,6 +591,46 @@ __global__ void __launch_bounds__(SLOTS * 32) k_bin_level_in(LevelInSrcs srcs, u
     if (HS) hs_post(hp, blockIdx.x, blockIdx.x + 1);
 }
 
+
+// Rows p, p + 64, p + 128, ... of a merge round's compare-exchange list ->
+// rows of the merge array (aby3g_rowmap), without a division per row (a 32-
+// or 64-bit division is ~20-40 VALU ops, 16 of them per thread made the
+// mapped transposes VALU-bound): one division at the start, then each step
+// adds 64 / per_rep reps and 64 % per_rep positions with one carry.
+struct MapWalk {
+    u64 q, rep, k, qd, qm;
+};
+__device__ __forceinline__ MapWalk map_walk(const aby3g_rowmap& m, u64 p) {
+    MapWalk w;
+    w.q = m.first + p;
+    if (m.idx) return w;
+    if (((w.q | m.per_rep) >> 32) == 0) {
+        const u32 qq = (u32)w.q, pr = (u32)m.per_rep, r32 = qq / pr;
+        w.rep = r32;
+        w.k = qq - r32 * pr;
+        w.qd = 64u / pr;
+        w.qm = 64u - (u32)w.qd * pr;
+    } else {
+        w.rep = w.q / m.per_rep;
+        w.k = w.q - w.rep * m.per_rep;
+        w.qd = 64 / m.per_rep;
+        w.qm = 64 - w.qd * m.per_rep;
+    }
+    return w;
+}
+__device__ __forceinline__ u64 map_walk_row(const aby3g_rowmap& m, const MapWalk& w) {
+    return m.idx ? m.idx[w.q] : m.start + w.rep * m.rep_stride + w.k * m.step;
+}
+__device__ __forceinline__ void map_walk_next(const aby3g_rowmap& m, MapWalk& w) {
+    w.q += 64;
+    if (m.idx) return;
+    w.k += w.qm;
+    w.rep += w.qd;
+    if (w.k >= m.per_rep) {
+        w.k -= m.per_rep;
+        ++w.rep;
+    }
+}
 
 // LDS-tiled bits -> wires over mapped source rows (the round's gather fused
 // into setInput). Rows mapped outside the source read as zero.
@@ -844,39 +776,17 @@ int aby3g_bin_level_rr(const aby3g_gate* gates, const uint32_t* recv_rows, const
                               z, sendbuf, nullptr, nullptr, stream);
 }
 
-// TMP A/B switches (removed once measured)
-static bool tmp_env(const char* n) {
-    const char* e = getenv(n);
-    return e && e[0] == '1';
-}
-
 static int bin_level(const aby3g_gate* gates, const uint32_t* recv_rows, const uint32_t* batch_ends,
                      uint32_t nbatches, const uint64_t* recvbuf, const uint32_t* unpack_wires, uint32_t nunpack,
                      uint64_t* mem, uint64_t wires, uint64_t words, const uint64_t* z, uint64_t* sendbuf,
-                     const aby3g_handoff* wait, const aby3g_handoff* post, const aby3g_map_out* out,
-                     aby3g_stream stream) {
+                     const aby3g_handoff* wait, const aby3g_handoff* post, aby3g_stream stream) {
     const uint2* rrows = reinterpret_cast<const uint2*>(recv_rows);
     return guarded([&] {
         ABY3G_REQUIRE(!rrows || recvbuf, "recv_rows without a recv buffer");
         ABY3G_REQUIRE(words % kLevelWords == 0, "words must be padded to a multiple of 32 (2048 rows)");
         ABY3G_REQUIRE(!(wait && wait->flags) || nunpack, "a hand-off wait without received shares");
         ABY3G_REQUIRE(!(post && post->flags) || sendbuf, "a hand-off post without a send buffer");
-        MapOut om{};
-        if (out) {
-            ABY3G_REQUIRE(out->nbits >= 1 && out->nbits <= 64, "mapped outputs: 1..64 wires");
-            ABY3G_REQUIRE(out->out != nullptr && out->rows <= words * 64, "mapped outputs: rows within the engine");
-            for (int o = 0; o < 2; ++o) {
-                om.wires[o] = out->wires[o];
-                om.map[o] = out->map[o];
-                if (out->wires[o]) check_map(&out->map[o], out->rows, out->out_rows);
-            }
-            ABY3G_REQUIRE(om.wires[0] || om.wires[1], "mapped outputs: no output");
-            om.nbits = out->nbits;
-            om.out = out->out;
-            om.outRows = out->out_rows;
-            om.rows = out->rows;
-        }
-        if ((!nbatches && !nunpack && !out) || !words) return;
+        if ((!nbatches && !nunpack) || !words) return;
         // one workgroup per chunk; in-kernel hand-offs are used only for
         // launches of at most 64 chunks, or 512 from a light producer
         // (Channel::handoffPost), so the spinning workgroups of two parties'
@@ -889,21 +799,21 @@ static int bin_level(const aby3g_gate* gates, const uint32_t* recv_rows, const u
         // with hand-offs the send rows are stored write-through and the
         // received ones read past L1 (both ways, so one instantiation covers
         // a launch that only waits or only posts)
-#define ABY3G_LEVEL_LAUNCH(SL, H, O)                                                                             \
-    launch(PROBE_BINARY, k_bin_level<SL, H, O>, dim3(wgs), dim3(SL * 32), 0, S(stream), gates, rrows, batch_ends, \
-           nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp, om)
-        // the mapped read-out moves 64 KiB of wire words and 32 KiB of rows
-        // per chunk: 16-wave workgroups (the 32-slot form) to hide its
-        // latency, whatever the grid size
-        if (out && (wgs < kLevelSmallMaxWgs || !tmp_env("ABY3G_TMP_OUT8")))
-            hs ? ABY3G_LEVEL_LAUNCH(32, true, true) : ABY3G_LEVEL_LAUNCH(32, false, true);
-        else if (out)
-            hs ? ABY3G_LEVEL_LAUNCH(8, true, true) : ABY3G_LEVEL_LAUNCH(8, false, true);
-        else if (wgs < kLevelSmallMaxWgs)
-            hs ? ABY3G_LEVEL_LAUNCH(32, true, false) : ABY3G_LEVEL_LAUNCH(32, false, false);
-        else
-            hs ? ABY3G_LEVEL_LAUNCH(8, true, false) : ABY3G_LEVEL_LAUNCH(8, false, false);
-#undef ABY3G_LEVEL_LAUNCH
+        if (wgs < kLevelSmallMaxWgs) {
+            if (hs)
+                launch(PROBE_BINARY, k_bin_level<32, true>, dim3(wgs), dim3(32 * 32), 0, S(stream), gates, rrows,
+                       batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp);
+            else
+                launch(PROBE_BINARY, k_bin_level<32, false>, dim3(wgs), dim3(32 * 32), 0, S(stream), gates, rrows,
+                       batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp);
+        } else {
+            if (hs)
+                launch(PROBE_BINARY, k_bin_level<8, true>, dim3(wgs), dim3(8 * 32), 0, S(stream), gates, rrows,
+                       batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp);
+            else
+                launch(PROBE_BINARY, k_bin_level<8, false>, dim3(wgs), dim3(8 * 32), 0, S(stream), gates, rrows,
+                       batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp);
+        }
     });
 }
 
@@ -912,29 +822,7 @@ int aby3g_bin_level_hs(const aby3g_gate* gates, const uint32_t* recv_rows, const
                        uint64_t* mem, uint64_t wires, uint64_t words, const uint64_t* z, uint64_t* sendbuf,
                        const aby3g_handoff* wait, const aby3g_handoff* post, aby3g_stream stream) {
     return bin_level(gates, recv_rows, batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z,
-                     sendbuf, wait, post, nullptr, stream);
-}
-
-int aby3g_bin_level_out(const aby3g_gate* gates, const uint32_t* recv_rows, const uint32_t* batch_ends,
-                        uint32_t nbatches, const uint64_t* recvbuf, const uint32_t* unpack_wires, uint32_t nunpack,
-                        uint64_t* mem, uint64_t wires, uint64_t words, const uint64_t* z, uint64_t* sendbuf,
-                        const aby3g_handoff* wait, const aby3g_handoff* post, const aby3g_map_out* out,
-                        aby3g_stream stream) {
-    if (!out) return guarded([] { ABY3G_REQUIRE(false, "null output description"); });
-    return bin_level(gates, recv_rows, batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z,
-                     sendbuf, wait, post, out, stream);
-}
-
-int aby3g_bin_level_out_residency(int* per_cu) {
-    return guarded([&] {
-        ABY3G_REQUIRE(per_cu != nullptr, "null argument");
-        if (tmp_env("ABY3G_TMP_OUT8"))
-            ABY3G_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                per_cu, reinterpret_cast<const void*>(k_bin_level<8, true, true>), 8 * 32, 0));
-        else
-            ABY3G_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                per_cu, reinterpret_cast<const void*>(k_bin_level<32, true, true>), 32 * 32, 0));
-    });
+                     sendbuf, wait, post, stream);
 }
 
 int aby3g_bin_level_residency(int* cus, int* per_cu_small, int* per_cu_large, int* small_max_wgs) {
@@ -943,14 +831,14 @@ int aby3g_bin_level_residency(int* cus, int* per_cu_small, int* per_cu_large, in
         const int dev = current_device();
         ABY3G_CHECK_HIP(hipDeviceGetAttribute(cus, hipDeviceAttributeMultiprocessorCount, dev));
         // the consumers that spin: the hand-off instantiations of the level
-        // kernel, one chunk per workgroup (the mapped read-out form has a
-        // figure of its own, aby3g_bin_level_out_residency)
+        // kernel, one chunk per workgroup (the only in-kernel waiters of the
+        // binary engine)
         int a = 0;
         ABY3G_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &a, reinterpret_cast<const void*>(k_bin_level<32, true, false>), 32 * 32, 0));
+            &a, reinterpret_cast<const void*>(k_bin_level<32, true>), 32 * 32, 0));
         *per_cu_small = a;
         ABY3G_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &a, reinterpret_cast<const void*>(k_bin_level<8, true, false>), 8 * 32, 0));
+            &a, reinterpret_cast<const void*>(k_bin_level<8, true>), 8 * 32, 0));
         *per_cu_large = a;
         *small_max_wgs = (int)kLevelSmallMaxWgs;
     });
@@ -1014,7 +902,6 @@ int aby3g_bits_to_wires_lin(const aby3g_wire_src* srcs, uint32_t nsrc, uint64_t 
         for (u32 k = 0; k < nsrc; ++k) {
             ABY3G_REQUIRE(srcs[k].wire_rows != nullptr, "null wire rows");
             ABY3G_REQUIRE(srcs[k].nbits <= srcs[k].cols64 * 64, "nbits exceeds input columns");
-            ABY3G_REQUIRE(srcs[k].map_rows == 0, "mapped sources only in aby3g_bin_level_in");
             ws.s[k] = srcs[k];
             cols = std::max<u64>(cols, (srcs[k].nbits + 63) / 64);
         }
@@ -1030,7 +917,6 @@ int aby3g_lin_copy_out(const aby3g_wire_src* srcs, uint32_t nsrc, uint64_t rows,
         WireSrcs ws{};
         u64 n = 0;
         for (u32 k = 0; k < nsrc; ++k) {
-            ABY3G_REQUIRE(srcs[k].map_rows == 0, "mapped sources only in aby3g_bin_level_in");
             ws.s[k] = srcs[k];
             if (srcs[k].copy_out) n = std::max<u64>(n, rows * srcs[k].cols64);
         }
@@ -1072,9 +958,6 @@ int aby3g_bin_level_in(const aby3g_wire_src* srcs, uint32_t nsrc, uint64_t rows,
                 d.coef[t] = (u64)s.coef[t];
             }
             d.constant = (u64)s.constant;
-            d.map = s.row_map;
-            d.mapRows = s.map_rows;
-            if (s.map_rows) check_map(&s.row_map, rows, s.map_rows);
             d.share = (u32)(off / shareStride);
             d.wire = (u32)((off % shareStride) / words);
             d.nbits = s.nbits;
@@ -1093,11 +976,7 @@ int aby3g_bin_level_in(const aby3g_wire_src* srcs, uint32_t nsrc, uint64_t rows,
         }();
         ABY3G_REQUIRE(attr || lds <= (64 << 10), "could not raise the fused level's dynamic LDS limit");
         nsrc = nl;
-        // mapped sources (a merge round's gathers): 16-wave workgroups to
-        // hide the gathers' latency, whatever the grid size
-        bool mapped = false;
-        for (u32 k = 0; k < nl; ++k) mapped = mapped || ls.s[k].mapRows;
-        if (wgs < kLevelSmallMaxWgs || (mapped && !tmp_env("ABY3G_TMP_IN8"))) {
+        if (wgs < kLevelSmallMaxWgs) {
             if (hp.flags)
                 launch(PROBE_BINARY, k_bin_level_in<32, true>, dim3(wgs), dim3(32 * 32), lds, S(stream), ls, nsrc,
                        (u64)rows, in_lo, nin, write_inputs, gates, batch_ends, nbatches, mem, wires, words, z, sendbuf,

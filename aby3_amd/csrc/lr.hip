@@ -35,16 +35,6 @@ namespace {
 
 constexpr u32 kLrThreads = 512;
 constexpr u32 kLrWaves = kLrThreads / 64;
-// a level runs in one wave when its unpack and every batch have at most this
-// many gate-words (one per lane: with two per lane the serial second round
-// cost more than the barriers saved, 0.0493 vs 0.0462 ms)
-constexpr u32 kSoloItems = 64;
-// orders one wave's memory accesses (LDS or global) before its next ones, for
-// every lane of the wave: the lockstep levels' stand-in for a barrier
-__device__ __forceinline__ void wave_order() {
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
 constexpr u32 kLrMaxB = 2048;
 constexpr u32 kLrMaxD = 4096;
 // the circuit's engine memory and AND masks live in LDS (beside the 64 KiB
@@ -762,26 +752,7 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
     // batches, then publish its AND shares
     const u64* zm = zmw;
     const u32 W32 = (u32)W;
-    // The small levels at the end of the circuit (the comparators' last
-    // carry steps: every batch and the unpack at most kSoloItems gate-words)
-    // run in wave 0 alone, in lockstep, with wave-scope ordering between
-    // batches instead of workgroup barriers: three barriers of eight waves
-    // per level, for a few dozen gate-words, cost more than the work. The
-    // other waves go on to the barrier after the levels.
-    u32 firstSolo = cir.nlevels;
-    for (u32 lv = cir.nlevels; lv-- > 0;) {
-        const aby3g_lr_level& l = levelsL[lv];
-        u32 items = lv > 0 ? levelsL[lv - 1].nand * W32 : ~0u;  // level 0's inputs come from phase 2
-        u32 b0 = 0;
-        for (u32 b = 0; b < l.nbatch; ++b) {
-            const u32 e = batchEndsL[l.batch_off + b];
-            items = max(items, (e - b0) * W32);
-            b0 = e;
-        }
-        if (items > kSoloItems) break;
-        firstSolo = lv;
-    }
-    for (u32 lv = 0; lv < firstSolo; ++lv) {
+    for (u32 lv = 0; lv <= cir.nlevels; ++lv) {
         if (lv > 0 && levelsL[lv - 1].nand) {
             const aby3g_lr_level& pl = levelsL[lv - 1];
             const u64* grows = pv + L.lvl + 2 * (u64)pl.and_wire_off * W;
@@ -821,59 +792,6 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
             begin = end;
         }
         if (lv < 16) lr_stamp(PT, 16 + lv);
-    }
-    if (firstSolo < cir.nlevels) {
-        if (wave == 0) {
-            bool ok = true;
-            for (u32 lv = firstSolo; lv <= cir.nlevels && ok; ++lv) {
-                if (levelsL[lv - 1].nand) {
-                    const aby3g_lr_level& pl = levelsL[lv - 1];
-                    const u64* grows = pv + L.lvl + 2 * (u64)pl.and_wire_off * W;
-                    MsgWait mw = msg_begin(tag, status);
-                    for (u32 q = lane; q < pl.nand * W32 && mw.ok; q += 64) {
-                        const u64 v = msg_get(grows, q, mw);
-                        const u32 j = q / W32, w = q - j * W32;
-                        if (mw.ok) mem[WS + (u64)andWires[pl.and_wire_off + j] * W + w] = v;
-                    }
-                    if (lane == 0 && ticks)
-                        __hip_atomic_fetch_add((gu64*)ticks, wall_clock64() - mw.t0, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                    ok = __all(mw.ok);
-                    wave_order();
-                }
-                if (lv == cir.nlevels || !ok) break;
-                const aby3g_lr_level& lvr = levelsL[lv];
-                u64* gsend = my + L.lvl + 2 * (u64)lvr.and_wire_off * W;
-                u32 begin = 0;
-                for (u32 b = 0; b < lvr.nbatch; ++b) {
-                    const u32 end = batchEndsL[lvr.batch_off + b];
-                    for (u32 q = lane; q < (end - begin) * W32; q += 64) {
-                        const u32 gq = q / W32, w = q - gq * W32;
-                        const aby3g_gate g = gates[lvr.first_gate + begin + gq];
-                        const bool unary = g.type == ABY3G_GATE_COPY || g.type == ABY3G_GATE_INV;
-                        const u32 in1 = unary ? g.in0 : g.in1;
-                        const u64 x0 = mem[(u64)g.in0 * W + w], x1 = mem[WS + (u64)g.in0 * W + w];
-                        const u64 y0 = mem[(u64)in1 * W + w], y1 = mem[WS + (u64)in1 * W + w];
-                        if (gate_is_and(g.type)) {
-                            const u64 r = gate_and_share(g.type, x0, x1, y0, y1) ^ zm[(u64)g.z_row * W + w];
-                            mem[(u64)g.out * W + w] = r;
-                            msg_put(gsend, (u64)g.send_row * W + w, r, tag);
-                        } else {
-                            u64 o0, o1;
-                            gate_local(g.type, x0, x1, y0, y1, o0, o1);
-                            mem[(u64)g.out * W + w] = o0;
-                            mem[WS + (u64)g.out * W + w] = o1;
-                        }
-                    }
-                    wave_order();
-                    begin = end;
-                }
-                if (lv < 16) lr_stamp(PT, 16 + lv);
-            }
-            if (!ok && lane == 0) msgBad = 1;
-        }
-        __syncthreads();
-        if (msgBad) return;
     }
     lr_stamp(PT, 6);
     // regions (getOutput, 1 bit each): reg[t][h][i]

@@ -638,7 +638,7 @@ bool Channel::handoffWouldPost(const Gpu& gpu, u64 rows, u64 producerBytes) cons
     return !(chunks > kHandoffChunks || (chunks > kHandoffMaxChunks && producerBytes > kHandoffLightBytes));
 }
 
-aby3g_handoff Channel::handoffPost(Gpu& gpu, u64 rows, u64 producerBytes, const void* payload, bool outConsumer) {
+aby3g_handoff Channel::handoffPost(Gpu& gpu, u64 rows, u64 producerBytes, const void* payload) {
     if (!mOut) throw std::runtime_error("channel not connected");
     Pipe& p = *mOut;
     if (p.link) {
@@ -648,7 +648,7 @@ aby3g_handoff Channel::handoffPost(Gpu& gpu, u64 rows, u64 producerBytes, const 
             return aby3g_handoff{nullptr, 0, nullptr};
         const u64 chunks = std::max<u64>(1, (rows + ABY3G_HANDOFF_ROWS - 1) / ABY3G_HANDOFF_ROWS);
         // three processes on the device: each brings its own queues' stream-op waits
-        if (!handoffResidencyOk(handoffResidency(gpu.device()), chunks, 3, outConsumer) || chunks > kHandoffChunks ||
+        if (!handoffResidencyOk(handoffResidency(gpu.device()), chunks, 3) || chunks > kHandoffChunks ||
             (chunks > kHandoffMaxChunks && producerBytes > kHandoffLightBytes))
             return aby3g_handoff{nullptr, 0, nullptr};
         return aby3g_handoff{p.arenaFlags(), ++p.hsSeq, nullptr};
@@ -672,8 +672,7 @@ aby3g_handoff Channel::handoffPost(Gpu& gpu, u64 rows, u64 producerBytes, const 
     const u64 chunks = std::max<u64>(1, (rows + ABY3G_HANDOFF_ROWS - 1) / ABY3G_HANDOFF_ROWS);
     // the residency rule first: a consumer launch that could starve its
     // producer of slots keeps the stream hand-off
-    if (!handoffResidencyOk(handoffResidency(gpu.device()), chunks, 1, outConsumer))
-        return aby3g_handoff{nullptr, 0, nullptr};
+    if (!handoffResidencyOk(handoffResidency(gpu.device()), chunks)) return aby3g_handoff{nullptr, 0, nullptr};
     // Large messages from a heavy producer keep the stream hand-off: a
     // consumer launch of many workgroups would hold its CUs spinning while the
     // producer still runs (measured slower on C3 / C5 at 512 chunks with every
@@ -690,8 +689,8 @@ bool Channel::handoffCapable(const Gpu& gpu) const {
     return true;
 }
 
-bool handoffResidencyOk(const HandoffResidency& r, u64 chunks, int processes, bool outConsumer) {
-    const int per = outConsumer ? r.perCuOut : chunks < (u64)std::max(0, r.smallMaxWgs) ? r.perCuSmall : r.perCuLarge;
+bool handoffResidencyOk(const HandoffResidency& r, u64 chunks, int processes) {
+    const int per = chunks < (u64)std::max(0, r.smallMaxWgs) ? r.perCuSmall : r.perCuLarge;
     if (per <= 0 || r.cus <= 0 || !chunks || processes < 1) return false;
     const u64 cusHeld = (chunks + (u64)per - 1) / (u64)per;
     return 2 * cusHeld + (u64)processes * (u64)std::max(0, r.otherSpinners) + 1 <= (u64)r.cus;
@@ -706,7 +705,6 @@ const HandoffResidency& handoffResidency(int device) {
     HandoffResidency r;
     GPU_CALL(aby3g_set_device(device));
     GPU_CALL(aby3g_bin_level_residency(&r.cus, &r.perCuSmall, &r.perCuLarge, &r.smallMaxWgs));
-    GPU_CALL(aby3g_bin_level_out_residency(&r.perCuOut));
     // stream-operation waits can spin on every stream of the device: at most
     // one per hardware queue of the process
     r.otherSpinners = hwQueuesPerDevice();

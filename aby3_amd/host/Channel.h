@@ -86,10 +86,7 @@ public:
     // in-kernel only from light producers)
     // payload: the message's buffer; between processes it must lie in this
     // direction's arena (evalSendBuffer) for an in-kernel hand-off
-    // outConsumer: the launch that waits for this message is the mapped
-    // read-out form (aby3g_bin_level_out), whose residency differs
-    aby3g_handoff handoffPost(Gpu& gpu, u64 rows, u64 producerBytes = 0, const void* payload = nullptr,
-                              bool outConsumer = false);
+    aby3g_handoff handoffPost(Gpu& gpu, u64 rows, u64 producerBytes = 0, const void* payload = nullptr);
     // One party per process on one GPU: a buffer for an evaluation's messages
     // inside this direction's IPC-mapped arena (two slots, alternating per
     // call), which the receiver reads in place -- null when the direction has
@@ -170,10 +167,8 @@ struct HandoffResidency {
     int perCuSmall = 0, perCuLarge = 0;  // level-kernel workgroups resident per CU
     int smallMaxWgs = 0;
     int otherSpinners = 0;
-    int perCuOut = 0;  // the mapped read-out form (a round's last launch): one size for every grid
 };
-// outConsumer: the message's consumer is the mapped read-out form
-bool handoffResidencyOk(const HandoffResidency& r, u64 chunks, int processes = 1, bool outConsumer = false);
+bool handoffResidencyOk(const HandoffResidency& r, u64 chunks, int processes = 1);
 // the current device's figures (aby3g_bin_level_residency, computed once per
 // device; otherSpinners = GPU_MAX_HW_QUEUES)
 const HandoffResidency& handoffResidency(int device);

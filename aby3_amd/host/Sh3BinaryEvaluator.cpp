@@ -123,8 +123,6 @@ void Sh3BinaryEvaluator::setCir(BetaCircuit* cir, u64 width, block prevSeed, blo
     mKeyNext = nextSeed;
     mPendingIn.clear();  // held inputs belong to the previous circuit
     mPendingHold.clear();
-    mPendingMapped = PendingMapped{};
-    mOutFuse = OutFuse{};
     Gpu& g = Gpu::current();
     mGpu = &g;
     upload(g);
@@ -229,15 +227,6 @@ void Sh3BinaryEvaluator::setInput(u64 i, const sbMatrix& in, const aby3g_rowmap&
     mLevel = 0;
 }
 
-// ABY3_FUSE_INPUTS=1 / 0 turns the fused first level on / off (A/B runs)
-static bool fuseInputsEnabled() {
-    static const bool on = [] {
-        const char* e = getenv("ABY3_FUSE_INPUTS");
-        return e ? e[0] == '1' : kFuseInputsDefault;
-    }();
-    return on;
-}
-
 void Sh3BinaryEvaluator::setInputs(u64 i, const aby3g_rowmap& mi, u64 j, const aby3g_rowmap& mj,
                                    const sbMatrix& in) {
     if (!mCir) throw RTE_LOC;
@@ -250,29 +239,6 @@ void Sh3BinaryEvaluator::setInputs(u64 i, const aby3g_rowmap& mi, u64 j, const a
             if ((*wires)[k] != (*wires)[k - 1] + 1) throw std::runtime_error("expecting contiguous input wires. " LOCATION);
     Gpu& g = *mGpu;
     const u64 W = mCir->mWireCount;
-    // The gathers fused into the first level's launch (aby3g_bin_level_in
-    // with mapped sources): both inputs, both shares, as four sources, when
-    // the circuit's first level takes its inputs that way
-    if (fuseInputsEnabled() && mCur->fuseInputs && mPendingIn.empty() && wi.size() <= 64 && wj.size() <= 64 &&
-        in.i64Cols() == 1 && !mCur->levelBatches.empty() && mCur->levelBatches[0] &&
-        4 <= ABY3G_WIRE_SRC_MAX) {
-        for (int which = 0; which < 2; ++which)
-            for (int sh = 0; sh < 2; ++sh) {
-                const auto& wires = which ? wj : wi;
-                aby3g_wire_src s{};
-                s.term[0] = in.share(sh);
-                s.coef[0] = 1;
-                s.cols64 = 1;
-                s.nbits = (u32)wires.size();
-                s.wire_rows = mMem.as<u64>() + ((u64)sh * W + wires[0]) * mWords;
-                s.row_map = which ? mj : mi;
-                s.map_rows = in.rows();
-                mPendingIn.push_back(s);
-            }
-        mPendingMapped = PendingMapped{true, i, j, mi, mj, in.data(), in.rows(), in.i64Cols(), (u32)wi.size()};
-        mLevel = 0;
-        return;
-    }
     const aby3g_rowmap maps[2] = {mi, mj};
     u64* dst[2] = {mMem.as<u64>() + wi[0] * mWords, mMem.as<u64>() + wj[0] * mWords};
     GPU_CALL(aby3g_bits_to_wires_map_n(in.data(), in.rows(), in.i64Cols(), (u32)wi.size(), maps, dst, 2, mRows,
@@ -280,20 +246,18 @@ void Sh3BinaryEvaluator::setInputs(u64 i, const aby3g_rowmap& mi, u64 j, const a
     mLevel = 0;
 }
 
+// ABY3_FUSE_INPUTS=1 / 0 turns the fused first level on / off (A/B runs)
+static bool fuseInputsEnabled() {
+    static const bool on = [] {
+        const char* e = getenv("ABY3_FUSE_INPUTS");
+        return e ? e[0] == '1' : kFuseInputsDefault;
+    }();
+    return on;
+}
+
 void Sh3BinaryEvaluator::flushPendingInputs(bool dropHolds) {
     if (mPendingIn.empty()) return;
-    if (mPendingMapped.on) {
-        // the held gathers the separate way (aby3g_bits_to_wires_map_n)
-        const PendingMapped& m = mPendingMapped;
-        const u64 W = mCir->mWireCount;
-        const aby3g_rowmap maps[2] = {m.mi, m.mj};
-        u64* dst[2] = {mMem.as<u64>() + mCir->mInputs[m.i][0] * mWords, mMem.as<u64>() + mCir->mInputs[m.j][0] * mWords};
-        GPU_CALL(aby3g_bits_to_wires_map_n(m.in, m.inRows, m.cols64, m.nbits, maps, dst, 2, mRows, W * mWords, mWords,
-                                           mGpu->stream()));
-        mPendingMapped = PendingMapped{};
-    } else {
-        GPU_CALL(aby3g_bits_to_wires_lin(mPendingIn.data(), (u32)mPendingIn.size(), mRows, mWords, mGpu->stream()));
-    }
+    GPU_CALL(aby3g_bits_to_wires_lin(mPendingIn.data(), (u32)mPendingIn.size(), mRows, mWords, mGpu->stream()));
     mPendingIn.clear();
     readHeld(dropHolds);
 }
@@ -529,10 +493,7 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
     }
     mAndDone += nAnd;
     // this level's bytes (about 72 per gate and 64-row word)
-    // the next launch (this message's consumer) may be the mapped read-out form
-    const bool outNext = mOutFuse.on && mLevel + 1 == mCur->lastLaunchLevel;
-    if (nAnd)
-        hp = comm.mNext.handoffPost(g, mRows, (u64)mCir->mLevelCounts[mLevel] * mWords * 72, send->data(), outNext);
+    if (nAnd) hp = comm.mNext.handoffPost(g, mRows, (u64)mCir->mLevelCounts[mLevel] * mWords * 72, send->data());
     if (nb && mZPending) waitZ();
     // the first level with its inputs (aby3g_bin_level_in) when the held
     // sources make up every input wire (an input set another way lives in
@@ -545,35 +506,14 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
                                     mCur->batchEnds + mCur->levelBatchOffset[0], nb, mMem.as<u64>(), W, mWords, mZPtr,
                                     send ? send->as<u64>() : nullptr, &hp, g.stream()));
         mPendingIn.clear();
-        mPendingMapped = PendingMapped{};
         readHeld(true);
     } else if (nb || nUnpack) {
         const aby3g_gate* gl = nb ? mCur->gates + mCur->levelFirstGate[mLevel] : nullptr;
         const u32* be = nb ? mCur->batchEnds + mCur->levelBatchOffset[mLevel] : nullptr;
         const u32* rr = (nb && recv) ? mCur->recvRows + 2 * (u64)mCur->levelFirstGate[mLevel] : nullptr;
-        if (mOutFuse.on && mLevel == mCur->lastLaunchLevel) {
-            // the last launch also writes the outputs into their mapped rows
-            aby3g_map_out mo{};
-            const u64 idx[2] = {mOutFuse.i, mOutFuse.j};
-            const aby3g_rowmap maps[2] = {mOutFuse.mi, mOutFuse.mj};
-            for (int o = 0; o < 2; ++o)
-                if (idx[o] != kNoOutput) {
-                    mo.wires[o] = mCur->allOutputWires + mCur->outputOffsets[idx[o]];
-                    mo.map[o] = maps[o];
-                }
-            mo.nbits = (u32)mOutFuse.out->bitCount();
-            mo.out = mOutFuse.out->data();
-            mo.out_rows = mOutFuse.out->rows();
-            mo.rows = mRows;
-            GPU_CALL(aby3g_bin_level_out(gl, rr, be, nb, recv ? recv->as<u64>() : nullptr,
-                                         nUnpack ? mCur->outWires[mLevel - 1] : nullptr, nUnpack, mMem.as<u64>(), W,
-                                         mWords, mZPtr, send ? send->as<u64>() : nullptr, &hw, &hp, &mo, g.stream()));
-            mOutFuse.done = true;
-        } else {
-            GPU_CALL(aby3g_bin_level_hs(gl, rr, be, nb, recv ? recv->as<u64>() : nullptr,
-                                        nUnpack ? mCur->outWires[mLevel - 1] : nullptr, nUnpack, mMem.as<u64>(), W,
-                                        mWords, mZPtr, send ? send->as<u64>() : nullptr, &hw, &hp, g.stream()));
-        }
+        GPU_CALL(aby3g_bin_level_hs(gl, rr, be, nb, recv ? recv->as<u64>() : nullptr,
+                                    nUnpack ? mCur->outWires[mLevel - 1] : nullptr, nUnpack, mMem.as<u64>(), W, mWords,
+                                    mZPtr, send ? send->as<u64>() : nullptr, &hw, &hp, g.stream()));
     }
 
     if (recv) {
@@ -630,34 +570,8 @@ void Sh3BinaryEvaluator::getOutput(u64 i, sbMatrix& out) {
                                   g.stream()));
 }
 
-static bool sameMap(const aby3g_rowmap& a, const aby3g_rowmap& b) {
-    return a.first == b.first && a.start == b.start && a.step == b.step && a.per_rep == b.per_rep &&
-           a.rep_stride == b.rep_stride && a.idx == b.idx;
-}
-
-bool Sh3BinaryEvaluator::outFuseCovers(u64 i, const aby3g_rowmap* mi, u64 j, const aby3g_rowmap* mj,
-                                       const sbMatrix& out) const {
-    const OutFuse& f = mOutFuse;
-    if (!f.done || f.out != &out || f.i != i || f.j != j) return false;
-    return (i == kNoOutput || sameMap(*mi, f.mi)) && (j == kNoOutput || sameMap(*mj, f.mj));
-}
-
-void Sh3BinaryEvaluator::fuseOutputs(u64 i, const aby3g_rowmap& mi, u64 j, const aby3g_rowmap& mj, sbMatrix& out) {
-    if (!mCir) throw RTE_LOC;
-    mOutFuse = OutFuse{};
-    if (i == kNoOutput && j == kNoOutput) return;
-    for (u64 k : {i, j})
-        if (k != kNoOutput && (k >= mCir->mOutputs.size() || mCir->mOutputs[k].size() != out.bitCount()))
-            throw std::invalid_argument("fuseOutputs: output index or width");
-    // the last launch must be a later level's (the fused first level has no
-    // read-out form), one 64-bit column
-    if (mCur->lastLaunchLevel == 0 || out.bitCount() == 0 || out.bitCount() > 64 || out.i64Cols() != 1) return;
-    mOutFuse = OutFuse{true, false, i, j, mi, mj, &out};
-}
-
 void Sh3BinaryEvaluator::getOutputs(u64 i, const aby3g_rowmap& mi, u64 j, const aby3g_rowmap& mj, sbMatrix& out) {
     if (i >= mCir->mOutputs.size() || j >= mCir->mOutputs.size()) throw RTE_LOC;
-    if (outFuseCovers(i, &mi, j, &mj, out)) return;  // written by the last launch
     if (out.bitCount() != mCir->mOutputs[i].size() || out.bitCount() != mCir->mOutputs[j].size())
         throw std::invalid_argument("output matrix wrong size");
     Gpu& g = *mGpu;
@@ -670,7 +584,6 @@ void Sh3BinaryEvaluator::getOutputs(u64 i, const aby3g_rowmap& mi, u64 j, const 
 
 void Sh3BinaryEvaluator::getOutput(u64 i, sbMatrix& out, const aby3g_rowmap& map) {
     if (i >= mCir->mOutputs.size()) throw RTE_LOC;
-    if (outFuseCovers(i, &map, kNoOutput, nullptr, out) || outFuseCovers(kNoOutput, nullptr, i, &map, out)) return;
     const auto& wires = mCir->mOutputs[i];
     if (out.bitCount() != wires.size()) throw std::invalid_argument("output matrix wrong size");
     Gpu& g = *mGpu;

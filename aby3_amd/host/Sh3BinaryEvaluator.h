@@ -69,15 +69,6 @@ public:
     void getOutput(u64 i, sbMatrix& out, const aby3g_rowmap& map);
     // getOutput(i, out, mi) and getOutput(j, out, mj) in one launch (the maps' rows disjoint)
     void getOutputs(u64 i, const aby3g_rowmap& mi, u64 j, const aby3g_rowmap& mj, sbMatrix& out);
-    // The same read-outs done by the evaluation's last launch itself
-    // (aby3g_bin_level_out: a merge round's scatters fused into its last
-    // level). Call before asyncEvaluate; i or j may be kNoOutput. The later
-    // getOutputs / getOutput(.., map) with the same arguments then have
-    // nothing left to do. Without the fused form (the last launch is the
-    // first level, or an output wider than 64 wires) it does nothing and the
-    // later calls read out as usual. `out` must stay alive until then.
-    static constexpr u64 kNoOutput = ~0ull;
-    void fuseOutputs(u64 i, const aby3g_rowmap& mi, u64 j, const aby3g_rowmap& mj, sbMatrix& out);
 
     bool hasMoreRounds() const { return mLevel <= mCir->mLevelCounts.size(); }
     void roundCallback(CommPkg& comm, Sh3Task task);
@@ -143,24 +134,6 @@ private:
     // buffers the held sources read (e.g. a received message): kept alive
     // until the launch that reads them is enqueued (holdForInputs)
     std::vector<std::shared_ptr<DeviceBuffer>> mPendingHold;
-    // setInputs(i, mi, j, mj, in) held as four mapped sources for the first
-    // level (its gathers fused into that launch); flushPendingInputs replays
-    // the separate gather transposes with these arguments
-    struct PendingMapped {
-        bool on = false;
-        u64 i = 0, j = 0;
-        aby3g_rowmap mi{}, mj{};
-        const i64* in = nullptr;
-        u64 inRows = 0, cols64 = 0;
-        u32 nbits = 0;
-    } mPendingMapped;
-    struct OutFuse {
-        bool on = false, done = false;
-        u64 i = 0, j = 0;
-        aby3g_rowmap mi{}, mj{};
-        sbMatrix* out = nullptr;
-    } mOutFuse;
-    bool outFuseCovers(u64 i, const aby3g_rowmap* mi, u64 j, const aby3g_rowmap* mj, const sbMatrix& out) const;
     void readHeld(bool drop);
     // writes them to mMem the separate way (dropHolds false: more held
     // sources that read the same buffers follow)

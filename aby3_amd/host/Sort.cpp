@@ -53,10 +53,7 @@ void compareExchange(Sh3BinaryEvaluator& eng, const sbMatrix& src, sbMatrix& dst
         aby3g_rowmap m[4] = {gx, gy, sx ? *sx : gx, sy ? *sy : gy};
         for (auto& x : m) x.first += c;
         eng.setCir(cir, n, eval.mShareGen);
-        eng.setInputs(0, m[0], 1, m[1], src);  // both gathers (fused into the first level's launch)
-        // both scatters by the last level's launch (aby3g_bin_level_out)
-        const u64 none = Sh3BinaryEvaluator::kNoOutput;
-        eng.fuseOutputs(sx ? 0 : none, m[2], sy ? 1 : none, m[3], dst);
+        eng.setInputs(0, m[0], 1, m[1], src);  // both gathers in one launch
         eng.asyncEvaluate(rt.noDependencies())
             .then([&](Sh3Task&) {
                 if (sx && sy)

@@ -66,18 +66,10 @@ class RowMap(ctypes.Structure):
 
 
 class WireSrc(ctypes.Structure):
-    """aby3g_wire_src: one source of aby3g_bits_to_wires_lin (map_rows != 0:
-    the rows gathered through row_map, aby3g_bin_level_in only)."""
+    """aby3g_wire_src: one source of aby3g_bits_to_wires_lin."""
     _fields_ = [("term", ctypes.POINTER(ctypes.c_int64) * 4), ("coef", ctypes.c_int64 * 4),
                 ("constant", ctypes.c_int64), ("cols64", c_uint64), ("nbits", c_uint32),
-                ("wire_rows", ctypes.POINTER(c_uint64)), ("copy_out", ctypes.POINTER(ctypes.c_int64)),
-                ("row_map", RowMap), ("map_rows", c_uint64)]
-
-
-class MapOut(ctypes.Structure):
-    """aby3g_map_out: the mapped read-out of aby3g_bin_level_out."""
-    _fields_ = [("wires", c_void_p * 2), ("map", RowMap * 2), ("nbits", c_uint32), ("out", c_void_p),
-                ("out_rows", c_uint64), ("rows", c_uint64)]
+                ("wire_rows", ctypes.POINTER(c_uint64)), ("copy_out", ctypes.POINTER(ctypes.c_int64))]
 
 
 def key16(b: bytes):
@@ -168,13 +160,9 @@ _SIGS = {
     # the aby3g_handoff / aby3g_lr_iter / aby3g_lr_circuit structs go by pointer
     "aby3g_bin_level_hs": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_uint32, c_void_p, c_void_p, ctypes.c_uint32,
                                    c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "aby3g_bin_level_out": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_uint32, c_void_p, c_void_p, ctypes.c_uint32,
-                                    c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                                    c_void_p]),
     "aby3g_handoff_status": (c_int, [POINTER(ctypes.c_uint32)]),
     "aby3g_set_handoff_timeout_us": (c_int, [c_uint64]),
     "aby3g_bin_level_residency": (c_int, [POINTER(c_int), POINTER(c_int), POINTER(c_int), POINTER(c_int)]),
-    "aby3g_bin_level_out_residency": (c_int, [POINTER(c_int)]),
     "aby3g_stream_count": (c_int, [c_int, POINTER(c_int)]),
     "aby3g_malloc_uncached": (c_int, [POINTER(c_void_p), c_size_t]),
     "aby3g_device_uuid": (c_int, [c_int, c_void_p]),

@@ -416,8 +416,6 @@ int aby3g_bin_level_hs(const aby3g_gate* gates, const uint32_t* recv_rows, const
  * (hipOccupancyMaxActiveBlocksPerMultiprocessor) -- the small-grid form
  * (launches of fewer than *small_max_wgs workgroups) and the large one. */
 int aby3g_bin_level_residency(int* cus, int* per_cu_small, int* per_cu_large, int* small_max_wgs);
-/* workgroups per CU of aby3g_bin_level_out's hand-off form (one launch size) */
-int aby3g_bin_level_out_residency(int* per_cu);
 int aby3g_bin_unpack(const uint64_t* recvbuf, const uint32_t* out_wires, uint32_t n, uint64_t* mem, uint64_t wires,
                      uint64_t words, aby3g_stream stream);
 /* setInput (:200-276): bit-transpose a [rows][cols64] i64 share matrix into
@@ -471,28 +469,6 @@ int aby3g_bits_to_wires_map_n(const int64_t* in, uint64_t in_rows, uint64_t cols
 int aby3g_wires_to_bits_map_n(const uint64_t* mem, uint64_t share_stride, const uint32_t* const* wires,
                               uint32_t nbits, uint64_t words, int64_t* out, uint64_t out_rows,
                               const aby3g_rowmap* maps, uint32_t n, uint64_t rows, aby3g_stream stream);
-/* aby3g_bin_level_hs, then getOutput of up to two outputs into mapped rows
- * fused into the same launch -- the last launch of a merge round's cmp_swap,
- * with its two scatters (Sort.cpp:366-392, BoolBasic.cpp:275-312): after the
- * level's gates, output o's wires (wires[o], a DEVICE array of nbits <= 64
- * wire ids; NULL: no such output) are read back per 2048-row chunk,
- * bit-transposed, and circuit row p of share s goes to row map[o](p) of
- * share s of out ([2][out_rows], one 64-bit column), as
- * aby3g_wires_to_bits_map_n would after this level. Rows p >= rows and
- * rows mapped at or past out_rows are not written. */
-typedef struct {
-    const uint32_t* wires[2];
-    aby3g_rowmap map[2];
-    uint32_t nbits;
-    int64_t* out;
-    uint64_t out_rows;
-    uint64_t rows;
-} aby3g_map_out;
-int aby3g_bin_level_out(const aby3g_gate* gates, const uint32_t* recv_rows, const uint32_t* batch_ends,
-                        uint32_t nbatches, const uint64_t* recvbuf, const uint32_t* unpack_wires, uint32_t nunpack,
-                        uint64_t* mem, uint64_t wires, uint64_t words, const uint64_t* z, uint64_t* sendbuf,
-                        const aby3g_handoff* wait, const aby3g_handoff* post, const aby3g_map_out* out,
-                        aby3g_stream stream);
 
 /* setInput of shares that are linear combinations of arithmetic shares,
  * several inputs / shares in one launch (the two-input binary resharing of
@@ -501,10 +477,7 @@ int aby3g_bin_level_out(const aby3g_gate* gates, const uint32_t* recv_rows, cons
  * v[r] = sum_t coef[t] * term[t][r * cols64 + c] + constant (mod 2^64);
  * all terms NULL writes zero wires. copy_out (optional) receives
  * sum_t coef[t] * term[t][...] (without the constant), e.g. P0's share to
- * send. At most ABY3G_WIRE_SRC_MAX sources per call. map_rows != 0 (only
- * in aby3g_bin_level_in): circuit row r reads row row_map(r) of the terms
- * instead of row r -- the gather of a merge round (Sort.cpp:366-392) --, rows
- * mapped at or past map_rows reading zero; the others take map_rows 0. */
+ * send. At most ABY3G_WIRE_SRC_MAX sources per call. */
 #define ABY3G_WIRE_SRC_MAX 8
 typedef struct {
     const int64_t* term[4];
@@ -514,8 +487,6 @@ typedef struct {
     uint32_t nbits;
     uint64_t* wire_rows;
     int64_t* copy_out;
-    aby3g_rowmap row_map;
-    uint64_t map_rows;
 } aby3g_wire_src;
 int aby3g_bits_to_wires_lin(const aby3g_wire_src* srcs, uint32_t nsrc, uint64_t rows, uint64_t words,
                             aby3g_stream stream);

@@ -21,7 +21,7 @@ it = 50
 class WireSrc(ctypes.Structure):
     _fields_ = [("term", ctypes.c_void_p * 4), ("coef", ctypes.c_int64 * 4), ("constant", ctypes.c_int64),
                 ("cols64", ctypes.c_uint64), ("nbits", ctypes.c_uint32), ("wire_rows", ctypes.c_void_p),
-                ("copy_out", ctypes.c_void_p), ("row_map", ctypes.c_uint64 * 6), ("map_rows", ctypes.c_uint64)]
+                ("copy_out", ctypes.c_void_p)]
 
 
 def timed(fn):

@@ -304,6 +304,19 @@ int aby3g_stream_destroy(aby3g_stream stream) {
         g_streams.erase(S(stream));
     });
 }
+int aby3g_null_queue_init(void) {
+    return guarded([&] {
+        static std::mutex mu;
+        static std::map<int, void*> done;  // per device: the word the null stream zeroed
+        const int dev = current_device();
+        std::lock_guard<std::mutex> lk(mu);
+        if (done.count(dev)) return;
+        void* q = nullptr;
+        ABY3G_CHECK_HIP(hipMalloc(&q, 256));
+        ABY3G_CHECK_HIP(hipMemset(q, 0, 256));  // the null stream: its hardware queue is created here
+        done[dev] = q;
+    });
+}
 int aby3g_stream_count(int device, int* n) {
     return guarded([&] {
         ABY3G_REQUIRE(n != nullptr, "null argument");

@@ -164,6 +164,7 @@ _SIGS = {
     "aby3g_set_handoff_timeout_us": (c_int, [c_uint64]),
     "aby3g_bin_level_residency": (c_int, [POINTER(c_int), POINTER(c_int), POINTER(c_int), POINTER(c_int)]),
     "aby3g_stream_count": (c_int, [c_int, POINTER(c_int)]),
+    "aby3g_null_queue_init": (c_int, []),
     "aby3g_malloc_uncached": (c_int, [POINTER(c_void_p), c_size_t]),
     "aby3g_device_uuid": (c_int, [c_int, c_void_p]),
     "aby3g_event_query": (c_int, [c_void_p, POINTER(c_int)]),

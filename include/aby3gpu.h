@@ -87,6 +87,12 @@ int aby3g_event_elapsed_ms(aby3g_event start, aby3g_event end, float* ms);
  * value before its later work starts. A cross-stream hand-off on one device
  * costs ~8 us this way against ~13.5 us for an event record + wait
  * (scripts/pingpong.hip); the channels of co-located parties use it. */
+/* Creates HIP's null stream (and so its hardware queue) on the current
+ * device, once per process and device; a no-op afterwards. The host calls it
+ * after all its parties' streams exist and before they enqueue work: HIP
+ * hands out hardware queues in stream-creation order, and where the null
+ * stream's queue comes in that order changed the jobs' speed. */
+int aby3g_null_queue_init(void);
 int aby3g_signal_alloc(uint64_t** word); /* zeroed (on a temporary stream, never the null stream,
                                             and waited for), on the current device */
 int aby3g_stream_write_value(aby3g_stream stream, uint64_t* word, uint64_t value);

@@ -45,6 +45,7 @@ OVERRIDES = {
     "aby3g_probe_read": "*ms = 0; *launches = 0; return 0;",
     "aby3g_handoff_status": "*timeouts = 0; return 0;",
     "aby3g_stream_count": "*n = 0; return 0;",
+    "aby3g_null_queue_init": "return 0;",
     "aby3g_bin_level_residency": "*cus = 256; *per_cu_small = 1; *per_cu_large = 5; *small_max_wgs = 128; return 0;",
     "aby3g_aes_block_host": "for (int i = 0; i < 16; ++i) out[i] = key[i] ^ (uint8_t)(ctr >> (8 * (i & 7))); return 0;",
     "aby3g_lr_mailbox_bytes": "return 4096;",

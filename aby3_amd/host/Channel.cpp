@@ -629,15 +629,6 @@ void Channel::asyncSendShared(std::shared_ptr<DeviceBuffer> buf, size_t bytes, G
     mOut->push(std::move(m));
 }
 
-bool Channel::handoffWouldPost(const Gpu& gpu, u64 rows, u64 producerBytes) const {
-    if (!mOut) return false;
-    const Pipe& p = *mOut;
-    if (!p.kernelHandoff || p.link || p.signalDevice != gpu.device() || kernelsSerialized() || !p.hsFlags) return false;
-    const u64 chunks = std::max<u64>(1, (rows + ABY3G_HANDOFF_ROWS - 1) / ABY3G_HANDOFF_ROWS);
-    if (!handoffResidencyOk(handoffResidency(gpu.device()), chunks)) return false;
-    return !(chunks > kHandoffChunks || (chunks > kHandoffMaxChunks && producerBytes > kHandoffLightBytes));
-}
-
 aby3g_handoff Channel::handoffPost(Gpu& gpu, u64 rows, u64 producerBytes, const void* payload) {
     if (!mOut) throw std::runtime_error("channel not connected");
     Pipe& p = *mOut;

@@ -100,9 +100,6 @@ public:
     // lease with evalSendEnd() once the evaluation's last message is sent.
     std::shared_ptr<DeviceBuffer> evalSendBuffer(Gpu& gpu, size_t bytes, u64 andLevels);
     void evalSendEnd();
-    // Would handoffPost(gpu, rows, producerBytes) hand the next message over
-    // in-kernel? (no side effects; the same answer handoffPost gives)
-    bool handoffWouldPost(const Gpu& gpu, u64 rows, u64 producerBytes = 0) const;
     // Both directions join parties on `gpu`'s device in this process whose
     // ring allows kernel hand-offs (a fused launch may then address the
     // peer's device memory and poll it).

@@ -344,6 +344,9 @@ void Sh3BinaryEvaluator::setInputs(const std::vector<WireInput>& in) {
         if (srcs.size() == ABY3G_WIRE_SRC_MAX) flush();
     }
     flush();
+    // transposed now (not held for the first level): the buffers the terms
+    // read are fenced behind that launch and released
+    if (mPendingIn.empty()) readHeld(true);
     mLevel = 0;
 }
 

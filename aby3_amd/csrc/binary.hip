@@ -440,19 +440,36 @@ __global__ void __launch_bounds__(64) k_b2w_lin_regs(WireSrcs ws, u64 rows, u64 
         if (c * 64 + b < src.nbits) out[(c * 64 + b) * words + w] = R[b];
 }
 
-// copy_out of every source only (aby3g_lin_copy_out), a thread per element
+// copy_out of every source only (aby3g_lin_copy_out), a thread per two
+// elements: 16-byte loads and stores (1 KiB per wave instruction; the copy-out
+// is the reshare message the next party's first level waits for)
 __global__ void __launch_bounds__(256) k_lin_copy(WireSrcs ws, u32 nsrc, u64 rows) {
-    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
+    const u64 i = ((u64)blockIdx.x * 256 + threadIdx.x) * 2;
 #pragma unroll
     for (u32 k = 0; k < ABY3G_WIRE_SRC_MAX; ++k) {
         if (k >= nsrc) break;
         const aby3g_wire_src& src = ws.s[k];
-        if (!src.copy_out || i >= rows * src.cols64) continue;
-        u64 v = 0;
+        const u64 n = rows * src.cols64;
+        if (!src.copy_out || i >= n) continue;
+        // 16-byte accesses when every pointer allows them (pool blocks do)
+        bool vec = i + 1 < n && ((uintptr_t)src.copy_out & 15) == 0;
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-            if (src.term[t]) v += (u64)src.coef[t] * (u64)src.term[t][i];
-        src.copy_out[i] = (i64)v;
+        for (int t = 0; t < 4; ++t) vec = vec && ((uintptr_t)src.term[t] & 15) == 0;
+        if (vec) {
+            u64x2 v = u64x2{0, 0};
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (src.term[t]) v += (u64)src.coef[t] * *reinterpret_cast<const u64x2*>(src.term[t] + i);
+            *reinterpret_cast<u64x2*>(src.copy_out + i) = v;
+        } else {
+            for (u64 j = i; j < i + 2 && j < n; ++j) {
+                u64 v = 0;
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    if (src.term[t]) v += (u64)src.coef[t] * (u64)src.term[t][j];
+                src.copy_out[j] = (i64)v;
+            }
+        }
     }
 }
 
@@ -921,7 +938,7 @@ int aby3g_lin_copy_out(const aby3g_wire_src* srcs, uint32_t nsrc, uint64_t rows,
             if (srcs[k].copy_out) n = std::max<u64>(n, rows * srcs[k].cols64);
         }
         if (!n) return;
-        launch(PROBE_OTHER, k_lin_copy, dim3((u32)((n + 255) / 256)), dim3(256), 0, S(stream), ws, nsrc, (u64)rows);
+        launch(PROBE_OTHER, k_lin_copy, dim3((u32)((n + 511) / 512)), dim3(256), 0, S(stream), ws, nsrc, (u64)rows);
     });
 }
 

@@ -138,6 +138,24 @@ def load_pmc(kind: str, cfg: dict, field: str = "hbm_bytes_per_launch"):
     return best
 
 
+def load_mfma(cfg: dict):
+    """The newest committed MFMA PMC summary (profiles/mfma_*.json, written by
+    scripts/mfma_summary.py for the C2 job at 1024^3), or None."""
+    import glob
+
+    if cfg != {"m": 1024, "k": 1024, "n": 1024}:
+        return None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "mfma_r*.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    keep = ("avg_ns", "effective_clock_ghz", "mfma_busy_frac_of_occupied_simds", "mfma_busy_over_issued_cycles",
+            "mfma_instructions", "note")
+    out = {k: d[k] for k in keep if k in d}
+    out["source"] = os.path.join("profiles", os.path.basename(files[-1]))
+    return out
+
+
 def compute_fraction(nt, job, params, dev, steps, warmup=3):
     """The local-compute fraction of wall clock, measured on the device: a
     separate pass of the job with every kernel launch bracketed by HIP events
@@ -678,6 +696,10 @@ def main():
             "job_mfma_rate_unit": "TOP/s: the three parties' share-GEMM int8 ops per step / the whole step",
             "launch_span_ms_overlapped": ovl_ms / max(ovl_n, 1),
             "ops_per_launch": info["gemm_int8_ops"],
+            # MFMA utilisation from the committed PMC pass of the same job
+            # (scripts/gemm_mfma_pmc.sh: SQ_VALU_MFMA_BUSY_CYCLES and the
+            # effective clock, GRBM_GUI_ACTIVE / 8 / wall), if there is one
+            "mfma_utilisation": load_mfma(cfg),
         },
         "kernel_ms_per_step": breakdown,
         # share of the wall clock a party's GPU stream spends computing (its

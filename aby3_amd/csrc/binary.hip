@@ -73,71 +73,123 @@ __global__ void __launch_bounds__(kGateBlock) k_bin_gates(const aby3g_gate* __re
 }
 
 // One whole communication level per launch. A workgroup owns 32 consecutive
-// words (2048 rows) of every wire; its threads are 8 (or, for launches of
-// few workgroups, 32) gate slots x 32 word lanes. It first unpacks the
+// words (2048 rows) of every wire; its 256 threads are 16 gate slots x 16
+// lanes of two words (or, for launches of few workgroups, 1024 threads: 32
+// slots x 32 lanes of one word). It first unpacks the
 // previous level's received AND shares into share 1, then runs the level's
 // gate batches in order, the slots striding over a batch's (independent)
 // gates, with a workgroup barrier
 // between batches: a gate only ever reads words of its own rows, so the
 // per-workgroup barrier orders every dependency of the level.
 constexpr u32 kLevelWords = 32;
-// launches of fewer workgroups than this take the 32-slot form (more gate
-// parallelism per workgroup), larger ones the 8-slot form
+// launches of fewer workgroups than this take the 1024-thread form (more
+// gate parallelism per workgroup), larger ones the 256-thread form
 constexpr u32 kLevelSmallMaxWgs = 128;
 
-// Operands of one gate on one word, loaded ahead of its evaluation so that a
-// slot can have several independent gates' loads in flight.
+// Words per lane: a lane of the level kernels' gate slots handles W
+// consecutive words of a gate's rows. The 256-thread forms take W = 2
+// (16-byte accesses, 16 lanes a slot, twice the slots of a workgroup): a
+// level alone 18.3 against 21.1 us (`scripts/bench_level.py`), C5 59.7-59.8
+// against 66.9-67.3 ms and C3 0.302-0.305 against 0.331 ms in a same-box
+// A/B. The 1024-thread forms of small launches keep W = 1 (C3's circuit over
+// 2^17 rows: 0.106-0.112 against 0.138-0.141 ms with W = 2).
+template <u32 W>
+struct Words;
+template <>
+struct Words<1> {
+    typedef u64 T;
+};
+template <>
+struct Words<2> {
+    typedef u64x2 T;
+};
+template <u32 W>
+using WordsT = typename Words<W>::T;
+
+template <u32 W>
+__device__ __forceinline__ WordsT<W> wzero() {
+    if constexpr (W == 1)
+        return 0;
+    else
+        return u64x2{0, 0};
+}
+template <u32 W>
+__device__ __forceinline__ WordsT<W> wld(const u64* p) {
+    return *reinterpret_cast<const WordsT<W>*>(p);
+}
+template <u32 W>
+__device__ __forceinline__ void wst(u64* p, WordsT<W> v) {
+    *reinterpret_cast<WordsT<W>*>(p) = v;
+}
+// received shares handed over in-kernel: read past this CU's L1 (sc1); sent
+// ones stored write-through
+template <u32 W>
+__device__ __forceinline__ WordsT<W> wld_hs(const u64* p) {
+    if constexpr (W == 1)
+        return hs_load(p);
+    else
+        return u64x2{hs_load(p), hs_load(p + 1)};
+}
+template <u32 W>
+__device__ __forceinline__ void wst_hs(u64* p, WordsT<W> v) {
+    if constexpr (W == 1) {
+        hs_store(p, v);
+    } else {
+        hs_store(p, v.x);
+        hs_store(p + 1, v.y);
+    }
+}
+
+// Operands of one gate on a lane's words, loaded ahead of its evaluation so
+// that a slot can have several independent gates' loads in flight.
+template <u32 W>
 struct GateOps {
-    u64 x0, x1, y0, y1, z;
+    WordsT<W> x0, x1, y0, y1, z;
 };
 
 // rr: the recv rows of the inputs' share 1 when they are the previous
 // level's AND outputs (~0u: read the engine memory), so that the gates need
 // not wait for the unpack of this launch
+template <u32 W>
 __device__ __forceinline__ void gate_load(const aby3g_gate& g, uint2 rr, const u64* s0, const u64* s1,
                                           const u64* __restrict__ recv, u64 words, u64 w, const u64* __restrict__ z,
-                                          GateOps& o, bool sc1) {  // sc1: compile-time constant at every call
+                                          GateOps<W>& o, bool sc1) {  // sc1: compile-time constant at every call
     // unary gates read in0 twice (in1 of an external gate list may be anything)
     const bool unary = g.type == ABY3G_GATE_COPY || g.type == ABY3G_GATE_INV;
     const u64 in1 = unary ? g.in0 : g.in1;
     const u32 r1 = unary ? rr.x : rr.y;
-    o.x0 = s0[g.in0 * words + w];
-    // received shares handed over in-kernel are read past this CU's L1 (sc1)
-    o.x1 = rr.x != ~0u ? (sc1 ? hs_load(recv + (u64)rr.x * words + w) : recv[(u64)rr.x * words + w])
-                       : s1[g.in0 * words + w];
-    o.y0 = s0[in1 * words + w];
-    o.y1 = r1 != ~0u ? (sc1 ? hs_load(recv + (u64)r1 * words + w) : recv[(u64)r1 * words + w]) : s1[in1 * words + w];
-    o.z = gate_is_and(g.type) ? z[(u64)g.z_row * words + w] : 0;
+    o.x0 = wld<W>(s0 + g.in0 * words + w);
+    o.x1 = rr.x != ~0u ? (sc1 ? wld_hs<W>(recv + (u64)rr.x * words + w) : wld<W>(recv + (u64)rr.x * words + w))
+                       : wld<W>(s1 + g.in0 * words + w);
+    o.y0 = wld<W>(s0 + in1 * words + w);
+    o.y1 = r1 != ~0u ? (sc1 ? wld_hs<W>(recv + (u64)r1 * words + w) : wld<W>(recv + (u64)r1 * words + w))
+                     : wld<W>(s1 + in1 * words + w);
+    o.z = gate_is_and(g.type) ? wld<W>(z + (u64)g.z_row * words + w) : wzero<W>();
 }
 
-__device__ __forceinline__ void gate_eval(const aby3g_gate& g, const GateOps& o, u64* s0, u64* s1, u64 words, u64 w,
-                                          u64* __restrict__ sendbuf, bool wt) {
-    const u64 x0 = o.x0, x1 = o.x1, y0 = o.y0, y1 = o.y1;
-    u64 o0, o1;
-    switch (g.type) {
-        case ABY3G_GATE_COPY:
-        case ABY3G_GATE_INV:
-        case ABY3G_GATE_XOR:
-        case ABY3G_GATE_NXOR: gate_local(g.type, x0, x1, y0, y1, o0, o1); break;
-        default: {
-            const u64 r = gate_and_share(g.type, x0, x1, y0, y1) ^ o.z;
-            s0[g.out * words + w] = r;
-            if (wt)  // a message handed over in-kernel: write-through
-                hs_store(sendbuf + (u64)g.send_row * words + w, r);
-            else
-                sendbuf[(u64)g.send_row * words + w] = r;
-            return;
-        }
+template <u32 W>
+__device__ __forceinline__ void gate_eval(const aby3g_gate& g, const GateOps<W>& o, u64* s0, u64* s1, u64 words,
+                                          u64 w, u64* __restrict__ sendbuf, bool wt) {
+    if (gate_is_and(g.type)) {
+        const WordsT<W> r = gate_and_share(g.type, o.x0, o.x1, o.y0, o.y1) ^ o.z;
+        wst<W>(s0 + g.out * words + w, r);
+        if (wt)  // a message handed over in-kernel: write-through
+            wst_hs<W>(sendbuf + (u64)g.send_row * words + w, r);
+        else
+            wst<W>(sendbuf + (u64)g.send_row * words + w, r);
+        return;
     }
-    s0[g.out * words + w] = o0;
-    s1[g.out * words + w] = o1;
+    WordsT<W> o0, o1;
+    gate_local(g.type, o.x0, o.x1, o.y0, o.y1, o0, o1);
+    wst<W>(s0 + g.out * words + w, o0);
+    wst<W>(s1 + g.out * words + w, o1);
 }
 
-// SLOTS gate slots x 32 word lanes. Each slot takes kLevelUnroll gates of a
-// batch per iteration, all their loads issued before any evaluation (the
+// SLOTS * W gate slots x 32 / W lanes. Each slot takes kLevelUnroll gates of
+// a batch per iteration, all their loads issued before any evaluation (the
 // gates of a batch are independent), so a batch of G gates costs about
-// G / (SLOTS * kLevelUnroll) dependent memory round trips -- the bound for the
-// few-workgroup launches of small row counts (LR: 256 rows, one workgroup).
+// G / (SLOTS * W * kLevelUnroll) dependent memory round trips -- the bound for
+// the few-workgroup launches of small row counts (LR: 256 rows, one workgroup).
 constexpr u32 kLevelUnroll = 4;
 // With rrows (per gate, see gate_load) no gate reads the wires this launch
 // unpacks, so the first batch starts without a barrier after the unpack.
@@ -147,7 +199,7 @@ constexpr u32 kLevelUnroll = 4;
 // publishes its own send rows for the next party's same workgroup (hp) --
 // the levels of the three parties pipeline chunk by chunk.
 static_assert(kLevelWords * 64 == ABY3G_HANDOFF_ROWS, "a level workgroup is one hand-off chunk");
-template <u32 SLOTS, bool HS>
+template <u32 SLOTS, bool HS, u32 W, u32 U = kLevelUnroll>
 __global__ void __launch_bounds__(SLOTS * 32) k_bin_level(const aby3g_gate* __restrict__ gates,
                                                          const uint2* __restrict__ rrows,
                                                          const u32* __restrict__ batch_ends, u32 nbatches,
@@ -159,33 +211,35 @@ __global__ void __launch_bounds__(SLOTS * 32) k_bin_level(const aby3g_gate* __re
     // HS: the in-kernel hand-off instantiation (sc1 payload accesses, waits
     // and posts); the other is the plain streaming kernel
     if (HS && !hs_wait(hw, blockIdx.x, blockIdx.x + 1)) return;
-    const u32 lane = threadIdx.x & 31, slot = threadIdx.x >> 5;
-    const u64 w = (u64)blockIdx.x * kLevelWords + lane;
+    constexpr u32 kLanes = 32 / W, NS = SLOTS * W;
+    const u32 lane = threadIdx.x % kLanes, slot = threadIdx.x / kLanes;
+    const u64 w = (u64)blockIdx.x * kLevelWords + W * lane;
     u64* s0 = mem;
     u64* s1 = mem + wires * words;
 #pragma unroll 4
-    for (u32 j = slot; j < nunpack; j += SLOTS)
-        s1[(u64)unpack_wires[j] * words + w] = (HS && hw.flags) ? hs_load(recv + (u64)j * words + w) : recv[(u64)j * words + w];
+    for (u32 j = slot; j < nunpack; j += NS)
+        wst<W>(s1 + (u64)unpack_wires[j] * words + w,
+               (HS && hw.flags) ? wld_hs<W>(recv + (u64)j * words + w) : wld<W>(recv + (u64)j * words + w));
     u32 begin = 0;
     for (u32 b = 0; b < nbatches; ++b) {
         if (b || !rrows) __syncthreads();
         const u32 end = batch_ends[b];
-        for (u32 g0 = begin + slot; g0 < end; g0 += kLevelUnroll * SLOTS) {
-            aby3g_gate g[kLevelUnroll];
-            uint2 rr[kLevelUnroll];
-            GateOps o[kLevelUnroll];
+        for (u32 g0 = begin + slot; g0 < end; g0 += U * NS) {
+            aby3g_gate g[U];
+            uint2 rr[U];
+            GateOps<W> o[U];
 #pragma unroll
-            for (u32 k = 0; k < kLevelUnroll; ++k)
-                if (g0 + k * SLOTS < end) {
-                    g[k] = gates[g0 + k * SLOTS];
-                    rr[k] = rrows ? rrows[g0 + k * SLOTS] : make_uint2(~0u, ~0u);
+            for (u32 k = 0; k < U; ++k)
+                if (g0 + k * NS < end) {
+                    g[k] = gates[g0 + k * NS];
+                    rr[k] = rrows ? rrows[g0 + k * NS] : make_uint2(~0u, ~0u);
                 }
 #pragma unroll
-            for (u32 k = 0; k < kLevelUnroll; ++k)
-                if (g0 + k * SLOTS < end) gate_load(g[k], rr[k], s0, s1, recv, words, w, z, o[k], HS);
+            for (u32 k = 0; k < U; ++k)
+                if (g0 + k * NS < end) gate_load<W>(g[k], rr[k], s0, s1, recv, words, w, z, o[k], HS);
 #pragma unroll
-            for (u32 k = 0; k < kLevelUnroll; ++k)
-                if (g0 + k * SLOTS < end) gate_eval(g[k], o[k], s0, s1, words, w, sendbuf, HS);
+            for (u32 k = 0; k < U; ++k)
+                if (g0 + k * NS < end) gate_eval<W>(g[k], o[k], s0, s1, words, w, sendbuf, HS);
         }
         begin = end;
     }
@@ -490,30 +544,32 @@ constexpr u32 kInMax = ABY3G_LEVEL_IN_MAX_WIRES;
 // operands of one gate: input wires through tab (the LDS row of (wire - inLo,
 // share) in win, kInZero: an all-zero source), other wires from mem
 constexpr u32 kInZero = 0xffff;
-__device__ __forceinline__ u64 in_word(const u64* win, unsigned short row, u32 wl) {
-    return row == kInZero ? 0 : win[(u32)row * kLevelWords + wl];
+template <u32 W = 1>
+__device__ __forceinline__ WordsT<W> in_word(const u64* win, unsigned short row, u32 wl) {
+    return row == kInZero ? wzero<W>() : wld<W>(win + (u32)row * kLevelWords + wl);
 }
-__device__ __forceinline__ void gate_load_in(const aby3g_gate& g, const u64* win, const unsigned short* tab, u32 inLo, u32 nin,
-                                             const u64* s0, const u64* s1, u64 words, u64 w, u32 wl,
-                                             const u64* __restrict__ z, GateOps& o) {
+template <u32 W>
+__device__ __forceinline__ void gate_load_in(const aby3g_gate& g, const u64* win, const unsigned short* tab, u32 inLo,
+                                             u32 nin, const u64* s0, const u64* s1, u64 words, u64 w, u32 wl,
+                                             const u64* __restrict__ z, GateOps<W>& o) {
     const bool unary = g.type == ABY3G_GATE_COPY || g.type == ABY3G_GATE_INV;
     const u32 in1 = unary ? g.in0 : g.in1;
     const u32 a = g.in0 - inLo, b = in1 - inLo;
     if (a < nin) {
-        o.x0 = in_word(win, tab[2 * a], wl);
-        o.x1 = in_word(win, tab[2 * a + 1], wl);
+        o.x0 = in_word<W>(win, tab[2 * a], wl);
+        o.x1 = in_word<W>(win, tab[2 * a + 1], wl);
     } else {
-        o.x0 = s0[(u64)g.in0 * words + w];
-        o.x1 = s1[(u64)g.in0 * words + w];
+        o.x0 = wld<W>(s0 + (u64)g.in0 * words + w);
+        o.x1 = wld<W>(s1 + (u64)g.in0 * words + w);
     }
     if (b < nin) {
-        o.y0 = in_word(win, tab[2 * b], wl);
-        o.y1 = in_word(win, tab[2 * b + 1], wl);
+        o.y0 = in_word<W>(win, tab[2 * b], wl);
+        o.y1 = in_word<W>(win, tab[2 * b + 1], wl);
     } else {
-        o.y0 = s0[(u64)in1 * words + w];
-        o.y1 = s1[(u64)in1 * words + w];
+        o.y0 = wld<W>(s0 + (u64)in1 * words + w);
+        o.y1 = wld<W>(s1 + (u64)in1 * words + w);
     }
-    o.z = gate_is_and(g.type) ? z[(u64)g.z_row * words + w] : 0;
+    o.z = gate_is_and(g.type) ? wld<W>(z + (u64)g.z_row * words + w) : wzero<W>();
 }
 
 // One workgroup per ABY3G_HANDOFF_ROWS chunk, as k_bin_level. Its waves first
@@ -525,7 +581,7 @@ __device__ __forceinline__ void gate_load_in(const aby3g_gate& g, const u64* win
 // 64 rows). The inputs are read once, as the rows of the shares, and the
 // level's gates then read the input wires from LDS instead of HBM (the first
 // level of a 64-bit comparison reads each input wire 2-3 times).
-template <u32 SLOTS, bool HS>
+template <u32 SLOTS, bool HS, u32 W>
 __global__ void __launch_bounds__(SLOTS * 32) k_bin_level_in(LevelInSrcs srcs, u32 nsrc, u64 rows, u32 inLo, u32 nin,
                                                             int writeInputs, const aby3g_gate* __restrict__ gates,
                                                             const u32* __restrict__ batch_ends, u32 nbatches,
@@ -584,24 +640,25 @@ __global__ void __launch_bounds__(SLOTS * 32) k_bin_level_in(LevelInSrcs srcs, u
             const u32 wl = i % kLevelWords, sh = (i / kLevelWords) & 1, wi = i / (2 * kLevelWords);
             (sh ? s1 : s0)[(u64)(inLo + wi) * words + w0 + wl] = in_word(win, tab[2 * wi + sh], wl);
         }
-    const u32 lane = tid & 31, slot = tid >> 5;
-    const u64 w = w0 + lane;
+    constexpr u32 kLanes = 32 / W, NS = SLOTS * W;
+    const u32 wl = W * (tid % kLanes), slot = tid / kLanes;
+    const u64 w = w0 + wl;
     u32 begin = 0;
     for (u32 b = 0; b < nbatches; ++b) {
         if (b) __syncthreads();
         const u32 end = batch_ends[b];
-        for (u32 g0 = begin + slot; g0 < end; g0 += kLevelUnroll * SLOTS) {
+        for (u32 g0 = begin + slot; g0 < end; g0 += kLevelUnroll * NS) {
             aby3g_gate g[kLevelUnroll];
-            GateOps o[kLevelUnroll];
+            GateOps<W> o[kLevelUnroll];
 #pragma unroll
             for (u32 k = 0; k < kLevelUnroll; ++k)
-                if (g0 + k * SLOTS < end) g[k] = gates[g0 + k * SLOTS];
+                if (g0 + k * NS < end) g[k] = gates[g0 + k * NS];
 #pragma unroll
             for (u32 k = 0; k < kLevelUnroll; ++k)
-                if (g0 + k * SLOTS < end) gate_load_in(g[k], win, tab, inLo, nin, s0, s1, words, w, lane, z, o[k]);
+                if (g0 + k * NS < end) gate_load_in<W>(g[k], win, tab, inLo, nin, s0, s1, words, w, wl, z, o[k]);
 #pragma unroll
             for (u32 k = 0; k < kLevelUnroll; ++k)
-                if (g0 + k * SLOTS < end) gate_eval(g[k], o[k], s0, s1, words, w, sendbuf, HS);
+                if (g0 + k * NS < end) gate_eval<W>(g[k], o[k], s0, s1, words, w, sendbuf, HS);
         }
         begin = end;
     }
@@ -818,17 +875,22 @@ static int bin_level(const aby3g_gate* gates, const uint32_t* recv_rows, const u
         // a launch that only waits or only posts)
         if (wgs < kLevelSmallMaxWgs) {
             if (hs)
-                launch(PROBE_BINARY, k_bin_level<32, true>, dim3(wgs), dim3(32 * 32), 0, S(stream), gates, rrows,
+                launch(PROBE_BINARY, k_bin_level<32, true, 1>, dim3(wgs), dim3(32 * 32), 0, S(stream), gates, rrows,
                        batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp);
             else
-                launch(PROBE_BINARY, k_bin_level<32, false>, dim3(wgs), dim3(32 * 32), 0, S(stream), gates, rrows,
+                launch(PROBE_BINARY, k_bin_level<32, false, 1>, dim3(wgs), dim3(32 * 32), 0, S(stream), gates, rrows,
                        batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp);
         } else {
+            // the hand-off form unrolls two gates a slot, not four: 74 VGPRs
+            // against 130, six workgroups a CU against three, so that C3's
+            // 512-chunk messages still pass the residency rule (C3 0.302-0.305
+            // against 0.337-0.338 ms with the four-gate form and stream
+            // hand-offs, and 0.308-0.311 with one word per lane)
             if (hs)
-                launch(PROBE_BINARY, k_bin_level<8, true>, dim3(wgs), dim3(8 * 32), 0, S(stream), gates, rrows,
+                launch(PROBE_BINARY, k_bin_level<8, true, 2, 2>, dim3(wgs), dim3(8 * 32), 0, S(stream), gates, rrows,
                        batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp);
             else
-                launch(PROBE_BINARY, k_bin_level<8, false>, dim3(wgs), dim3(8 * 32), 0, S(stream), gates, rrows,
+                launch(PROBE_BINARY, k_bin_level<8, false, 2>, dim3(wgs), dim3(8 * 32), 0, S(stream), gates, rrows,
                        batch_ends, nbatches, recvbuf, unpack_wires, nunpack, mem, wires, words, z, sendbuf, hw, hp);
         }
     });
@@ -852,10 +914,10 @@ int aby3g_bin_level_residency(int* cus, int* per_cu_small, int* per_cu_large, in
         // binary engine)
         int a = 0;
         ABY3G_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &a, reinterpret_cast<const void*>(k_bin_level<32, true>), 32 * 32, 0));
+            &a, reinterpret_cast<const void*>(k_bin_level<32, true, 1>), 32 * 32, 0));
         *per_cu_small = a;
         ABY3G_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &a, reinterpret_cast<const void*>(k_bin_level<8, true>), 8 * 32, 0));
+            &a, reinterpret_cast<const void*>(k_bin_level<8, true, 2, 2>), 8 * 32, 0));
         *per_cu_large = a;
         *small_max_wgs = (int)kLevelSmallMaxWgs;
     });
@@ -986,8 +1048,8 @@ int aby3g_bin_level_in(const aby3g_wire_src* srcs, uint32_t nsrc, uint64_t rows,
         const size_t lds = (size_t)nl * 64 * kLevelWords * 8;
         static const bool attr = [] {  // up to 8 sources (128 KiB) of dynamic LDS, once per process
             bool ok = true;
-            for (const void* f : {(const void*)k_bin_level_in<32, true>, (const void*)k_bin_level_in<32, false>,
-                                  (const void*)k_bin_level_in<8, true>, (const void*)k_bin_level_in<8, false>})
+            for (const void* f : {(const void*)k_bin_level_in<32, true, 1>, (const void*)k_bin_level_in<32, false, 1>,
+                                  (const void*)k_bin_level_in<8, true, 2>, (const void*)k_bin_level_in<8, false, 2>})
                 ok = ok && hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 128 << 10) == hipSuccess;
             return ok;
         }();
@@ -995,20 +1057,20 @@ int aby3g_bin_level_in(const aby3g_wire_src* srcs, uint32_t nsrc, uint64_t rows,
         nsrc = nl;
         if (wgs < kLevelSmallMaxWgs) {
             if (hp.flags)
-                launch(PROBE_BINARY, k_bin_level_in<32, true>, dim3(wgs), dim3(32 * 32), lds, S(stream), ls, nsrc,
+                launch(PROBE_BINARY, k_bin_level_in<32, true, 1>, dim3(wgs), dim3(32 * 32), lds, S(stream), ls, nsrc,
                        (u64)rows, in_lo, nin, write_inputs, gates, batch_ends, nbatches, mem, wires, words, z, sendbuf,
                        hp);
             else
-                launch(PROBE_BINARY, k_bin_level_in<32, false>, dim3(wgs), dim3(32 * 32), lds, S(stream), ls, nsrc,
+                launch(PROBE_BINARY, k_bin_level_in<32, false, 1>, dim3(wgs), dim3(32 * 32), lds, S(stream), ls, nsrc,
                        (u64)rows, in_lo, nin, write_inputs, gates, batch_ends, nbatches, mem, wires, words, z, sendbuf,
                        hp);
         } else {
             if (hp.flags)
-                launch(PROBE_BINARY, k_bin_level_in<8, true>, dim3(wgs), dim3(8 * 32), lds, S(stream), ls, nsrc,
+                launch(PROBE_BINARY, k_bin_level_in<8, true, 2>, dim3(wgs), dim3(8 * 32), lds, S(stream), ls, nsrc,
                        (u64)rows, in_lo, nin, write_inputs, gates, batch_ends, nbatches, mem, wires, words, z, sendbuf,
                        hp);
             else
-                launch(PROBE_BINARY, k_bin_level_in<8, false>, dim3(wgs), dim3(8 * 32), lds, S(stream), ls, nsrc,
+                launch(PROBE_BINARY, k_bin_level_in<8, false, 2>, dim3(wgs), dim3(8 * 32), lds, S(stream), ls, nsrc,
                        (u64)rows, in_lo, nin, write_inputs, gates, batch_ends, nbatches, mem, wires, words, z, sendbuf,
                        hp);
         }

@@ -393,15 +393,17 @@ inline hipStream_t S(aby3g_stream s) { return reinterpret_cast<hipStream_t>(s); 
 __device__ __forceinline__ bool gate_is_and(u32 t) {
     return t == ABY3G_GATE_AND || t == ABY3G_GATE_OR || t == ABY3G_GATE_NOR || t == ABY3G_GATE_NA_AND;
 }
-// share 0 of an AND-type gate before its mask
-__device__ __forceinline__ u64 gate_and_share(u32 type, u64 x0, u64 x1, u64 y0, u64 y1) {
+// share 0 of an AND-type gate before its mask (T: u64, or a vector of words)
+template <class T>
+__device__ __forceinline__ T gate_and_share(u32 type, T x0, T x1, T y0, T y1) {
     if (type == ABY3G_GATE_AND) return (x0 & y0) ^ (x0 & y1) ^ (x1 & y0);
     if (type == ABY3G_GATE_OR) return (x0 & y0) ^ (x0 & y1) ^ (x1 & y0) ^ x0 ^ y0;
     if (type == ABY3G_GATE_NOR) return (~x0 & ~y0) ^ (~x0 & ~y1) ^ (~x1 & ~y0);
     return (~x0 & y0) ^ (~x0 & y1) ^ (~x1 & y0);  // NA_AND
 }
 // both shares of a local gate (COPY, INV, XOR, NXOR)
-__device__ __forceinline__ void gate_local(u32 type, u64 x0, u64 x1, u64 y0, u64 y1, u64& o0, u64& o1) {
+template <class T>
+__device__ __forceinline__ void gate_local(u32 type, T x0, T x1, T y0, T y1, T& o0, T& o1) {
     switch (type) {
         case ABY3G_GATE_COPY: o0 = x0; o1 = x1; break;
         case ABY3G_GATE_INV: o0 = ~x0; o1 = ~x1; break;

@@ -763,6 +763,7 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
                 if (mw.ok) mem[WS + (u64)andWires[pl.and_wire_off + j] * W + w] = v;
             }
             if (!msg_done(mw, &msgBad, ticks)) return;
+            if (lv <= 7) lr_stamp(PT, 23 + lv);  // level lv - 1's AND shares in
         }
         if (lv == cir.nlevels) break;
         const aby3g_lr_level& lvr = levelsL[lv];

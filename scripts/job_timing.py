@@ -12,6 +12,7 @@ job = sys.argv[1]
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 40
 jobs = {"mul": (nt.JOB_MUL_TRUNC, [1024, 1024, 1024, 16, 1], 10),
         "mul2": (nt.JOB_MUL_TRUNC, [1024, 1024, 1024, 16, 1, 2], 10), "msb": (nt.JOB_MSB, [1 << 20], 5),
+        "msb17": (nt.JOB_MSB, [1 << 17], 5),
         "sort": (nt.JOB_SORT, [1 << 20], 1), "lr": (nt.JOB_LR, [1000000, 128, 256, 16, 11], 20),
         "a2b": (nt.JOB_A2B, [1 << 20], 5)}
 j, params, warm = jobs[job]

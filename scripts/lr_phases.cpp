@@ -128,6 +128,24 @@ int main(int argc, char** argv) {
                     std::printf(" L%d %.1f", lv, v[v.size() / 2]);
                 }
             }
+            // slots 23 + lv (lv = 1..7): level lv - 1's AND shares received and unpacked
+            std::printf("\n   level lv: wait for lv-1's shares + unpack / gates:");
+            for (int lv = 1; lv < 8; ++lv) {
+                std::vector<double> a, b;
+                for (u64 t = iters / 2; t < iters; ++t) {
+                    const u64 e0 = stamps[p][32 * t + 16 + lv - 1], r = stamps[p][32 * t + 23 + lv],
+                              e1 = stamps[p][32 * t + 16 + lv];
+                    if (r && e1) {
+                        a.push_back(0.01 * (double)(r - e0));
+                        b.push_back(0.01 * (double)(e1 - r));
+                    }
+                }
+                if (!a.empty()) {
+                    std::sort(a.begin(), a.end());
+                    std::sort(b.begin(), b.end());
+                    std::printf(" L%d %.2f/%.2f", lv, a[a.size() / 2], b[b.size() / 2]);
+                }
+            }
             std::printf("\n  ");
         }
         std::vector<double> gap;  // launch-to-launch gap: end of t-1 to start of t

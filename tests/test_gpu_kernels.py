@@ -550,7 +550,7 @@ def test_handoff_residency_rule(gpu):
     of k_bin_level has silently moved them back to stream hand-offs."""
     cus, small, large, smax = (ctypes.c_int() for _ in range(4))
     nt.lib().bin_level_residency(ctypes.byref(cus), ctypes.byref(small), ctypes.byref(large), ctypes.byref(smax))
-    print(f"residency: {cus.value} CUs, k_bin_level<32,true> {small.value}/CU, <8,true> {large.value}/CU, "
+    print(f"residency: {cus.value} CUs, k_bin_level<32,true,1> {small.value}/CU, <8,true,2,2> {large.value}/CU, "
           f"small form below {smax.value} workgroups")
     assert cus.value >= 1 and small.value >= 1 and large.value >= 1
     per = lambda c: small.value if c < smax.value else large.value  # noqa: E731

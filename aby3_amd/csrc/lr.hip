@@ -752,27 +752,33 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
     // batches, then publish its AND shares
     const u64* zm = zmw;
     const u32 W32 = (u32)W;
+    // gate-word q -> (q / W, q % W): a shift when W is a power of two (a
+    // 32-bit division is ~30 VALU ops on the levels' critical path)
+    const u32 wsh = (W32 & (W32 - 1)) == 0 ? (u32)__builtin_ctz(W32) : 32u;
+    auto wdiv = [&](u32 q) { return wsh < 32 ? q >> wsh : q / W32; };
     for (u32 lv = 0; lv <= cir.nlevels; ++lv) {
         if (lv > 0 && levelsL[lv - 1].nand) {
-            const aby3g_lr_level& pl = levelsL[lv - 1];
+            const aby3g_lr_level pl = levelsL[lv - 1];
             const u64* grows = pv + L.lvl + 2 * (u64)pl.and_wire_off * W;
             MsgWait mw = msg_begin(tag, status);
             for (u32 q = tid; q < pl.nand * W32 && mw.ok; q += kLrThreads) {
                 const u64 v = msg_get(grows, q, mw);
-                const u32 j = q / W32, w = q - j * W32;
+                const u32 j = wdiv(q), w = q - j * W32;
                 if (mw.ok) mem[WS + (u64)andWires[pl.and_wire_off + j] * W + w] = v;
             }
             if (!msg_done(mw, &msgBad, ticks)) return;
             if (lv <= 7) lr_stamp(PT, 23 + lv);  // level lv - 1's AND shares in
         }
         if (lv == cir.nlevels) break;
-        const aby3g_lr_level& lvr = levelsL[lv];
+        // by value: the engine memory's LDS stores below would otherwise
+        // force a re-read of the level's fields after every gate
+        const aby3g_lr_level lvr = levelsL[lv];
         u64* gsend = my + L.lvl + 2 * (u64)lvr.and_wire_off * W;
         u32 begin = 0;
         for (u32 b = 0; b < lvr.nbatch; ++b) {
             const u32 end = batchEndsL[lvr.batch_off + b];
             for (u32 q = tid; q < (end - begin) * W32; q += kLrThreads) {
-                const u32 gq = q / W32, w = q - gq * W32;  // 32-bit: a 64-bit divide per gate-word cost ~1 us per level
+                const u32 gq = wdiv(q), w = q - gq * W32;
                 const aby3g_gate g = gates[lvr.first_gate + begin + gq];
                 const bool unary = g.type == ABY3G_GATE_COPY || g.type == ABY3G_GATE_INV;
                 const u32 in1 = unary ? g.in0 : g.in1;
@@ -789,7 +795,9 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
                     mem[WS + (u64)g.out * W + w] = o1;
                 }
             }
+            if (lv < 8 && b < 4) lr_stamp(PT, 64 + 4 * lv + b);
             __syncthreads();
+            if (lv < 8 && b < 4) lr_stamp(PT, 32 + 4 * lv + b);
             begin = end;
         }
         if (lv < 16) lr_stamp(PT, 16 + lv);

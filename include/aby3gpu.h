@@ -583,7 +583,7 @@ typedef struct {
     uint64_t epoch;
     uint32_t sys_scope;
     uint64_t* wait_ticks;    /* optional: in-kernel wait (100 MHz ticks) added here */
-    uint64_t* phase_ticks;   /* optional: [32] wall-clock stamps of the phases (profiling) */
+    uint64_t* phase_ticks;   /* optional: [96] wall-clock stamps of the phases (profiling) */
     /* the evaluator's ShareGen streams (seeds) and zero-share keys */
     uint8_t prev_seed[16], next_seed[16];
     uint8_t zs_prev[16], zs_next[16];

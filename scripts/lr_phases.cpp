@@ -50,21 +50,21 @@ int main(int argc, char** argv) {
             }
             aby3ML ml(rt, enc, ev, D);
             SgdState st;
-            DeviceBuffer dIdx(rt.gpu(), idx.size() * 4), ticks(rt.gpu(), iters * 32 * 8);
+            DeviceBuffer dIdx(rt.gpu(), idx.size() * 4), ticks(rt.gpu(), iters * 96 * 8);
             toDevice(dIdx.data(), idx.data(), idx.size() * 4, rt.gpu());
-            const std::vector<u64> zeros(iters * 32, 0);  // unused slots read 0
-            toDevice(ticks.data(), zeros.data(), iters * 32 * 8, rt.gpu());
+            const std::vector<u64> zeros(iters * 96, 0);  // unused slots read 0
+            toDevice(ticks.data(), zeros.data(), iters * 96 * 8, rt.gpu());
             rt.gpu().sync();
             const auto t0 = std::chrono::steady_clock::now();
             for (u64 t = 0; t < iters; ++t) {
-                st.phaseTicks = ticks.as<u64>() + 32 * t;
+                st.phaseTicks = ticks.as<u64>() + 96 * t;
                 sgdLogisticStep(ml, sX, sY, sW, dIdx.as<u32>() + t * B, B, aB, st);
             }
             rt.gpu().sync();
             if (p == 0)
                 wallUs = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-            stamps[p].resize(iters * 32);
-            toHost(stamps[p].data(), ticks.data(), iters * 32 * 8, rt.gpu());
+            stamps[p].resize(iters * 96);
+            toHost(stamps[p].data(), ticks.data(), iters * 96 * 8, rt.gpu());
             if (!st.fused) std::printf("party %d: fused form NOT taken\n", p);
         });
     for (auto& t : th) t.join();
@@ -79,30 +79,30 @@ int main(int argc, char** argv) {
         for (int ph = 0; ph < 11; ++ph) {
             std::vector<double> v;
             for (u64 t = iters / 2; t < iters; ++t)
-                v.push_back(0.01 * (double)(stamps[p][32 * t + ph + 1] - stamps[p][32 * t + ph]));
+                v.push_back(0.01 * (double)(stamps[p][96 * t + ph + 1] - stamps[p][96 * t + ph]));
             std::sort(v.begin(), v.end());
             std::printf(" %s %.1f |", names[ph], v[v.size() / 2]);
             tot += v[v.size() / 2];
         }
         {
             std::vector<double> v;
-            for (u64 t = iters / 2; t < iters; ++t) v.push_back(0.01 * (double)(stamps[p][32 * t + 12] - stamps[p][32 * t]));
+            for (u64 t = iters / 2; t < iters; ++t) v.push_back(0.01 * (double)(stamps[p][96 * t + 12] - stamps[p][96 * t]));
             std::sort(v.begin(), v.end());
             std::printf(" (table fill %.1f)", v[v.size() / 2]);
             std::vector<double> f;
             for (u64 t = iters / 2; t < iters; ++t)
-                f.push_back(100.0 * (double)(stamps[p][32 * t + 14] - stamps[p][32 * t + 13]) /
-                            (double)(stamps[p][32 * t + 11] - stamps[p][32 * t]));
+                f.push_back(100.0 * (double)(stamps[p][96 * t + 14] - stamps[p][96 * t + 13]) /
+                            (double)(stamps[p][96 * t + 11] - stamps[p][96 * t]));
             std::sort(f.begin(), f.end());
             std::printf(" (shader clock %.0f MHz)", f[f.size() / 2]);
             std::vector<double> pr;  // slot 15: an optional probe stamp after slot 12
             for (u64 t = iters / 2; t < iters; ++t)
-                if (stamps[p][32 * t + 15]) pr.push_back(0.01 * (double)(stamps[p][32 * t + 15] - stamps[p][32 * t + 12]));
+                if (stamps[p][96 * t + 15]) pr.push_back(0.01 * (double)(stamps[p][96 * t + 15] - stamps[p][96 * t + 12]));
             std::vector<double> sk, ld;
             for (u64 t = iters / 2; t < iters; ++t)
-                if (stamps[p][32 * t + 31]) {
-                    sk.push_back(0.01 * (double)(stamps[p][32 * t + 30] - stamps[p][32 * t]));
-                    ld.push_back(0.01 * (double)(stamps[p][32 * t + 31] - stamps[p][32 * t]));
+                if (stamps[p][96 * t + 31]) {
+                    sk.push_back(0.01 * (double)(stamps[p][96 * t + 30] - stamps[p][96 * t]));
+                    ld.push_back(0.01 * (double)(stamps[p][96 * t + 31] - stamps[p][96 * t]));
                 }
             if (!sk.empty()) {
                 std::sort(sk.begin(), sk.end());
@@ -120,7 +120,7 @@ int main(int argc, char** argv) {
             for (int lv = 0; lv < 8; ++lv) {
                 std::vector<double> v;
                 for (u64 t = iters / 2; t < iters; ++t) {
-                    const u64 a = stamps[p][32 * t + (lv ? 16 + lv - 1 : 5)], b = stamps[p][32 * t + 16 + lv];
+                    const u64 a = stamps[p][96 * t + (lv ? 16 + lv - 1 : 5)], b = stamps[p][96 * t + 16 + lv];
                     if (b) v.push_back(0.01 * (double)(b - a));
                 }
                 if (!v.empty()) {
@@ -133,8 +133,8 @@ int main(int argc, char** argv) {
             for (int lv = 1; lv < 8; ++lv) {
                 std::vector<double> a, b;
                 for (u64 t = iters / 2; t < iters; ++t) {
-                    const u64 e0 = stamps[p][32 * t + 16 + lv - 1], r = stamps[p][32 * t + 23 + lv],
-                              e1 = stamps[p][32 * t + 16 + lv];
+                    const u64 e0 = stamps[p][96 * t + 16 + lv - 1], r = stamps[p][96 * t + 23 + lv],
+                              e1 = stamps[p][96 * t + 16 + lv];
                     if (r && e1) {
                         a.push_back(0.01 * (double)(r - e0));
                         b.push_back(0.01 * (double)(e1 - r));
@@ -146,10 +146,40 @@ int main(int argc, char** argv) {
                     std::printf(" L%d %.2f/%.2f", lv, a[a.size() / 2], b[b.size() / 2]);
                 }
             }
+            // slots 32 + 4 lv + b: end of batch b of level lv (b < 4)
+            std::printf("\n   batch ends after the shares (us):");
+            for (int lv = 1; lv < 8; ++lv) {
+                std::printf(" L%d", lv);
+                for (int b = 0; b < 4; ++b) {
+                    std::vector<double> v;
+                    for (u64 t = iters / 2; t < iters; ++t) {
+                        const u64 r = stamps[p][96 * t + 23 + lv], e = stamps[p][96 * t + 32 + 4 * lv + b];
+                        if (r && e) v.push_back(0.01 * (double)(e - r));
+                    }
+                    if (v.empty()) break;
+                    std::sort(v.begin(), v.end());
+                    std::printf("%s%.2f", b ? "," : " ", v[v.size() / 2]);
+                }
+            }
+            // slots 64 + 4 lv + b: thread 0 before batch b's barrier
+            std::printf("\n   thread 0 before the barrier (us):");
+            for (int lv = 1; lv < 8; ++lv) {
+                std::printf(" L%d", lv);
+                for (int b = 0; b < 4; ++b) {
+                    std::vector<double> v;
+                    for (u64 t = iters / 2; t < iters; ++t) {
+                        const u64 r = stamps[p][96 * t + 23 + lv], e = stamps[p][96 * t + 64 + 4 * lv + b];
+                        if (r && e) v.push_back(0.01 * (double)(e - r));
+                    }
+                    if (v.empty()) break;
+                    std::sort(v.begin(), v.end());
+                    std::printf("%s%.2f", b ? "," : " ", v[v.size() / 2]);
+                }
+            }
             std::printf("\n  ");
         }
         std::vector<double> gap;  // launch-to-launch gap: end of t-1 to start of t
-        for (u64 t = iters / 2; t < iters; ++t) gap.push_back(0.01 * (double)(stamps[p][32 * t] - stamps[p][32 * (t - 1) + 11]));
+        for (u64 t = iters / 2; t < iters; ++t) gap.push_back(0.01 * (double)(stamps[p][96 * t] - stamps[p][96 * (t - 1) + 11]));
         std::sort(gap.begin(), gap.end());
         std::printf(" total %.1f us, gap between launches %.1f us\n", tot, gap[gap.size() / 2]);
     }

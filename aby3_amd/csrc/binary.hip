@@ -416,15 +416,26 @@ __global__ void __launch_bounds__(64) k_w2b_regs(const u64* __restrict__ mem, u6
 __global__ void __launch_bounds__(256) k_w2b_few(const u64* __restrict__ mem, u64 shareStride,
                                                  const u32* __restrict__ wires, u32 nbits, u64 words,
                                                  i64* __restrict__ out, u64 rows) {
-    const u64 r = (u64)blockIdx.x * 256 + threadIdx.x;
+    // two rows a thread: one 16-byte store when both exist and are 16-byte
+    // aligned (r is even: an even row count and an aligned output)
+    const u64 r = 2 * ((u64)blockIdx.x * 256 + threadIdx.x);
     if (r >= rows) return;
     mem += (u64)blockIdx.y * shareStride;
     out += (u64)blockIdx.y * rows;
     const u64 w = r >> 6;
-    const u32 sh = (u32)(r & 63);
-    u64 v = 0;
-    for (u32 b = 0; b < nbits; ++b) v |= ((mem[(u64)wires[b] * words + w] >> sh) & 1ull) << b;
-    out[r] = (i64)v;
+    const u32 sh = (u32)(r & 63);  // even: rows r, r + 1 share the word
+    u64 v0 = 0, v1 = 0;
+    for (u32 b = 0; b < nbits; ++b) {
+        const u64 x = mem[(u64)wires[b] * words + w] >> sh;
+        v0 |= (x & 1ull) << b;
+        v1 |= ((x >> 1) & 1ull) << b;
+    }
+    if (r + 1 < rows && ((uintptr_t)(out + r) & 15) == 0) {
+        *reinterpret_cast<u64x2*>(out + r) = u64x2{v0, v1};
+    } else {
+        out[r] = (i64)v0;
+        if (r + 1 < rows) out[r + 1] = (i64)v1;
+    }
 }
 
 // The mapped (gather / scatter) transposes keep the LDS-tiled kernels below:
@@ -1088,7 +1099,7 @@ int aby3g_wires_to_bits2(const uint64_t* mem, uint64_t share_stride, const uint3
         ABY3G_REQUIRE(words * 64 >= rows, "words too small for rows");
         if (!nbits || !rows) return;
         if (nbits <= 8) {
-            launch(PROBE_OTHER, k_w2b_few, dim3((u32)((rows + 255) / 256), 2), dim3(256), 0, S(stream), mem,
+            launch(PROBE_OTHER, k_w2b_few, dim3((u32)((rows + 511) / 512), 2), dim3(256), 0, S(stream), mem,
                    (u64)share_stride, wires, nbits, (u64)words, out, (u64)rows);
             return;
         }

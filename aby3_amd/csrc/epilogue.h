@@ -168,6 +168,9 @@ __device__ __forceinline__ void trunc_pair_block(u32* lds, const u32* __restrict
     const AesKey& k = *reinterpret_cast<const AesKey*>(reinterpret_cast<const char*>(&kk) + off);
     const u64 w0 = h ? pw0 : nw0;
     const u64 c_first = w0 >> 1, c_last = (w0 + n - 1) >> 1;
+    typedef long long i64x2v __attribute__((ext_vector_type(2)));
+    // 16-byte stores: an even stream offset and 16-byte aligned outputs
+    const bool vec = (w0 & 1) == 0 && (((uintptr_t)R | (uintptr_t)RT0 | (uintptr_t)RT1 | (uintptr_t)z) & 15) == 0;
     const u64 per = (u64)nblocks * (blockDim.x >> 1);  // threads per stream
     // two counters per step (c, c + per), as k_aes_ctr
     for (u64 c = c_first + ((u64)bid * (blockDim.x >> 7) + (wave >> 1)) * 64 + lane; c <= c_last; c += 2 * per) {
@@ -181,18 +184,37 @@ __device__ __forceinline__ void trunc_pair_block(u32* lds, const u32* __restrict
             w[0] = lo[0], w[1] = hi[0], w[2] = lo[1], w[3] = hi[1];
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const u64 j = 2 * (c + (q >> 1) * per) + (q & 1);
-            if (j < w0 || j - w0 >= n) continue;
+        for (int p2 = 0; p2 < 2; ++p2) {
+            // the block's two words are elements i, i + 1: one 16-byte store
+            // per output when both exist and the stream offset is even
+            const u64 j = 2 * (c + p2 * per);
             const u64 i = j - w0;
-            const i64 t = (i64)w[q];
-            if (h) {
-                RT1[i] = t >> (d + 2);
-            } else {
-                const i64 r = t >> 2;
-                if (R) R[i] = r;
-                if (z) z[i] = (i64)(src(i) - (u64)r);
-                RT0[i] = t >> (d + 2);
+            if (vec && j >= w0 && i + 1 < n) {
+                const i64 t0 = (i64)w[2 * p2], t1 = (i64)w[2 * p2 + 1];
+                if (h) {
+                    *reinterpret_cast<i64x2v*>(RT1 + i) = i64x2v{t0 >> (d + 2), t1 >> (d + 2)};
+                } else {
+                    const i64 r0 = t0 >> 2, r1 = t1 >> 2;
+                    if (R) *reinterpret_cast<i64x2v*>(R + i) = i64x2v{r0, r1};
+                    if (z) *reinterpret_cast<i64x2v*>(z + i) = i64x2v{(i64)(src(i) - (u64)r0), (i64)(src(i + 1) - (u64)r1)};
+                    *reinterpret_cast<i64x2v*>(RT0 + i) = i64x2v{t0 >> (d + 2), t1 >> (d + 2)};
+                }
+                continue;
+            }
+#pragma unroll
+            for (int q = 2 * p2; q < 2 * p2 + 2; ++q) {
+                const u64 jq = 2 * (c + (q >> 1) * per) + (q & 1);
+                if (jq < w0 || jq - w0 >= n) continue;
+                const u64 iq = jq - w0;
+                const i64 t = (i64)w[q];
+                if (h) {
+                    RT1[iq] = t >> (d + 2);
+                } else {
+                    const i64 r = t >> 2;
+                    if (R) R[iq] = r;
+                    if (z) z[iq] = (i64)(src(iq) - (u64)r);
+                    RT0[iq] = t >> (d + 2);
+                }
             }
         }
     }

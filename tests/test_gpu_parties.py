@@ -29,17 +29,25 @@ def run_parties(job, params, steps, tag, timeout=150, lag_ms=0, layout=1):
         penv = dict(env, ABY3_TEST_LAG_MS=str(lag_ms)) if party == 0 and lag_ms else env
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "party_worker.py"), *a],
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=penv))
-    outs = []
+    res = []
     try:
         for p in procs:
-            o, e = p.communicate(timeout=timeout)
-            assert p.returncode == 0, f"party exited {p.returncode}: {e[-3000:]}"
-            outs.append(json.loads(o.strip().splitlines()[-1]))
+            try:
+                o, e = p.communicate(timeout=timeout)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                o, e = p.communicate()
+            res.append((p.returncode, o, e))
     finally:
         for p in procs:
             if p.poll() is None:
                 p.kill()
-    return outs
+    # every party's exit and stderr tail on a failure: a party that waits out
+    # its link timeout is usually the symptom, the cause is in a peer's log
+    if any(rc != 0 for rc, _, _ in res):
+        report = "\n".join(f"--- party {i} exited {rc}:\n{e[-2000:]}" for i, (rc, _, e) in enumerate(res))
+        raise AssertionError("a party failed\n" + report)
+    return [json.loads(o.strip().splitlines()[-1]) for _, o, _ in res]
 
 
 def colocated_digests(job, params, steps):

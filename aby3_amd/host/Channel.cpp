@@ -85,8 +85,9 @@ struct LinkSlot {
 // in-kernel hand-offs: messages of at most kHandoffMaxChunks chunks (128 Ki
 // rows), or of at most kHandoffChunks chunks (1 Mi rows) from a light
 // producer -- and only within the device's residency rule
-// (handoffResidencyOk: with the level kernel at 94 VGPRs, 5 workgroups of the
-// large form per CU, two 512-chunk consumers hold 206 of 256 CUs on MI355X).
+// (handoffResidencyOk: with the hand-off level kernel at 74 VGPRs, 6
+// workgroups of the large form per CU, two 512-chunk consumers hold 172 of
+// 256 CUs on MI355X).
 constexpr u64 kHandoffMaxChunks = 64;
 constexpr u64 kHandoffChunks = 512;  // flags per direction
 // A producing launch of at most this many HBM bytes is light: its consumer's
@@ -95,6 +96,11 @@ constexpr u64 kHandoffChunks = 512;  // flags per direction
 // large message 0.386-0.399 ms / 80.3-80.8 ms; in-kernel from producers of
 // <= 2 MiB the same; <= 8 MiB 0.376-0.382 / 75.6-76.6; <= 32 MiB
 // 0.363-0.368 / 72.1-73.6; every level in-kernel 0.376-0.384 / 75.7-75.9.
+// The bound is also a safety margin: with the 16-byte level kernels (round
+// 5) every level in-kernel ended a 300-step C3 run with 55 hand-off
+// timeouts, the three parties' heavy first levels and their consumers
+// holding the device; <= 64 MiB measured 2-3 % faster in one sample and is
+// not taken without a safety argument that covers heavy producers.
 constexpr u64 kHandoffLightBytes = (u64)32 << 20;
 
 // how long a receive polls before it sleeps on the condition variable

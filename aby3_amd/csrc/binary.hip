@@ -760,10 +760,21 @@ __global__ void __launch_bounds__(256) k_bits_to_wires_map(const i64* __restrict
 #pragma unroll
     for (u32 k = 0; k < kWaveWords; ++k) tile[lane * kTilePitch + wave * kWaveWords + k] = vv[k];
     __syncthreads();
-    for (u32 idx = threadIdx.x; idx < 64 * kTileWords; idx += 256) {
-        const u32 b = idx / kTileWords, wl = idx % kTileWords;
+    // two words a thread: one 16-byte store when both are in the row and aligned
+    for (u32 idx = threadIdx.x; idx < 32 * kTileWords; idx += 256) {
+        const u32 b = idx / (kTileWords / 2), wl = 2 * (idx % (kTileWords / 2));
         const u64 bit = c * 64 + b;
-        if (bit < nbits && w0 + wl < words) wrows[bit * words + w0 + wl] = tile[b * kTilePitch + wl];
+        if (bit < nbits && w0 + wl < words) {
+            u64* dst = wrows + bit * words + w0 + wl;
+            const u64 v0 = tile[b * kTilePitch + wl], v1 = tile[b * kTilePitch + wl + 1];
+            const bool both = w0 + wl + 1 < words;
+            if (both && ((uintptr_t)dst & 15) == 0) {
+                *reinterpret_cast<u64x2*>(dst) = u64x2{v0, v1};
+            } else {
+                dst[0] = v0;
+                if (both) dst[1] = v1;
+            }
+        }
     }
 }
 
@@ -781,17 +792,28 @@ __global__ void __launch_bounds__(256) k_wires_to_bits_map(const u64* __restrict
     const u64 rw = (rows + 63) / 64;
     const u64 tilesPerCol = (rw + kTileWords - 1) / kTileWords;
     const u64 c = blockIdx.x / tilesPerCol, w0 = (blockIdx.x % tilesPerCol) * kTileWords;
-    u64 vv[kWaveWords];  // 64 x kTileWords words over 256 threads
+    u64 vv[kWaveWords];  // 64 x kTileWords words over 256 threads, two words a thread per load (16 bytes)
 #pragma unroll
-    for (u32 j = 0; j < kWaveWords; ++j) {
-        const u32 idx = threadIdx.x + 256 * j, b = idx / kTileWords, wl = idx % kTileWords;
+    for (u32 j = 0; j < kWaveWords / 2; ++j) {
+        const u32 idx = threadIdx.x + 256 * j, b = idx / (kTileWords / 2), wl = 2 * (idx % (kTileWords / 2));
         const u64 bit = c * 64 + b;
-        vv[j] = (bit < nbits && w0 + wl < rw) ? mem[(u64)wires[bit] * words + w0 + wl] : 0;
+        u64x2 v = u64x2{0, 0};
+        if (bit < nbits && w0 + wl < rw) {
+            const u64* src = mem + (u64)wires[bit] * words + w0 + wl;
+            const bool both = w0 + wl + 1 < rw;
+            if (both && ((uintptr_t)src & 15) == 0)
+                v = *reinterpret_cast<const u64x2*>(src);
+            else
+                v = u64x2{src[0], both ? src[1] : 0};
+        }
+        vv[2 * j] = v.x;
+        vv[2 * j + 1] = v.y;
     }
 #pragma unroll
-    for (u32 j = 0; j < kWaveWords; ++j) {
-        const u32 idx = threadIdx.x + 256 * j;
-        tile[(idx / kTileWords) * kTilePitch + idx % kTileWords] = vv[j];
+    for (u32 j = 0; j < kWaveWords / 2; ++j) {
+        const u32 idx = threadIdx.x + 256 * j, b = idx / (kTileWords / 2), wl = 2 * (idx % (kTileWords / 2));
+        tile[b * kTilePitch + wl] = vv[2 * j];
+        tile[b * kTilePitch + wl + 1] = vv[2 * j + 1];
     }
     __syncthreads();
     const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;

@@ -316,16 +316,20 @@ def _map_rows(first, start, step, per_rep, rep_stride, n):
     return start + (q // per_rep) * rep_stride + (q % per_rep) * step
 
 
-@pytest.mark.parametrize("in_rows,rows,mp", [
-    (4096, 2048, (0, 0, 1, 1024, 2048)),      # merge round 0: first halves of 2 lists of 1024
-    (4096, 1500, (0, 1, 2, 1500, 4096)),      # odd slots, one rep
-    (5000, 1999, (17, 3, 2, 7, 16)),          # chunk offset, short reps
-    (300, 300, None),                          # explicit index list (a permutation)
-    (2049, 1, (0, 2048, 1, 1, 0)),
+@pytest.mark.parametrize("in_rows,rows,mp,padded", [
+    (4096, 2048, (0, 0, 1, 1024, 2048), True),      # merge round 0: first halves of 2 lists of 1024
+    (4096, 1500, (0, 1, 2, 1500, 4096), True),      # odd slots, one rep
+    (5000, 1999, (17, 3, 2, 7, 16), True),          # chunk offset, short reps
+    (300, 300, None, True),                          # explicit index list (a permutation)
+    (2049, 1, (0, 2048, 1, 1, 0), True),
+    (5000, 150, (0, 7, 3, 150, 5000), False),       # 3 words a wire: odd rows of words, unaligned pairs
+    (5000, 190, (1, 0, 1, 95, 200), False),
 ])
-def test_transposes_mapped(gpu, in_rows, rows, mp):
+def test_transposes_mapped(gpu, in_rows, rows, mp, padded):
     """bits_to_wires_map / wires_to_bits_map (the merge rounds' fused gather
-    and scatter) against numpy; the scatter leaves unmapped rows untouched."""
+    and scatter) against numpy; the scatter leaves unmapped rows untouched.
+    Unpadded word counts (odd, so every other wire row starts 8 bytes off a
+    16-byte boundary) take the kernels' one-word paths."""
     import torch
 
     x = rnd(in_rows + rows, 2 * in_rows).reshape(2, in_rows, 1)
@@ -336,7 +340,7 @@ def test_transposes_mapped(gpu, in_rows, rows, mp):
     else:
         src = _map_rows(*mp, rows)
         rm = nt.RowMap(*mp, None)
-    words = 32 * ((rows + 2047) // 2048)
+    words = 32 * ((rows + 2047) // 2048) if padded else (rows + 63) // 64
     mem = empty(2 * 64 * words)
     gpu.bits_to_wires_map(P(dev(x)), in_rows, 1, 64, ctypes.byref(rm), rows, P(mem), 64 * words, words, None)
     m = host(mem).view(np.uint64).reshape(2, 64, words)

@@ -210,8 +210,8 @@ struct Pipe {
     }
 
     // readiness of a device payload enqueued so far on `gpu`'s stream
-    void signalReady(Msg& m, Gpu& gpu, Event* fallback) {
-        if (signalDevice >= 0 && signalDevice == gpu.device()) {
+    void signalReady(Msg& m, Gpu& gpu, Event* fallback, bool useWord = true) {
+        if (useWord && signalDevice >= 0 && signalDevice == gpu.device()) {
             if (!word) throw std::runtime_error("channel: signal word not allocated at ring construction");
             m.sigWord = word;
             m.sigValue = ++devSeq;
@@ -617,7 +617,7 @@ std::shared_ptr<DeviceBuffer> RecvFuture::getShared() const {
     return st.out;
 }
 
-void Channel::asyncSendShared(std::shared_ptr<DeviceBuffer> buf, size_t bytes, Gpu& gpu) {
+void Channel::sendShared(std::shared_ptr<DeviceBuffer> buf, size_t bytes, Gpu& gpu, bool word) {
     if (!mOut) throw std::runtime_error("channel not connected");
     if (!buf || buf->bytes() < bytes) throw std::runtime_error("asyncSendShared: buffer smaller than the message");
     GPU_CALL(aby3g_set_device(gpu.device()));
@@ -630,9 +630,17 @@ void Channel::asyncSendShared(std::shared_ptr<DeviceBuffer> buf, size_t bytes, G
     m.device = true;
     m.bytes = bytes;
     m.shared = std::move(buf);
-    if (mOut->signalDevice != gpu.device()) m.ready = std::make_shared<Event>();
-    mOut->signalReady(m, gpu, m.ready.get());
+    if (!word || mOut->signalDevice != gpu.device()) m.ready = std::make_shared<Event>();
+    mOut->signalReady(m, gpu, m.ready.get(), word);
     mOut->push(std::move(m));
+}
+
+void Channel::asyncSendShared(std::shared_ptr<DeviceBuffer> buf, size_t bytes, Gpu& gpu) {
+    sendShared(std::move(buf), bytes, gpu, true);
+}
+
+void Channel::asyncSendSharedEvent(std::shared_ptr<DeviceBuffer> buf, size_t bytes, Gpu& gpu) {
+    sendShared(std::move(buf), bytes, gpu, false);
 }
 
 aby3g_handoff Channel::handoffPost(Gpu& gpu, u64 rows, u64 producerBytes, const void* payload) {

@@ -75,6 +75,13 @@ public:
     // the sender's stream at send time. The receiver reads it in place (over
     // xGMI when on another GPU) and fences it when done.
     void asyncSendShared(std::shared_ptr<DeviceBuffer> buf, size_t bytes, Gpu& gpu);
+    // the same, readiness signalled by an event record even on one device (no
+    // stream-write / stream-wait blit kernels on the queues): for messages
+    // whose receiver waits long anyway (asyncMul's truncation z, behind the
+    // peers' share GEMMs), where it measured as fast as the signal word
+    // (C2 0.2548-0.2566 vs 0.2568-0.2575 ms); the binary engine's level
+    // messages keep the signal word (C3 0.313-0.315 vs 0.323 ms with events)
+    void asyncSendSharedEvent(std::shared_ptr<DeviceBuffer> buf, size_t bytes, Gpu& gpu);
     RecvFuture asyncRecvShared(size_t bytes, Gpu& gpu);
     // In-kernel hand-off of the next zero-copy message (co-located parties on
     // one device whose ring was made with kernel hand-offs): the flags and
@@ -118,6 +125,7 @@ public:
     bool connected() const { return mOut && mIn; }
 
 private:
+    void sendShared(std::shared_ptr<DeviceBuffer> buf, size_t bytes, Gpu& gpu, bool word);
     std::shared_ptr<Pipe> mOut, mIn;
 };
 

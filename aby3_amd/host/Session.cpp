@@ -520,6 +520,28 @@ struct Session {
         turnCv.notify_all();
     }
 
+    // One party per process, at close: drain this party's streams and
+    // exchange a token with both neighbours before anything is torn down, so
+    // that no process frees (or exits with) a staging slot or mailbox a peer
+    // is still to open or read. A run that failed skips it (a peer may be gone).
+    void leaveTogether(PartyCtx& p) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            if (!err.empty()) return;
+        }
+        try {
+            p.rt.gpu().sync();
+            const u64 token = 0xC105Eull;
+            u64 a = 0, b = 0;
+            p.rt.mComm.mNext.asyncSendCopy(token);
+            p.rt.mComm.mPrev.asyncSendCopy(token);
+            p.rt.mComm.mNext.recv(a);
+            p.rt.mComm.mPrev.recv(b);
+        } catch (const std::exception&) {
+            // a peer that closed on an error: nothing left to wait for
+        }
+    }
+
     void worker(int i, int device, int probe) {
         PartyCtx p;
         u64 seen = 0;
@@ -590,7 +612,10 @@ struct Session {
                 c = cmd;
                 n = steps;
             }
-            if (c == 2) return;
+            if (c == 2) {
+                if (locals.size() == 1) leaveTogether(p);
+                return;
+            }
             try {
                 if (!err.empty()) throw std::runtime_error("session failed earlier");
                 if (c == 1) {

@@ -149,8 +149,8 @@ Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, const si64Matrix& A, const si64Matri
             // reveal z to parties 0 and 1 (:681-684)
             const u64 p = self.getRuntime().mPartyIdx;
             const u64 next = (p + 1) % 3, prev = (p + 2) % 3;
-            if (next < 2) comm.mNext.asyncSendShared(z, bytes, g);
-            if (prev < 2) comm.mPrev.asyncSendShared(z, bytes, g);
+            if (next < 2) comm.mNext.asyncSendSharedEvent(z, bytes, g);
+            if (prev < 2) comm.mPrev.asyncSendSharedEvent(z, bytes, g);
             if (p < 2) {
                 auto fu0 = comm.mNext.asyncRecvShared(bytes, g);
                 auto fu1 = comm.mPrev.asyncRecvShared(bytes, g);

@@ -136,6 +136,17 @@ struct FusedLr {
         GPU_CALL(aby3g_ipc_open(&hp, &f->mapped[1]));
         f->nextBox = f->mapped[0];
         f->prevBox = f->mapped[1];
+        // Every party's earlier work (the setup's copies in and out of the
+        // peers' staging slots) drained before any party's first fused launch,
+        // whose workgroups spin on the peers' mailboxes: a three-process run
+        // once ended its first iteration with every party's waits timed out.
+        g.sync();
+        const u64 token = 1;
+        u64 tn = 0, tp = 0;
+        comm.mNext.asyncSendCopy(token);
+        comm.mPrev.asyncSendCopy(token);
+        comm.mNext.recv(tn);
+        comm.mPrev.recv(tp);
         return f;
     }
 

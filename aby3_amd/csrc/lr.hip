@@ -647,6 +647,7 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
     const u32* andWires = cir.and_wires;
     const aby3g_lr_level* levelsL = cir.levels;
     const u32* batchEndsL = cir.batch_ends;
+    const aby3g_lr_gate_ext* extL = cir.ext;
     if (kLds) {
         u32* gl = reinterpret_cast<u32*>(zmw + (u64)cir.nand * W);
         const u32* gg = reinterpret_cast<const u32*>(cir.gates);
@@ -667,6 +668,12 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
         for (u32 i = threadIdx.x; i < nbatches; i += kLrThreads) be[i] = cir.batch_ends[i];
         levelsL = reinterpret_cast<const aby3g_lr_level*>(lvl);
         batchEndsL = be;
+        if (cir.ext) {  // the folded gates' operand terms (16 bytes an entry)
+            u32* ex = be + ((nbatches + 3) & ~3u);
+            const u32* eg = reinterpret_cast<const u32*>(cir.ext);
+            for (u32 i = threadIdx.x; i < cir.next * (u32)(sizeof(aby3g_lr_gate_ext) / 4); i += kLrThreads) ex[i] = eg[i];
+            extL = reinterpret_cast<const aby3g_lr_gate_ext*>(ex);
+        }
         // read from the levels on, after phase 1's barriers
     }
 
@@ -779,11 +786,31 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
             const u32 end = batchEndsL[lvr.batch_off + b];
             for (u32 q = tid; q < (end - begin) * W32; q += kLrThreads) {
                 const u32 gq = wdiv(q), w = q - gq * W32;
+                // a gate folded into the first batch has its operands' XOR terms
+                // in ext; read beside the descriptor (one LDS round trip for both)
+                const bool folded = extL && begin + gq >= lvr.fused_first;
+                aby3g_lr_gate_ext e;
+                if (folded) e = extL[lvr.ext_off + begin + gq - lvr.fused_first];
                 const aby3g_gate g = gates[lvr.first_gate + begin + gq];
                 const bool unary = g.type == ABY3G_GATE_COPY || g.type == ABY3G_GATE_INV;
                 const u32 in1 = unary ? g.in0 : g.in1;
-                const u64 x0 = mem[(u64)g.in0 * W + w], x1 = mem[WS + (u64)g.in0 * W + w];
-                const u64 y0 = mem[(u64)in1 * W + w], y1 = mem[WS + (u64)in1 * W + w];
+                u64 x0 = mem[(u64)g.in0 * W + w], x1 = mem[WS + (u64)g.in0 * W + w];
+                u64 y0 = mem[(u64)in1 * W + w], y1 = mem[WS + (u64)in1 * W + w];
+                if (folded) {
+#pragma unroll
+                    for (int t = 0; t < 3; ++t) {
+                        if (e.x[t] != 0xFFFF) {
+                            x0 ^= mem[(u64)e.x[t] * W + w];
+                            x1 ^= mem[WS + (u64)e.x[t] * W + w];
+                        }
+                        if (e.y[t] != 0xFFFF) {
+                            y0 ^= mem[(u64)e.y[t] * W + w];
+                            y1 ^= mem[WS + (u64)e.y[t] * W + w];
+                        }
+                    }
+                    if (e.flags & 1) x0 = ~x0, x1 = ~x1;
+                    if (e.flags & 2) y0 = ~y0, y1 = ~y1;
+                }
                 if (gate_is_and(g.type)) {
                     const u64 r = gate_and_share(g.type, x0, x1, y0, y1) ^ zm[(u64)g.z_row * W + w];
                     mem[(u64)g.out * W + w] = r;
@@ -1078,6 +1105,7 @@ int aby3g_lr_iteration(const aby3g_lr_iter* it, aby3g_stream stream) {
         ABY3G_REQUIRE(it->X && it->Y && it->w && it->batch && it->scratch && it->mailbox && it->next_mailbox &&
                           it->prev_mailbox && it->cir.gates && it->cir.levels,
                       "null pointer");
+        ABY3G_REQUIRE(!it->cir.ext || it->cir.wires < 0xFFFF, "folded gate terms address wires by 16 bits");
         ABY3G_REQUIRE(it->t1_next_off % 8 == 0 && it->t1_prev_off % 8 == 0 && it->t2_next_off % 8 == 0 &&
                           it->t2_prev_off % 8 == 0 && it->ot_next_off % 8 == 0 && it->ot_prev_off % 8 == 0,
                       "stream offsets must be multiples of 8");
@@ -1099,10 +1127,12 @@ int aby3g_lr_iteration(const aby3g_lr_iter* it, aby3g_stream stream) {
             K.mn2 = expand_key(it->next_rand.mask_next);
         }
         const Layout L(it->B, it->d, it->cir);
-        // engine memory, masks, gates, AND wires (padded to 4), level table, batch ends (<= ngates)
+        // engine memory, masks, gates, AND wires (padded to 4), level table, batch ends (<= ngates, padded
+        // to 4), folded gates' operand terms
         const u64 dynBytes = (2 * (u64)it->cir.wires + it->cir.nand) * L.W * 8 +
                              (u64)it->cir.ngates * sizeof(aby3g_gate) + 4 * (((u64)it->cir.nand + 3) & ~3ull) +
-                             (u64)it->cir.nlevels * sizeof(aby3g_lr_level) + 4 * (u64)it->cir.ngates;
+                             (u64)it->cir.nlevels * sizeof(aby3g_lr_level) + 4 * (((u64)it->cir.ngates + 3) & ~3ull) +
+                             (it->cir.ext ? (u64)it->cir.next * sizeof(aby3g_lr_gate_ext) : 0);
         const int inLds = dynBytes <= kLrDynLdsMax;
         static const bool attr = [] {  // dynamic LDS beyond the default limit, once per process
             return hipFuncSetAttribute((const void*)k_lr_iter, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -1,5 +1,7 @@
 #include "aby3ML.h"
 #include <algorithm>
+#include <iterator>
+#include <unordered_map>
 #include <cmath>
 #include <cstring>
 #include <random>
@@ -170,14 +172,24 @@ struct FusedLr {
         }
         std::vector<u32> ends, andWires;
         std::vector<aby3g_lr_level> levels;
+        std::vector<aby3g_lr_gate_ext> ext;
+        const bool fold = foldLevels(*c, gates, ext);
         size_t gi = 0;
         for (size_t L = 0; L < c->mLevelCounts.size(); ++L) {
             aby3g_lr_level lv{};
             const auto& batches = c->mLevelBatches[L];
             lv.first_gate = batches.empty() ? 0 : batches.front().begin;
-            lv.nbatch = (u32)batches.size();
             lv.batch_off = (u32)ends.size();
-            for (const auto& b : batches) ends.push_back(b.begin + b.count - lv.first_gate);
+            if (fold && !batches.empty()) {
+                // one batch: the later batches' gates folded into the first (foldLevels)
+                lv.nbatch = 1;
+                ends.push_back(batches.back().begin + batches.back().count - lv.first_gate);
+                lv.fused_first = batches.front().count;
+                lv.ext_off = (u32)foldOff[L];
+            } else {
+                lv.nbatch = (u32)batches.size();
+                for (const auto& b : batches) ends.push_back(b.begin + b.count - lv.first_gate);
+            }
             lv.and_wire_off = (u32)andWires.size();
             for (u32 k = 0; k < c->mLevelCounts[L]; ++k, ++gi)
                 if (isAndType(c->mLevelGates[gi].type)) andWires.push_back(c->mLevelGates[gi].out);
@@ -196,6 +208,7 @@ struct FusedLr {
         const size_t oE = put(ends.data(), ends.size() * 4);
         const size_t oL = put(levels.data(), levels.size() * sizeof(aby3g_lr_level));
         const size_t oA = put(andWires.data(), andWires.size() * 4);
+        const size_t oX = put(ext.data(), ext.size() * sizeof(aby3g_lr_gate_ext));
         circuit.reset(g, host.size());
         toDevice(circuit.data(), host.data(), host.size(), g);
         const u8* base = circuit.as<u8>();
@@ -211,6 +224,77 @@ struct FusedLr {
         cir.batch_ends = reinterpret_cast<const u32*>(base + oE);
         cir.levels = reinterpret_cast<const aby3g_lr_level*>(base + oL);
         cir.and_wires = reinterpret_cast<const u32*>(base + oA);
+        cir.ext = fold && !ext.empty() ? reinterpret_cast<const aby3g_lr_gate_ext*>(base + oX) : nullptr;
+        cir.next = fold ? (u32)ext.size() : 0;
+    }
+
+    // Folds every level's later gate batches into its first: the local
+    // XOR / NXOR / INV / COPY gates of the level (whose outputs the later
+    // batches read) are substituted into the later gates' operands, each
+    // operand then the XOR of at most four wires available when the level
+    // starts, optionally inverted (aby3g_lr_gate_ext). The values, and so the
+    // shares, are the same as evaluating batch after batch; a level then takes
+    // one workgroup barrier instead of one per batch. Gates keep their batch
+    // order (the first batch, then the folded ones) and their z / send rows.
+    // Returns false (nothing folded) when an operand would need more terms or
+    // reduces to a constant.
+    std::vector<size_t> foldOff;  // per level: its first ext entry
+    bool foldLevels(const BetaCircuit& c, std::vector<aby3g_gate>& gates, std::vector<aby3g_lr_gate_ext>& ext) {
+        if (c.mWireCount >= 0xFFFF) return false;
+        struct Expr {
+            std::vector<u32> t;  // XOR terms, sorted, no repeats
+            bool inv = false;
+        };
+        auto xorInto = [](Expr& a, const Expr& b) {
+            std::vector<u32> r;
+            std::set_symmetric_difference(a.t.begin(), a.t.end(), b.t.begin(), b.t.end(), std::back_inserter(r));
+            a.t.swap(r);
+            a.inv ^= b.inv;
+        };
+        std::vector<aby3g_gate> out = gates;
+        std::vector<aby3g_lr_gate_ext> ex;
+        std::vector<size_t> offs;
+        for (size_t L = 0; L < c.mLevelCounts.size(); ++L) {
+            offs.push_back(ex.size());
+            const auto& batches = c.mLevelBatches[L];
+            std::unordered_map<u32, Expr> local;  // outputs of this level's local gates
+            auto expr = [&](u32 w) {
+                auto it = local.find(w);
+                if (it != local.end()) return it->second;
+                Expr e;
+                e.t = {w};
+                return e;
+            };
+            for (size_t b = 0; b < batches.size(); ++b)
+                for (u32 k = batches[b].begin; k < batches[b].begin + batches[b].count; ++k) {
+                    const aby3g_gate& gt = gates[k];
+                    const bool unary = gt.type == ABY3G_GATE_COPY || gt.type == ABY3G_GATE_INV;
+                    Expr x = expr(gt.in0), y = unary ? x : expr(gt.in1);
+                    if (b > 0) {
+                        for (const Expr* e : {&x, &y})
+                            if (e->t.empty() || e->t.size() > 4) return false;
+                        aby3g_lr_gate_ext e{};
+                        for (int i = 0; i < 3; ++i) {
+                            e.x[i] = (uint16_t)(i + 1 < (int)x.t.size() ? x.t[(size_t)i + 1] : 0xFFFF);
+                            e.y[i] = (uint16_t)(i + 1 < (int)y.t.size() ? y.t[(size_t)i + 1] : 0xFFFF);
+                        }
+                        e.flags = (uint16_t)((x.inv ? 1 : 0) | (y.inv ? 2 : 0));
+                        out[k].in0 = x.t[0];
+                        out[k].in1 = y.t[0];
+                        ex.push_back(e);
+                    }
+                    if (!isAndType((GateType)gt.type)) {  // a local gate: its output as an expression
+                        Expr o = x;
+                        if (gt.type == ABY3G_GATE_XOR || gt.type == ABY3G_GATE_NXOR) xorInto(o, y);
+                        if (gt.type == ABY3G_GATE_NXOR || gt.type == ABY3G_GATE_INV) o.inv = !o.inv;
+                        local[gt.out] = o;
+                    }
+                }
+        }
+        gates.swap(out);
+        ext.swap(ex);
+        foldOff.swap(offs);
+        return true;
     }
 
     // One iteration's randomness, in the order the op-by-op path takes it.

@@ -539,8 +539,18 @@ typedef struct {
     uint32_t batch_off;    /* into batch_ends (relative to first_gate) */
     uint32_t nand;         /* AND-type gates = send rows of the level */
     uint32_t and_wire_off; /* into and_wires: the level's AND outputs in send-row order */
-    uint32_t pad[3];
+    uint32_t fused_first;  /* gates of the level from this index on have an ext entry (ext != NULL) */
+    uint32_t ext_off;      /* into ext: the entry of gate fused_first */
+    uint32_t pad;
 } aby3g_lr_level;
+/* Operands of a gate folded into its level's first batch: operand x is the
+ * XOR of in0 and the wires x[0..2] (0xFFFF: none), inverted (both shares)
+ * when flags bit 0 is set; y likewise with in1, y[] and bit 1 -- the local
+ * XOR / NXOR / INV gates of the level's earlier batches substituted. */
+typedef struct {
+    uint16_t x[3], y[3];
+    uint16_t flags, pad;
+} aby3g_lr_gate_ext;
 typedef struct {
     uint32_t nlevels, wires, nand, ngates;
     uint32_t in_wire[3];  /* first wires of the 64-bit inputs aa_0, aa_1, b */
@@ -549,6 +559,9 @@ typedef struct {
     const uint32_t* batch_ends;
     const aby3g_lr_level* levels;
     const uint32_t* and_wires;
+    const aby3g_lr_gate_ext* ext; /* optional (NULL: no folded gates) */
+    uint32_t next;                /* entries of ext */
+    uint32_t pad;
 } aby3g_lr_circuit;
 
 /* The positions of one iteration's randomness (the same-named fields of

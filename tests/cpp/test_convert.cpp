@@ -160,7 +160,7 @@ static void bitInjection(u64 rows, u64 bits, bool twoRounds) {
     check(orc::revealInt(Y1).v == orc::revealInt(Y2).v, "oracle calls agree");
     for (u64 i = 0; i < rows; ++i)
         for (u64 j = 0; j < bits; ++j)
-            check(revealed[i * bits + j] == (((u64)x(i, j / 64) >> (j % 64)) & 1), "bitInjection revealed bit");
+            check((u64)revealed[i * bits + j] == (((u64)x(i, j / 64) >> (j % 64)) & 1), "bitInjection revealed bit");
 }
 
 // toBinaryMatrix of an odd number of words advances only P0's prev / P2's

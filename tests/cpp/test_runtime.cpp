@@ -99,7 +99,7 @@ static void reentrancy_test() {
     CommPkg comm;
     rt.init(0, comm, -1);
     bool threw = false;
-    auto t = rt.noDependencies().then([&](CommPkg&, Sh3Task self) {
+    rt.noDependencies().then([&](CommPkg&, Sh3Task self) {
         auto inner = self.then([](CommPkg&, Sh3Task) {});
         try {
             inner.get();  // Sh3Runtime.cpp:274-275 forbids this

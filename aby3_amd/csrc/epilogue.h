@@ -258,7 +258,11 @@ void launch_finish_trunc(Src src, const aby3g_trunc_streams& ts, u64 n, unsigned
     ABY3G_REQUIRE(d < 62, "shift too large");
     if (!n) return;
     const AesKeyPair kk{{expand_key(ts.next_seed), expand_key(ts.prev_seed)}};
-    u32 grid = aes_grid(n / 2 + 1, kEpiBlock / 2);
+    // one workgroup per CU at most (half aes_grid's cap): half the 64 KiB
+    // table fills, and the pass shares the chip with the co-located parties'
+    // share GEMMs (C2 0.2527-0.2547 against 0.2546-0.2557 ms with 512, same
+    // box; 128 measured 0.265)
+    const u32 grid = std::min<u32>(aes_grid(n / 2 + 1, kEpiBlock / 2), 256);
     launch(PROBE_EPILOGUE, k_finish_trunc<Src>, dim3(grid), dim3(kEpiBlock), 0, s, aes_table(), src, kk,
            ts.next_off / 8, ts.prev_off / 8, n, (u32)d, R, RT0, RT1, z);
 }

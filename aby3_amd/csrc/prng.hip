@@ -225,8 +225,13 @@ void share_draws_launch(int kind, const u8* kprev, const u8* knext, u64 base, u6
     if (!n) return;
     const AesKeyPair kk{{expand_key(kprev), expand_key(knext)}};
     u64 counters = ((base + n - 1) >> 1) - (base >> 1) + 1;
-    launch(family, k_share_draws, dim3(aes_grid(counters, kBlock)), dim3(kBlock), 0, s, aes_table(), kk, kind, base, n,
-           addend, out0, out1);
+    // at most one workgroup per CU: the draws run beside other work (a
+    // circuit's masks beside the previous comparison's latency-bound levels),
+    // and fewer 64 KiB-LDS workgroups leave the levels more CUs (C3
+    // 0.2999-0.3024 against 0.3088-0.3115 ms with aes_grid's 512, same box;
+    // 128 measured 0.344-0.352)
+    const u32 grid = std::min<u32>(aes_grid(counters, kBlock), 256);
+    launch(family, k_share_draws, dim3(grid), dim3(kBlock), 0, s, aes_table(), kk, kind, base, n, addend, out0, out1);
 }
 
 }  // namespace aby3g

@@ -179,12 +179,23 @@ __device__ __forceinline__ void digit_group(bool valid, u64 gid, u32 t, u8* img,
         const u32 row = t >> 3, kq = t & 7;
         const u64 m = r0 + row;
         u64 v0[4], v1[4];
+        const u64 kk = k0 + 4 * kq;
+        if (valid && m < M && kk + 4 <= K && K % 2 == 0 && (((u64)A0 | (u64)A1) & 15) == 0) {
+            // the row's 4 values as two 16-byte loads per share
+            typedef u64 u64v2 __attribute__((ext_vector_type(2)));
+            const u64v2* p0 = reinterpret_cast<const u64v2*>(A0 + m * K + kk);
+            const u64v2* p1 = reinterpret_cast<const u64v2*>(A1 + m * K + kk);
+            const u64v2 a0 = p0[0], a1 = p0[1], b0 = p1[0], b1 = p1[1];
+            v0[0] = a0.x, v0[1] = a0.y, v0[2] = a1.x, v0[3] = a1.y;
+            v1[0] = b0.x, v1[1] = b0.y, v1[2] = b1.x, v1[3] = b1.y;
+        } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const u64 k = k0 + 4 * kq + j;
-            const bool in = valid && m < M && k < K;
-            v0[j] = in ? (u64)A0[m * K + k] : 0;
-            v1[j] = in ? (u64)A1[m * K + k] : 0;
+            for (int j = 0; j < 4; ++j) {
+                const u64 k = kk + j;
+                const bool in = valid && m < M && k < K;
+                v0[j] = in ? (u64)A0[m * K + k] : 0;
+                v1[j] = in ? (u64)A1[m * K + k] : 0;
+            }
         }
         u32 w0[8], w1[8];
         digit_words(v0, w0);

@@ -43,8 +43,14 @@ struct ApiClock {
     }
 };
 
+// diagnostics: the names of the process's recent C-ABI calls (a ring of 32),
+// so that an asynchronous device fault that surfaces in a later call can be
+// traced to the work enqueued just before it (aby3g_recent_calls)
+void note_call(const char* name);
+
 template <class F>
-int guarded(F&& f) {
+int guarded_at(const char* name, F&& f) {
+    note_call(name);
     ApiClock clock;
     try {
         f();
@@ -57,6 +63,9 @@ int guarded(F&& f) {
         return ABY3G_EINVAL;
     }
 }
+// every C-ABI entry point reads `return guarded([&] { ... });`: the entry's
+// own name goes into the ring
+#define guarded(...) guarded_at(__func__, __VA_ARGS__)
 
 // ----------------------------------------------------------------- probe --
 enum ProbeFamily { PROBE_GEMM = 0, PROBE_EPILOGUE = 1, PROBE_BINARY = 2, PROBE_AES = 3, PROBE_OTHER = 4, PROBE_DIGITS = 5 };

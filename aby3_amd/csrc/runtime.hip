@@ -191,6 +191,12 @@ const u32* aes_table() {
     return (u32*)p;
 }
 
+static std::atomic<u64> g_call_n{0};
+static std::atomic<const char*> g_calls[32];
+void note_call(const char* name) {
+    g_calls[g_call_n.fetch_add(1, std::memory_order_relaxed) & 31].store(name, std::memory_order_relaxed);
+}
+
 namespace {
 // dst[0, n) <- src[0, n) in 16-byte pieces (both 16-byte aligned), grid-stride
 __global__ void __launch_bounds__(256) k_copy16(uint4* __restrict__ dst, const uint4* __restrict__ src, u64 n) {
@@ -219,6 +225,20 @@ using namespace aby3g;
 extern "C" {
 
 const char* aby3g_last_error(void) { return t_err.c_str(); }
+int aby3g_recent_calls(char* out, size_t cap) {
+    if (!out || !cap) return ABY3G_EINVAL;
+    std::string r;
+    const u64 n = g_call_n.load(std::memory_order_relaxed);
+    for (u64 k = 0; k < 32 && k < n; ++k) {
+        const char* c = g_calls[(n - 1 - k) & 31].load(std::memory_order_relaxed);
+        if (!c) continue;
+        if (!r.empty()) r += " < ";
+        r += c;
+    }
+    std::strncpy(out, r.c_str(), cap - 1);
+    out[cap - 1] = 0;
+    return ABY3G_OK;
+}
 int aby3g_version(void) { return 1; }
 
 int aby3g_device_count(int* n) {

@@ -1,4 +1,5 @@
 #include "Device.h"
+#include "Link.h"
 #include <mutex>
 #include <vector>
 #include <map>
@@ -19,7 +20,14 @@ size_t sizeClass(size_t bytes) {
 }  // namespace
 
 void gpuCheck(int rc, const char* what) {
-    if (rc != 0) throw std::runtime_error(std::string(what) + ": " + aby3g_last_error());
+    if (rc == 0) return;
+    std::string m = std::string(what) + ": " + aby3g_last_error();
+    if (rc == ABY3G_EHIP) {
+        // an error of the HIP runtime may be a device fault of earlier work
+        char recent[1024];
+        if (aby3g_recent_calls(recent, sizeof recent) == 0 && recent[0]) m += " [recent calls, newest first: " + std::string(recent) + "]";
+    }
+    throw std::runtime_error(m);
 }
 
 // Events are recycled: a protocol round creates several (message readiness,
@@ -120,6 +128,9 @@ void Gpu::bind() {
 void Gpu::sync() {
     GPU_CALL(aby3g_stream_sync(mStream));
     if (mAux) GPU_CALL(aby3g_stream_sync(mAux));
+    // one party per process: a failed peer's waits were released (~0 signal
+    // words, LinkEnd's watchdog), so the stream drained on garbage -- an error
+    if (LinkEnd::failed()) throw std::runtime_error("stream drained after a party failure: " + LinkEnd::failure());
 }
 
 u64* Gpu::waitTicks() {

@@ -54,7 +54,27 @@ public:
 
     static double timeoutS();
 
+    // ---- failing fast (the reference's Channel fails a pending receive when
+    // the peer's session closes) ----
+    // This process failed: every live link's header carries the abort word
+    // (this pid) and the message, and every signal word of every live link is
+    // set to ~0 so that no stream of any party stays parked on a wait this
+    // process will never satisfy. Idempotent; the first message is kept.
+    static void abortAll(const std::string& why);
+    // This process is leaving normally (after the closing token exchange): a
+    // peer that sees it exit does not take that for a failure.
+    static void closeAll();
+    // The first failure seen by this process (its own abort, a peer's abort
+    // word, or a peer process gone without closing), or "" -- once set, every
+    // link wait throws with it and the watchdog keeps the signal words released.
+    static std::string failure();
+    static bool failed();
+
 private:
+    static void releaseWords();
+    static void watchdog();
+    // one watchdog pass: a peer's abort word or a peer gone without closing
+    bool peerFailed(std::string& why) const;
     void waitFor(const char* what, const std::atomic<u64>& w, u64 atLeast) const;
     std::string mName;
     bool mSender;
@@ -65,6 +85,7 @@ private:
     struct Hdr;
     Hdr* mHdr = nullptr;
     u8* mRing = nullptr;
+    mutable double mNextAliveCheck = 0;  // watchdog: when to look at the peer's pid next
 };
 
 }  // namespace aby3

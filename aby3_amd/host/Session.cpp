@@ -1,5 +1,6 @@
 // C entry points (include/aby3.h): three persistent party threads running a
 // job of the hot path, for bench.py and the Python tests.
+#include "Link.h"
 #include <aby3.h>
 #include <algorithm>
 #include <atomic>
@@ -26,6 +27,18 @@ struct PartyCtx {
     Sh3Runtime rt;
     Sh3Encryptor enc;
     Sh3Evaluator eval;
+    bool ownProcess = false;  // one party per process (aby3h_party_create)
+    // One party per process, during setup: drain the stream and name the step
+    // if its work failed -- an asynchronous device fault otherwise surfaces in
+    // some later call (party 1's fault reported by a host copy).
+    void checkpoint(const char* step) {
+        if (!ownProcess) return;
+        try {
+            rt.gpu().sync();
+        } catch (const std::exception& e) {
+            throw std::runtime_error(std::string("after ") + step + ": " + e.what());
+        }
+    }
 };
 
 u64 xorshift(u64& x) {
@@ -335,12 +348,18 @@ struct LrJob : Job {
         sW[p.idx].resize(d, 1);
         if (p.idx == 0) {  // localFixedMatrix of train_data, train_label, W2 (main-logistic.cpp:117-121)
             p.enc.localIntMatrix(p.rt, X, sX[0]).get();
+            p.checkpoint("sharing X");
             p.enc.localIntMatrix(p.rt, Y, sY[0]).get();
+            p.checkpoint("sharing Y");
             p.enc.localIntMatrix(p.rt, w0, sW[0]).get();
+            p.checkpoint("sharing w");
         } else {
             p.enc.remoteIntMatrix(p.rt, sX[p.idx]).get();
+            p.checkpoint("receiving X");
             p.enc.remoteIntMatrix(p.rt, sY[p.idx]).get();
+            p.checkpoint("receiving Y");
             p.enc.remoteIntMatrix(p.rt, sW[p.idx]).get();
+            p.checkpoint("receiving w");
         }
         ml[p.idx] = std::make_unique<aby3ML>(p.rt, p.enc, p.eval, D);
         if (sample) {
@@ -349,6 +368,7 @@ struct LrJob : Job {
             dbatch[p.idx].reset(p.rt.gpu(), batches.size() * 4);
             toDevice(dbatch[p.idx].data(), batches.data(), batches.size() * 4, p.rt.gpu());
         }
+        p.checkpoint("batch indices");
     }
     void step(PartyCtx& p) override {
         const u64 t = iter[p.idx]++;
@@ -537,6 +557,7 @@ struct Session {
             p.rt.mComm.mPrev.asyncSendCopy(token);
             p.rt.mComm.mNext.recv(a);
             p.rt.mComm.mPrev.recv(b);
+            LinkEnd::closeAll();  // from here on, this process exiting is no failure to its peers
         } catch (const std::exception&) {
             // a peer that closed on an error: nothing left to wait for
         }
@@ -591,11 +612,15 @@ struct Session {
                 p.eval.init(i, toBlock(1, i), toBlock(1, (i + 1) % 3));
             }
             if (probe) GPU_CALL(aby3g_probe_enable_mask((u32)probe));
+            p.ownProcess = locals.size() == 1;
             job->setup(p);
+            p.checkpoint("the job's setup");
             p.rt.gpu().sync();
         } catch (const std::exception& e) {
             std::lock_guard<std::mutex> lk(mu);
             err = std::string("party ") + std::to_string(i) + " setup: " + e.what();
+            // one party per process: the peers stop waiting for it now
+            if (locals.size() == 1) LinkEnd::abortAll(err);
         }
         {
             std::lock_guard<std::mutex> lk(mu);
@@ -666,6 +691,7 @@ struct Session {
             } catch (const std::exception& e) {
                 std::lock_guard<std::mutex> lk(mu);
                 if (err.empty()) err = std::string("party ") + std::to_string(i) + ": " + e.what();
+                if (locals.size() == 1) LinkEnd::abortAll(err);
             }
             std::lock_guard<std::mutex> lk(mu);
             ++finished;

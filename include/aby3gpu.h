@@ -40,6 +40,11 @@ enum { ABY3G_OK = 0, ABY3G_EINVAL = 1, ABY3G_EHIP = 2, ABY3G_ENOMEM = 3 };
 
 /* ------------------------------------------------------------------ misc -- */
 const char* aby3g_last_error(void);
+/* Diagnostics: the names of this process's last 32 C-ABI calls, newest
+ * first, joined by " < " into out (cap bytes, NUL-terminated). A device fault
+ * is reported by a later call than the one that enqueued the faulting work;
+ * that work is among these. (No reference counterpart.) */
+int aby3g_recent_calls(char* out, size_t cap);
 int aby3g_version(void);
 int aby3g_device_count(int* n);
 /* The calling thread's current device. The library remembers the device

@@ -36,3 +36,14 @@ def gpu():
     lib = native.lib()
     lib.set_device(0)
     return lib
+
+
+# The multi-process transport tests (three party processes per case) run
+# after everything else: a transport fault there must not cut off the hot
+# path's parity tests behind it under `pytest -x` (a fault in
+# test_gpu_parties.py left every full-size C3/C4/C5 check unrun).
+_LAST = ("test_gpu_parties.py",)
+
+
+def pytest_collection_modifyitems(session, config, items):
+    items.sort(key=lambda it: any(it.nodeid.split("::")[0].endswith(n) for n in _LAST))

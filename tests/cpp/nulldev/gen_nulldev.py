@@ -14,6 +14,7 @@ HDR = os.path.join(HERE, "..", "..", "..", "include", "aby3gpu.h")
 OVERRIDES = {
     "aby3g_last_error": 'return "";',
     "aby3g_version": "return 1;",
+    "aby3g_recent_calls": "if (cap) out[0] = 0; return 0;",
     "aby3g_device_count": "*n = ND_DEVICES; return 0;",
     "aby3g_set_device": "if (device < 0 || device >= ND_DEVICES) return 1; t_device = device; return 0;",
     "aby3g_get_device": "*device = t_device; return 0;",
@@ -26,7 +27,7 @@ OVERRIDES = {
     "aby3g_device_sync": "g_blocking.fetch_add(1); return 0;",
     "aby3g_host_malloc": "*ptr = calloc(1, bytes ? bytes : 1); return *ptr ? 0 : 1;",
     "aby3g_host_free": "free(ptr); return 0;",
-    "aby3g_memcpy": "if (kind == 3) g_kind3.fetch_add(1); if (bytes) memmove(dst, src, bytes); return 0;",
+    "aby3g_memcpy": "if (nd_inject()) return 1; if (kind == 3) g_kind3.fetch_add(1); if (bytes) memmove(dst, src, bytes); return 0;",
     "aby3g_memset": "if (bytes) memset(dst, value, bytes); return 0;",
     "aby3g_stream_create": "*stream = new int(0); return 0;",
     "aby3g_stream_destroy": "delete (int*)stream; return 0;",
@@ -88,6 +89,15 @@ static int nd_peer(int device, int peer) {
 extern "C" void nulldev_stats(unsigned* peer_bits, unsigned long* kind3_copies) {
     *peer_bits = g_peer.load();
     *kind3_copies = g_kind3.load();
+}
+// failure injection (tests/cpp/nulldev/party_fail.cpp): the n-th copy from
+// now on fails, as a faulted device's next call does
+static std::atomic<long> g_fail_in{0};
+extern "C" void nulldev_fail_nth_memcpy(long n) { g_fail_in.store(n); }
+static bool nd_inject() {
+    long v = g_fail_in.load();
+    while (v > 0 && !g_fail_in.compare_exchange_weak(v, v - 1)) {}
+    return v == 1;
 }
 static char* g_arena = nullptr;
 static std::atomic<size_t>* g_off = nullptr;

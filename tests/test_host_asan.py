@@ -48,6 +48,23 @@ def test_party_processes_sanitized(tmp_path):
     assert "party_procs: ok" in r.stdout
 
 
+def test_party_failure_ends_peers_fast(tmp_path):
+    """One party per process, party 1 failing (a failed copy during its setup;
+    its process gone right after the ring is built): both peers exit non-zero
+    within 2 s, naming party 1's error or its exit (a
+    setup failure used to cost the peers the full link timeout)."""
+    exe = _build(str(tmp_path), "address", "party_fail.cpp")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0", ABY3_LINK_TIMEOUT_S="60")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    assert "party_fail: ok" in r.stdout, r.stdout
+    out = r.stdout
+    # mode 1: the peers name party 1's own error through the abort word
+    assert out.count("failed: party 1 setup") >= 2, out
+    # mode 2: the watchdog finds party 1's process gone without closing
+    assert out.count("exited without closing link") >= 2, out
+
+
 def test_link_large_cyclic_exchange(tmp_path):
     """Three processes, each sending host payloads of three times a link's
     ring size to the next party before receiving from the previous one

@@ -433,6 +433,12 @@ static_assert(sizeof(aby3g_ipc_handle) == sizeof(hipIpcMemHandle_t), "IPC handle
 int aby3g_ipc_get_handle(void* ptr, aby3g_ipc_handle* handle) {
     return guarded([&] {
         ABY3G_REQUIRE(ptr != nullptr && handle != nullptr, "null argument");
+        // whole 2 MiB-granular allocations only (include/aby3gpu.h)
+        void* base = nullptr;
+        size_t size = 0;
+        ABY3G_CHECK_HIP(hipMemGetAddressRange(&base, &size, ptr));
+        ABY3G_REQUIRE(base == ptr, "IPC export of a pointer inside an allocation");
+        ABY3G_REQUIRE(size % ABY3G_IPC_GRANULE == 0, "IPC export of an allocation that is not a multiple of 2 MiB");
         hipIpcMemHandle_t h;
         ABY3G_CHECK_HIP(hipIpcGetMemHandle(&h, ptr));
         std::memcpy(handle->bytes, &h, sizeof(h));

@@ -391,11 +391,12 @@ struct Pipe {
             }
             LinkSlot& s = lslots[(size_t)k];
             if (!s.ptr) {
-                // capacities are powers of two: a slot is outgrown at most
-                // log2(largest message / 64 KiB) times, so the retired buffers
-                // behind it (kept until teardown) add up to less than its
-                // current capacity, whatever the sequence of message sizes
-                size_t cap = 64 << 10;
+                // capacities are powers of two from 2 MiB (whole blocks: the
+                // IPC export rule, aby3g_ipc_get_handle): a slot is outgrown at
+                // most log2(largest message / 2 MiB) times, so the retired
+                // buffers behind it (kept until teardown) add up to less than
+                // its current capacity, whatever the sequence of message sizes
+                size_t cap = ipcBytes(1);
                 while (cap < bytes) cap <<= 1;
                 s.cap = cap;
                 GPU_CALL(aby3g_malloc(&s.ptr, s.cap));
@@ -955,7 +956,7 @@ CommPkg makeProcessRing(int party, const std::string& link, int device, bool sam
         GPU_CALL(aby3g_stream_create(&tmp));
         for (int to : {nx, pv}) {
             Pipe& p = *pipes[party][to];
-            GPU_CALL(aby3g_malloc(&p.arena, kArenaFlagBytes + 2 * slot));
+            GPU_CALL(aby3g_malloc(&p.arena, ipcBytes(kArenaFlagBytes + 2 * slot)));
             GPU_CALL(aby3g_memset(p.arena, 0, kArenaFlagBytes, tmp));
             GPU_CALL(aby3g_stream_sync(tmp));
             p.arenaSlot = slot;

@@ -23,6 +23,12 @@ struct block {
 };
 inline block toBlock(u64 hi, u64 lo) { return block{lo, hi}; }
 inline block toBlock(u64 lo) { return block{lo, 0}; }
+// bytes of a device allocation that is exported through IPC: whole 2 MiB
+// blocks (aby3g_ipc_get_handle refuses anything else)
+inline size_t ipcBytes(size_t b) {
+    const size_t g = (size_t)2 << 20;
+    return b ? (b + g - 1) / g * g : g;
+}
 
 #define ABY3_STR2(x) #x
 #define ABY3_STR(x) ABY3_STR2(x)

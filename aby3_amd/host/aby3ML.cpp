@@ -125,8 +125,9 @@ struct FusedLr {
         // bench -- uncached mailboxes and system-scope messages)
         f->sysScope = comm.forceRemote || std::memcmp(un, uuid, 16) != 0 || std::memcmp(up, uuid, 16) != 0;
         GPU_CALL(aby3g_set_device(g.device()));
-        GPU_CALL(f->sysScope ? aby3g_malloc_uncached(&f->ownBox, mb) : aby3g_malloc(&f->ownBox, mb));
-        GPU_CALL(aby3g_memset(f->ownBox, 0, mb, g.stream()));
+        const size_t mbx = ipcBytes(mb);  // exported: whole 2 MiB blocks
+        GPU_CALL(f->sysScope ? aby3g_malloc_uncached(&f->ownBox, mbx) : aby3g_malloc(&f->ownBox, mbx));
+        GPU_CALL(aby3g_memset(f->ownBox, 0, mbx, g.stream()));
         g.sync();  // zeroed before its handle leaves
         aby3g_ipc_handle h{}, hn{}, hp{};
         GPU_CALL(aby3g_ipc_get_handle(f->ownBox, &h));

@@ -145,7 +145,12 @@ int aby3g_set_handoff_timeout_us(uint64_t us);
 typedef struct {
     unsigned char bytes[64];
 } aby3g_ipc_handle;
-int aby3g_ipc_get_handle(void* ptr, aby3g_ipc_handle* handle); /* ptr: a base pointer from aby3g_malloc */
+/* ptr: the base pointer of an aby3g_malloc / aby3g_malloc_uncached allocation
+ * whose size is a multiple of ABY3G_IPC_GRANULE (2 MiB) -- anything else is
+ * refused (ABY3G_EINVAL). Smaller allocations may be fragments that the
+ * runtime carves out of a shared 2 MiB block; only whole blocks are exported. */
+#define ABY3G_IPC_GRANULE ((size_t)2 << 20)
+int aby3g_ipc_get_handle(void* ptr, aby3g_ipc_handle* handle);
 int aby3g_ipc_open(const aby3g_ipc_handle* handle, void** ptr); /* mapped for the current device */
 int aby3g_ipc_close(void* ptr);
 /* page-aligned host memory -> an address the current device's streams can

@@ -37,10 +37,10 @@ OVERRIDES = {
     "aby3g_event_record": "*(int*)ev = 1; return 0;",
     "aby3g_event_elapsed_ms": "*ms = 0; return 0;",
     "aby3g_event_query": "*done = 1; return 0;",
-    "aby3g_signal_alloc": "g_blocking.fetch_add(1); *word = (uint64_t*)calloc(1, 8); return *word ? 0 : 1;",
+    "aby3g_signal_alloc": "g_blocking.fetch_add(1); *word = (uint64_t*)nd_alloc(8); return *word ? 0 : 1;",
     "aby3g_stream_write_value": "__atomic_store_n(word, value, __ATOMIC_RELEASE); return 0;",
     "aby3g_stream_wait_value": "return nd_wait(word, value);",
-    "aby3g_ipc_get_handle": "memset(handle, 0, sizeof *handle); memcpy(handle->bytes, &ptr, sizeof ptr); return 0;",
+    "aby3g_ipc_get_handle": "if (!nd_ipc_exportable(ptr)) return 1; memset(handle, 0, sizeof *handle); memcpy(handle->bytes, &ptr, sizeof ptr); return 0;",
     "aby3g_ipc_open": "memcpy(ptr, handle->bytes, sizeof *ptr); return 0;",
     "aby3g_host_register": "*dev = host; return 0;",
     "aby3g_probe_read": "*ms = 0; *launches = 0; return 0;",
@@ -63,6 +63,7 @@ OVERRIDES = {
 # has run the matching write).
 PREAMBLE = r"""
 #include <atomic>
+#include <cstdio>
 #include <chrono>
 #include <fcntl.h>
 #include <sys/mman.h>
@@ -122,17 +123,42 @@ extern "C" int nulldev_shared_arena(size_t bytes) {
     g_cap = bytes;
     return 0;
 }
+// every block carries a 256-byte header (magic, size): the IPC export rule
+// of aby3g_ipc_get_handle -- base pointers of whole 2 MiB-granular
+// allocations only -- is checked here as on the device
+constexpr uint64_t ND_MAGIC = 0x6e646d656d626c6bull;
 static void* nd_alloc(size_t b) {
     if (!b) b = 1;
-    if (!g_arena) return calloc(1, b);
-    const size_t o = g_off->fetch_add((b + 255) & ~(size_t)255);
-    if (o + b > g_cap) return nullptr;
-    memset(g_arena + o, 0, b);
-    return g_arena + o;
+    char* h;
+    if (!g_arena) {
+        h = (char*)calloc(1, b + 256);
+        if (!h) return nullptr;
+    } else {
+        const size_t o = g_off->fetch_add((b + 256 + 255) & ~(size_t)255);
+        if (o + b + 256 > g_cap) return nullptr;
+        h = g_arena + o;
+        memset(h, 0, b + 256);
+    }
+    ((uint64_t*)h)[0] = ND_MAGIC;
+    ((uint64_t*)h)[1] = b;
+    return h + 256;
 }
 static void nd_free(void* p) {
+    if (!p) return;
     if (g_arena && (char*)p >= g_arena && (char*)p < g_arena + g_cap) return;
-    free(p);
+    free((char*)p - 256);
+}
+static bool nd_ipc_exportable(void* p) {
+    const uint64_t* h = (const uint64_t*)((char*)p - 256);
+    if (h[0] != ND_MAGIC) {
+        fprintf(stderr, "nulldev: IPC export of a pointer that is not an allocation's base\n");
+        return false;
+    }
+    if (h[1] % ((size_t)2 << 20)) {
+        fprintf(stderr, "nulldev: IPC export of a %llu-byte allocation (not whole 2 MiB blocks)\n", (unsigned long long)h[1]);
+        return false;
+    }
+    return true;
 }
 static int nd_wait(uint64_t* w, uint64_t v) {
     const auto t0 = std::chrono::steady_clock::now();

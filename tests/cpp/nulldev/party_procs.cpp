@@ -72,7 +72,7 @@ static int party_main(int party, const std::string& tag, bool ownDevice, bool fo
 }
 
 int main(int argc, char** argv) {
-    if (nulldev_shared_arena((size_t)1 << 30)) return 2;
+    if (nulldev_shared_arena((size_t)4 << 30)) return 2;
     // `party_procs <party> <tag>`: one party only, started by a launcher
     // (tests/test_dist.py: three gloo ranks, one party each, sharing the
     // named arena ND_ARENA)

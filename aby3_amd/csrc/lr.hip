@@ -774,7 +774,7 @@ __device__ __forceinline__ void lr_party(const u32* T0g, const aby3g_lr_iter& it
                 if (mw.ok) mem[WS + (u64)andWires[pl.and_wire_off + j] * W + w] = v;
             }
             if (!msg_done(mw, &msgBad, ticks)) return;
-            if (lv <= 7) lr_stamp(PT, 23 + lv);  // level lv - 1's AND shares in
+            if (lv < 16) lr_stamp(PT, 96 + lv);  // level lv - 1's AND shares in (ABY3G_LR_PHASE_SLOTS)
         }
         if (lv == cir.nlevels) break;
         // by value: the engine memory's LDS stores below would otherwise

@@ -155,7 +155,7 @@ struct Pipe {
     void* arena = nullptr;
     u64 arenaSlot = 0;   // bytes per evaluation slot
     u64 arenaNext = 0;   // sender: slots handed out
-    int arenaOpen = 0;   // sender: an evaluation holds a slot (evalSendBuffer .. evalSendEnd)
+    int arenaOpen = 0;   // sender: an evaluation holds a slot (evalSendBuffer's lease alive)
     bool arenaMapped = false;
     u64* arenaFlags() const { return (u64*)arena; }
     u8* arenaSlots() const { return (u8*)arena + kArenaFlagBytes; }
@@ -717,17 +717,20 @@ const HandoffResidency& handoffResidency(int device) {
     return byDevice.emplace(device, r).first->second;
 }
 
-std::shared_ptr<DeviceBuffer> Channel::evalSendBuffer(Gpu& gpu, size_t bytes, u64 andLevels) {
+std::shared_ptr<DeviceBuffer> Channel::evalSendBuffer(Gpu& gpu, size_t bytes, u64 andLevels,
+                                                     std::shared_ptr<void>* lease) {
+    if (!lease) throw std::runtime_error("evalSendBuffer: null lease");
     if (!mOut || !mOut->link || !mOut->arena || kernelsSerialized() || bytes > mOut->arenaSlot) return nullptr;
     Pipe& p = *mOut;
     if (andLevels < 2 || p.arenaOpen) return nullptr;
     p.arenaOpen = 1;
+    std::weak_ptr<Pipe> pipe = mOut;  // the lease does not keep the channel alive
+    static int tag;  // a non-null token: the lease tests true while held
+    *lease = std::shared_ptr<void>(&tag, [pipe](void*) {
+        if (auto q = pipe.lock()) q->arenaOpen = 0;
+    });
     const u64 slot = p.arenaNext++ & 1;
     return DeviceBuffer::borrow(p.arenaSlots() + slot * p.arenaSlot, bytes, &gpu);
-}
-
-void Channel::evalSendEnd() {
-    if (mOut) mOut->arenaOpen = 0;
 }
 
 bool Channel::linkedConcurrent() const {

@@ -103,10 +103,10 @@ public:
     // later; that is safe only when the evaluations run one after another on
     // the party's stream and each has two or more AND levels (the receiver's
     // reads of evaluation e precede, in its stream, its first message of e+1,
-    // which the sender's e+1 needs before it starts e+2). The caller ends its
-    // lease with evalSendEnd() once the evaluation's last message is sent.
-    std::shared_ptr<DeviceBuffer> evalSendBuffer(Gpu& gpu, size_t bytes, u64 andLevels);
-    void evalSendEnd();
+    // which the sender's e+1 needs before it starts e+2). The lease is held by
+    // *lease and ends when the caller drops it -- once the evaluation's last
+    // message is sent, or whenever the evaluation is reset or abandoned.
+    std::shared_ptr<DeviceBuffer> evalSendBuffer(Gpu& gpu, size_t bytes, u64 andLevels, std::shared_ptr<void>* lease);
     // Both directions join parties on `gpu`'s device in this process whose
     // ring allows kernel hand-offs (a fused launch may then address the
     // peer's device memory and poll it).

@@ -207,7 +207,8 @@ void* Gpu::alloc(size_t bytes) {
         // Out of memory. No recovery here: returning the cache to the driver
         // (hipFree) waits for the whole device, and mid-protocol that wait can
         // block on a peer's kernel that waits for this party's next launch.
-        // Callers trim() at a quiescent point (between runs) instead.
+        // The session trims the pools between runs instead, once a party's
+        // cache passes ABY3_POOL_TRIM_MB (aby3h_session_run, Session.cpp).
         size_t cached;
         {
             std::lock_guard<std::mutex> lk(mPool->mu);
@@ -215,7 +216,7 @@ void* Gpu::alloc(size_t bytes) {
         }
         throw std::runtime_error(std::string("device out of memory allocating ") + std::to_string(cls) +
                                  " bytes (" + std::to_string(cached) + " bytes cached by this party's pool; " +
-                                 "Gpu::trim() between runs returns them): " + aby3g_last_error());
+                                 "runs trim it past ABY3_POOL_TRIM_MB): " + aby3g_last_error());
     }
     return p;
 }

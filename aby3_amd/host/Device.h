@@ -92,7 +92,10 @@ public:
 
     void* alloc(size_t bytes);
     const std::shared_ptr<Pool>& pool() const { return mPool; }
-    size_t cachedBytes() const { return mPool->cached; }
+    size_t cachedBytes() const {
+        std::lock_guard<std::mutex> lk(mPool->mu);  // other parties' threads release late buffers into it
+        return mPool->cached;
+    }
     void trim();  // return cached blocks to the driver
 
     // Per-Gpu cache of derived device data (uploaded circuits, tables): the

@@ -510,6 +510,7 @@ struct Session {
     u64 digests[3] = {0, 0, 0};
     std::vector<CommPkg> comms;
     double hostEnqueueUs[3] = {0, 0, 0}, hostDrainUs[3] = {0, 0, 0}, hostRecvWaitUs[3] = {0, 0, 0};
+    size_t poolCached[3] = {0, 0, 0};  // each party's cached pool bytes after its last run
     double hostApiUs[3] = {0, 0, 0}, hostApiCalls[3] = {0, 0, 0};
     double deviceWaitUs[3] = {0, 0, 0};  // in-kernel waits for peers per step (Gpu::waitUs)
     int devices[3] = {0, 0, 0};
@@ -661,6 +662,7 @@ struct Session {
                     const auto t2 = std::chrono::steady_clock::now();
                     hostEnqueueUs[i] = n ? std::chrono::duration<double, std::micro>(t1 - t0).count() / n : 0;
                     hostDrainUs[i] = std::chrono::duration<double, std::micro>(t2 - t1).count();
+                    poolCached[i] = p.rt.gpu().cachedBytes();
                     deviceWaitUs[i] = n ? (p.rt.gpu().waitUs() - dw0) / n : 0;
                 } else if (c == 3) {
                     double ms = 0;
@@ -671,6 +673,12 @@ struct Session {
                     probeN[0] += cnt;
                 } else if (c == 4) {
                     GPU_CALL(aby3g_probe_reset());
+                } else if (c == 7) {
+                    // every local party is between runs with its streams
+                    // drained (aby3h_session_run): nothing of this process can
+                    // wait on a peer, so trim's device-wide wait cannot block
+                    p.rt.gpu().trim();
+                    poolCached[i] = 0;
                 } else if (c == 6) {
                     const SharedMat* r = job->result(i);
                     u64 h = 0xcbf29ce484222325ull;  // FNV-1a over both shares' bytes
@@ -709,6 +717,16 @@ struct Session {
         done.wait(lk, [&] { return finished == (int)locals.size(); });
     }
 };
+
+// cached pool bytes per party above which a run's end trims the pools
+// (ABY3_POOL_TRIM_MB, default 32 GiB of the 288 GB of HBM per MI355X)
+static size_t poolTrimBytes() {
+    static const size_t b = [] {
+        const char* e = getenv("ABY3_POOL_TRIM_MB");
+        return (e && *e ? (size_t)atoll(e) : (size_t)32 << 10) << 20;
+    }();
+    return b;
+}
 
 std::unique_ptr<Job> makeJob(int job, const uint64_t* params, int nparams) {
     auto P = [&](int i, u64 def) { return i < nparams ? params[i] : def; };
@@ -832,6 +850,14 @@ int aby3h_session_run(aby3h_session* h, uint64_t steps) {
         return 1;
     }
     s.command(1, steps);
+    if (s.err.empty()) {
+        // The pools keep every freed block cached for reuse (a mid-run free
+        // could wait on a peer, Device.cpp Gpu::alloc); past a bound, give the
+        // cache back here, between runs, where every local party is idle.
+        size_t most = 0;
+        for (int q : s.locals) most = std::max(most, s.poolCached[q]);
+        if (most > poolTrimBytes()) s.command(7);
+    }
     if (s.err.empty()) {
         try {
             for (int q : s.locals) {

@@ -133,6 +133,7 @@ void Sh3BinaryEvaluator::setCir(BetaCircuit* cir, u64 width, block prevSeed, blo
     if (mZPending) waitZ();  // setCir again before evaluating: the old draw lands first
     releaseZ();
     mSendAll.reset();
+    mArenaLease.reset();
     mAndDone = 0;
     const u64 zWords = (u64)cir->mAndCount * mWords;
     if (zWords) {
@@ -479,6 +480,7 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
     const u32 nAnd = gatesHere ? mCir->mLevelAndCounts[mLevel] : 0;
     if (mLevel == 0 && mAndDone) {  // evaluated again after setCir: a fresh send buffer
         mSendAll.reset();
+        mArenaLease.reset();
         mAndDone = 0;
     }
     std::shared_ptr<DeviceBuffer> send;
@@ -488,8 +490,7 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
             // the channel's IPC-mapped arena, read in place by the receiver
             u64 andLevels = 0;
             for (u32 c : mCir->mLevelAndCounts) andLevels += c != 0;
-            mSendAll = comm.mNext.evalSendBuffer(g, (u64)mCir->mAndCount * rowBytes, andLevels);
-            mArenaLease = mSendAll != nullptr;
+            mSendAll = comm.mNext.evalSendBuffer(g, (u64)mCir->mAndCount * rowBytes, andLevels, &mArenaLease);
             if (!mSendAll) mSendAll = std::make_shared<DeviceBuffer>(g, (u64)mCir->mAndCount * rowBytes);
         }
         send = DeviceBuffer::view(mSendAll, mAndDone * rowBytes, nAnd * rowBytes);
@@ -528,11 +529,8 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
     if (nAnd) {
         comm.mNext.asyncSendShared(send, nAnd * rowBytes, g, hp);
         mRecvFutr = comm.mPrev.asyncRecvShared(nAnd * rowBytes, g);
-        if (mArenaLease && mAndDone == mCir->mAndCount) {
-            // the evaluation's last message is sent: the arena may serve the next one
-            comm.mNext.evalSendEnd();
-            mArenaLease = false;
-        }
+        // the evaluation's last message is sent: the arena may serve the next one
+        if (mAndDone == mCir->mAndCount) mArenaLease.reset();
     }
     ++mLevel;
     if (hasMoreRounds()) task.then([this](CommPkg& c, Sh3Task& t) { roundCallback(c, t); }, "callback");

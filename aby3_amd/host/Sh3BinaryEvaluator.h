@@ -128,7 +128,9 @@ private:
     // last level, instead of per level
     std::shared_ptr<DeviceBuffer> mSendAll;
     u64 mAndDone = 0;  // AND outputs of the levels already run (their rows in mSendAll)
-    bool mArenaLease = false;  // mSendAll is the channel's arena slot (Channel::evalSendBuffer)
+    // held while mSendAll is the channel's arena slot (Channel::evalSendBuffer);
+    // dropped with mSendAll, after the evaluation's last message, or with this
+    std::shared_ptr<void> mArenaLease;
     // setInputs' sources held for the first level's launch (DevCircuit::fuseInputs)
     std::vector<aby3g_wire_src> mPendingIn;
     // buffers the held sources read (e.g. a received message): kept alive

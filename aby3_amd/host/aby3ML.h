@@ -40,7 +40,7 @@ struct SgdState {
     std::shared_ptr<FusedLr> fused;
     bool fusedChecked = false;
     bool fusedSysScope = false;  // the fused iteration's messages are system-scope (parties on other GPUs)
-    u64* phaseTicks = nullptr;  // optional device [32]: the fused launch's phase stamps (profiling)
+    u64* phaseTicks = nullptr;  // optional device [ABY3G_LR_PHASE_SLOTS]: the fused launch's phase stamps (profiling)
     const u32* nextBatch = nullptr;  // optional: the next iteration's batch (its rows prefetched into L2)
 };
 

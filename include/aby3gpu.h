@@ -590,6 +590,10 @@ typedef struct {
  * sys_scope: 0 when the three mailboxes are on this device (agent-scope
  * messages), 1 when a neighbour's is on another GPU (system scope; every
  * mailbox then from aby3g_malloc_uncached). */
+/* phase_ticks slots: 0-15 phases, 16 + lv end of circuit level lv (lv < 16),
+ * 32 + 4 lv + b / 64 + 4 lv + b batch b of level lv (lv < 8, b < 4),
+ * 96 + lv level lv - 1's AND shares received (1 <= lv < 16) */
+#define ABY3G_LR_PHASE_SLOTS 112
 typedef struct {
     int32_t party;
     uint32_t B, d, D, aB;
@@ -606,7 +610,7 @@ typedef struct {
     uint64_t epoch;
     uint32_t sys_scope;
     uint64_t* wait_ticks;    /* optional: in-kernel wait (100 MHz ticks) added here */
-    uint64_t* phase_ticks;   /* optional: [96] wall-clock stamps of the phases (profiling) */
+    uint64_t* phase_ticks;   /* optional: [ABY3G_LR_PHASE_SLOTS] wall-clock stamps of the phases (profiling) */
     /* the evaluator's ShareGen streams (seeds) and zero-share keys */
     uint8_t prev_seed[16], next_seed[16];
     uint8_t zs_prev[16], zs_next[16];

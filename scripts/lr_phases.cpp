@@ -9,6 +9,8 @@
 #include <thread>
 #include "aby3ML.h"
 
+constexpr unsigned long long S = ABY3G_LR_PHASE_SLOTS;  // stamp slots per iteration
+
 using namespace aby3;
 
 int main(int argc, char** argv) {
@@ -50,21 +52,21 @@ int main(int argc, char** argv) {
             }
             aby3ML ml(rt, enc, ev, D);
             SgdState st;
-            DeviceBuffer dIdx(rt.gpu(), idx.size() * 4), ticks(rt.gpu(), iters * 96 * 8);
+            DeviceBuffer dIdx(rt.gpu(), idx.size() * 4), ticks(rt.gpu(), iters * S * 8);
             toDevice(dIdx.data(), idx.data(), idx.size() * 4, rt.gpu());
-            const std::vector<u64> zeros(iters * 96, 0);  // unused slots read 0
-            toDevice(ticks.data(), zeros.data(), iters * 96 * 8, rt.gpu());
+            const std::vector<u64> zeros(iters * S, 0);  // unused slots read 0
+            toDevice(ticks.data(), zeros.data(), iters * S * 8, rt.gpu());
             rt.gpu().sync();
             const auto t0 = std::chrono::steady_clock::now();
             for (u64 t = 0; t < iters; ++t) {
-                st.phaseTicks = ticks.as<u64>() + 96 * t;
+                st.phaseTicks = ticks.as<u64>() + S * t;
                 sgdLogisticStep(ml, sX, sY, sW, dIdx.as<u32>() + t * B, B, aB, st);
             }
             rt.gpu().sync();
             if (p == 0)
                 wallUs = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-            stamps[p].resize(iters * 96);
-            toHost(stamps[p].data(), ticks.data(), iters * 96 * 8, rt.gpu());
+            stamps[p].resize(iters * S);
+            toHost(stamps[p].data(), ticks.data(), iters * S * 8, rt.gpu());
             if (!st.fused) std::printf("party %d: fused form NOT taken\n", p);
         });
     for (auto& t : th) t.join();
@@ -79,36 +81,25 @@ int main(int argc, char** argv) {
         for (int ph = 0; ph < 11; ++ph) {
             std::vector<double> v;
             for (u64 t = iters / 2; t < iters; ++t)
-                v.push_back(0.01 * (double)(stamps[p][96 * t + ph + 1] - stamps[p][96 * t + ph]));
+                v.push_back(0.01 * (double)(stamps[p][S * t + ph + 1] - stamps[p][S * t + ph]));
             std::sort(v.begin(), v.end());
             std::printf(" %s %.1f |", names[ph], v[v.size() / 2]);
             tot += v[v.size() / 2];
         }
         {
             std::vector<double> v;
-            for (u64 t = iters / 2; t < iters; ++t) v.push_back(0.01 * (double)(stamps[p][96 * t + 12] - stamps[p][96 * t]));
+            for (u64 t = iters / 2; t < iters; ++t) v.push_back(0.01 * (double)(stamps[p][S * t + 12] - stamps[p][S * t]));
             std::sort(v.begin(), v.end());
             std::printf(" (table fill %.1f)", v[v.size() / 2]);
             std::vector<double> f;
             for (u64 t = iters / 2; t < iters; ++t)
-                f.push_back(100.0 * (double)(stamps[p][96 * t + 14] - stamps[p][96 * t + 13]) /
-                            (double)(stamps[p][96 * t + 11] - stamps[p][96 * t]));
+                f.push_back(100.0 * (double)(stamps[p][S * t + 14] - stamps[p][S * t + 13]) /
+                            (double)(stamps[p][S * t + 11] - stamps[p][S * t]));
             std::sort(f.begin(), f.end());
             std::printf(" (shader clock %.0f MHz)", f[f.size() / 2]);
             std::vector<double> pr;  // slot 15: an optional probe stamp after slot 12
             for (u64 t = iters / 2; t < iters; ++t)
-                if (stamps[p][96 * t + 15]) pr.push_back(0.01 * (double)(stamps[p][96 * t + 15] - stamps[p][96 * t + 12]));
-            std::vector<double> sk, ld;
-            for (u64 t = iters / 2; t < iters; ++t)
-                if (stamps[p][96 * t + 31]) {
-                    sk.push_back(0.01 * (double)(stamps[p][96 * t + 30] - stamps[p][96 * t]));
-                    ld.push_back(0.01 * (double)(stamps[p][96 * t + 31] - stamps[p][96 * t]));
-                }
-            if (!sk.empty()) {
-                std::sort(sk.begin(), sk.end());
-                std::sort(ld.begin(), ld.end());
-                std::printf(" (probe last wave start %.1f, first load %.1f)", sk[sk.size() / 2], ld[ld.size() / 2]);
-            }
+                if (stamps[p][S * t + 15]) pr.push_back(0.01 * (double)(stamps[p][S * t + 15] - stamps[p][S * t + 12]));
             if (!pr.empty()) {
                 std::sort(pr.begin(), pr.end());
                 std::printf(" (probe 12->15 %.1f)", pr[pr.size() / 2]);
@@ -120,7 +111,7 @@ int main(int argc, char** argv) {
             for (int lv = 0; lv < 8; ++lv) {
                 std::vector<double> v;
                 for (u64 t = iters / 2; t < iters; ++t) {
-                    const u64 a = stamps[p][96 * t + (lv ? 16 + lv - 1 : 5)], b = stamps[p][96 * t + 16 + lv];
+                    const u64 a = stamps[p][S * t + (lv ? 16 + lv - 1 : 5)], b = stamps[p][S * t + 16 + lv];
                     if (b) v.push_back(0.01 * (double)(b - a));
                 }
                 if (!v.empty()) {
@@ -128,13 +119,13 @@ int main(int argc, char** argv) {
                     std::printf(" L%d %.1f", lv, v[v.size() / 2]);
                 }
             }
-            // slots 23 + lv (lv = 1..7): level lv - 1's AND shares received and unpacked
+            // slots 96 + lv (lv = 1..7): level lv - 1's AND shares received and unpacked
             std::printf("\n   level lv: wait for lv-1's shares + unpack / gates:");
             for (int lv = 1; lv < 8; ++lv) {
                 std::vector<double> a, b;
                 for (u64 t = iters / 2; t < iters; ++t) {
-                    const u64 e0 = stamps[p][96 * t + 16 + lv - 1], r = stamps[p][96 * t + 23 + lv],
-                              e1 = stamps[p][96 * t + 16 + lv];
+                    const u64 e0 = stamps[p][S * t + 16 + lv - 1], r = stamps[p][S * t + 96 + lv],
+                              e1 = stamps[p][S * t + 16 + lv];
                     if (r && e1) {
                         a.push_back(0.01 * (double)(r - e0));
                         b.push_back(0.01 * (double)(e1 - r));
@@ -153,7 +144,7 @@ int main(int argc, char** argv) {
                 for (int b = 0; b < 4; ++b) {
                     std::vector<double> v;
                     for (u64 t = iters / 2; t < iters; ++t) {
-                        const u64 r = stamps[p][96 * t + 23 + lv], e = stamps[p][96 * t + 32 + 4 * lv + b];
+                        const u64 r = stamps[p][S * t + 96 + lv], e = stamps[p][S * t + 32 + 4 * lv + b];
                         if (r && e) v.push_back(0.01 * (double)(e - r));
                     }
                     if (v.empty()) break;
@@ -168,7 +159,7 @@ int main(int argc, char** argv) {
                 for (int b = 0; b < 4; ++b) {
                     std::vector<double> v;
                     for (u64 t = iters / 2; t < iters; ++t) {
-                        const u64 r = stamps[p][96 * t + 23 + lv], e = stamps[p][96 * t + 64 + 4 * lv + b];
+                        const u64 r = stamps[p][S * t + 96 + lv], e = stamps[p][S * t + 64 + 4 * lv + b];
                         if (r && e) v.push_back(0.01 * (double)(e - r));
                     }
                     if (v.empty()) break;
@@ -179,7 +170,7 @@ int main(int argc, char** argv) {
             std::printf("\n  ");
         }
         std::vector<double> gap;  // launch-to-launch gap: end of t-1 to start of t
-        for (u64 t = iters / 2; t < iters; ++t) gap.push_back(0.01 * (double)(stamps[p][96 * t] - stamps[p][96 * (t - 1) + 11]));
+        for (u64 t = iters / 2; t < iters; ++t) gap.push_back(0.01 * (double)(stamps[p][S * t] - stamps[p][96 * (t - 1) + 11]));
         std::sort(gap.begin(), gap.end());
         std::printf(" total %.1f us, gap between launches %.1f us\n", tot, gap[gap.size() / 2]);
     }

@@ -65,6 +65,17 @@ def test_party_failure_ends_peers_fast(tmp_path):
     assert out.count("exited without closing link") >= 2, out
 
 
+def test_pool_trim(tmp_path):
+    """The stream-ordered pool: trim() empties a cache of mixed size classes
+    and allocation goes on; a session past ABY3_POOL_TRIM_MB trims its
+    parties' pools between runs."""
+    exe = _build(str(tmp_path), "address", "pool_trim.cpp")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    assert "pool_trim: ok" in r.stdout, r.stdout
+
+
 def test_link_large_cyclic_exchange(tmp_path):
     """Three processes, each sending host payloads of three times a link's
     ring size to the next party before receiving from the previous one

@@ -46,13 +46,17 @@ struct Msg {
     // offset, published in-kernel with sequence number lseq
     bool linkInKernel = false;
     u64 larena = 0;
+    // or, from another process on this GPU, in the sender's arena at larena,
+    // ready once the link's ready word reaches lseq (stream hand-off, no copy)
+    bool linkArena = false;
 };
 
 // a message descriptor on a link's ring (host payloads follow it)
 struct WireMsg {
     u64 bytes;
     u32 kind;  // 0 host payload, 1 device payload (staged), 2 in-kernel (arena), 3 arena announce,
-               // 4 device identity (the sender's device UUID in handle.bytes[0..15])
+               // 4 device identity (the sender's device UUID in handle.bytes[0..15]),
+               // 5 arena payload behind the ready word (stream hand-off, read in place)
     u32 slot;
     u64 gen, seq;  // kind 2: gen = offset in the arena's slots; kind 3: gen = slot bytes
     i64 device;    // the sender's device
@@ -417,6 +421,28 @@ struct Pipe {
         sent += bytes;
         ringWrite(std::vector<u8>((const u8*)&w, (const u8*)&w + sizeof w));
     }
+    // sender: a payload already in this direction's arena (the binary
+    // engine's evaluation slot, evalSendBuffer) goes by reference: the stream
+    // writes the ready word behind the producing kernel and the receiver's
+    // stream waits for it, then its kernels read the arena in place -- no
+    // staging copies. The slot is rewritten two evaluations later, after the
+    // receiver has read it (the rule of evalSendBuffer).
+    bool linkSendArena(const void* src, size_t bytes, Gpu& gpu) {
+        const u8* q = (const u8*)src;
+        if (!arena || arenaMapped || !q || q < arenaSlots() || q + bytes > arenaSlots() + 2 * arenaSlot) return false;
+        std::lock_guard<std::mutex> lk(mu);
+        WireMsg w{};
+        w.bytes = bytes;
+        w.kind = 5;
+        w.slot = kNoSlot;
+        w.gen = (u64)(q - arenaSlots());
+        w.seq = ++devSeq;
+        w.device = gpu.device();
+        GPU_CALL(aby3g_stream_write_value(gpu.stream(), link->readyDev(), w.seq));
+        sent += bytes;
+        ringWrite(std::vector<u8>((const u8*)&w, (const u8*)&w + sizeof w));
+        return true;
+    }
     // receiver: the next message off the ring, filed under its ticket
     void linkTake() {
         WireMsg w;
@@ -430,6 +456,13 @@ struct Pipe {
             m.device = true;
             m.link = true;
             m.linkInKernel = true;
+            m.larena = w.gen;
+            m.lseq = w.seq;
+            m.ldevice = (int)w.device;
+        } else if (w.kind == 5) {
+            m.device = true;
+            m.link = true;
+            m.linkArena = true;
             m.larena = w.gen;
             m.lseq = w.seq;
             m.ldevice = (int)w.device;
@@ -517,7 +550,8 @@ void RecvFuture::get() const {
     std::lock_guard<std::mutex> lk(st.mu);
     if (st.done) return;
     Msg m = st.pipe->pop(st.ticket);
-    if (m.shared) throw std::runtime_error("channel: zero-copy payload received by a copying receive");
+    if (m.shared || m.linkArena || m.linkInKernel)
+        throw std::runtime_error("channel: zero-copy payload received by a copying receive");
     if (m.bytes != st.bytes)
         throw std::runtime_error("channel: message size mismatch (expected " + std::to_string(st.bytes) + ", got " +
                                  std::to_string(m.bytes) + ")");
@@ -585,6 +619,21 @@ std::shared_ptr<DeviceBuffer> RecvFuture::getShared() const {
         st.done = true;
         return st.out;
     }
+    if (m.link && m.linkArena) {
+        // from another process on this GPU, by reference into the sender's
+        // arena: wait for the ready word, read in place (this mapping)
+        if (m.bytes != st.bytes)
+            throw std::runtime_error("channel: message size mismatch (expected " + std::to_string(st.bytes) +
+                                     ", got " + std::to_string(m.bytes) + ")");
+        Pipe& p = *st.pipe;
+        if (!p.arena || m.larena + m.bytes > 2 * p.arenaSlot)
+            throw std::runtime_error("channel: arena message outside the sender's arena");
+        GPU_CALL(aby3g_set_device(st.gpu->device()));
+        GPU_CALL(aby3g_stream_wait_value(st.gpu->stream(), p.link->readyDev(), m.lseq));
+        st.out = DeviceBuffer::borrow(p.arenaSlots() + m.larena, std::max<size_t>(m.bytes, 8), st.gpu);
+        st.done = true;
+        return st.out;
+    }
     if (m.link) {
         // from another process: the payload is copied out of the sender's
         // staging slot into a buffer of this party
@@ -623,8 +672,9 @@ void Channel::sendShared(std::shared_ptr<DeviceBuffer> buf, size_t bytes, Gpu& g
     if (!buf || buf->bytes() < bytes) throw std::runtime_error("asyncSendShared: buffer smaller than the message");
     GPU_CALL(aby3g_set_device(gpu.device()));
     if (mOut->link) {
-        // another process cannot read this buffer in place: stage a copy
-        mOut->linkSendDevice(buf->data(), bytes, gpu);
+        // another process reads an arena payload in place; anything else is
+        // staged (a copy into an IPC-exported slot)
+        if (!mOut->linkSendArena(buf->data(), bytes, gpu)) mOut->linkSendDevice(buf->data(), bytes, gpu);
         return;
     }
     Msg m;

@@ -22,6 +22,17 @@ namespace aby3 {
 namespace {
 thread_local std::string t_err;
 
+// co-located parties plan each share GEMM for 1/k of the CUs (k = 3 by
+// default; ABY3_GEMM_SHARING=1: full-chip plans, for A/B runs)
+static int colocatedGemmSharing() {
+    static const int k = [] {
+        const char* e = getenv("ABY3_GEMM_SHARING");
+        const int v = e && *e ? atoi(e) : 3;
+        return v >= 1 && v <= 8 ? v : 3;
+    }();
+    return k;
+}
+
 struct PartyCtx {
     int idx = 0;
     Sh3Runtime rt;
@@ -576,7 +587,7 @@ struct Session {
                 // (measured: 3 streams beat 6 sharing 4 queues on every job)
                 if (colocated) p.rt.gpu().aliasAux();
                 // their share GEMMs run side by side: each fills its share of the CUs
-                if (colocated) GPU_CALL(aby3g_set_gemm_sharing(3));
+                if (colocated) GPU_CALL(aby3g_set_gemm_sharing(colocatedGemmSharing()));
                 p.rt.gpu().aux();
             });
             // (only for parties sharing this process: one party per process

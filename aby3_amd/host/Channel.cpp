@@ -83,6 +83,7 @@ struct LinkSlot {
     size_t cap = 0;
     u64 gen = 0, lastSeq = 0;
     aby3g_ipc_handle h{};
+    bool reserved = false;  // handed to a producer (linkReserve), its message not sent yet
 };
 }  // namespace
 
@@ -352,6 +353,73 @@ struct Pipe {
             ringWrite(std::move(m.host));
         }
     }
+    // sender (mu held): a staging slot of at least `bytes` that the receiver
+    // has released -- its previous message's copy-out enqueued (host mark),
+    // and this stream made to wait for that copy-out to finish
+    u32 pickSlot(size_t bytes, Gpu& gpu) {
+        int k = -1;
+        auto free = [&](size_t i) {
+            return !lslots[i].reserved && link->posted((u32)i).load(std::memory_order_acquire) >= lslots[i].lastSeq;
+        };
+        u64 staged = 0;
+        for (const LinkSlot& ls : lslots) staged += ls.cap;
+        for (size_t i = 0; i < lslots.size() && k < 0; ++i)
+            if (lslots[i].cap >= bytes && free(i)) k = (int)i;
+        if (k < 0 && (lslots.size() >= LinkEnd::kMaxSlots || staged + bytes > LinkEnd::kMaxStagedBytes) &&
+            !lslots.empty()) {
+            // every slot holds a message the receiver has not taken yet and
+            // no more may be added: wait (up to the link timeout) until it
+            // takes the oldest one -- messages are taken in order, so a
+            // sender that runs ahead (party 2 of a truncating asyncMul only
+            // sends) is throttled instead of failing
+            size_t oldest = lslots.size();
+            for (size_t i = 0; i < lslots.size(); ++i)
+                if (!lslots[i].reserved && (oldest == lslots.size() || lslots[i].lastSeq < lslots[oldest].lastSeq))
+                    oldest = i;
+            if (oldest == lslots.size()) throw std::runtime_error("link: every staging slot is reserved");
+            link->waitPosted((u32)oldest, lslots[oldest].lastSeq);
+        }
+        for (size_t i = 0; i < lslots.size() && k < 0; ++i)
+            if (lslots[i].cap >= bytes && free(i)) k = (int)i;
+        for (size_t i = 0; i < lslots.size() && k < 0; ++i)
+            if (free(i)) {
+                // free but too small: replace it (the receiver may still be
+                // reading the old buffer on its stream: retire, don't free)
+                k = (int)i;
+                retired.push_back(Retired{lslots[i].ptr, (u32)i, lslots[i].lastSeq});
+                lslots[i].ptr = nullptr;
+            }
+        if (k < 0) {
+            lslots.emplace_back();
+            k = (int)lslots.size() - 1;
+        }
+        LinkSlot& sl = lslots[(size_t)k];
+        if (!sl.ptr) {
+            // capacities are powers of two from 2 MiB (whole blocks: the
+            // IPC export rule, aby3g_ipc_get_handle): a slot is outgrown at
+            // most log2(largest message / 2 MiB) times, so the retired
+            // buffers behind it (kept until teardown) add up to less than
+            // its current capacity, whatever the sequence of message sizes
+            size_t cap = ipcBytes(1);
+            while (cap < bytes) cap <<= 1;
+            sl.cap = cap;
+            GPU_CALL(aby3g_malloc(&sl.ptr, sl.cap));
+            GPU_CALL(aby3g_ipc_get_handle(sl.ptr, &sl.h));
+            ++sl.gen;
+        } else if (sl.lastSeq) {
+            // the receiver's copy-out of the slot's previous message
+            GPU_CALL(aby3g_stream_wait_value(gpu.stream(), link->consumedDev((u32)k), sl.lastSeq));
+        }
+        return (u32)k;
+    }
+    // sender: a staging slot for a producer to write its message into
+    // directly (Channel::linkSendBuffer); the send then skips the copy
+    void* linkReserve(size_t bytes, Gpu& gpu) {
+        std::lock_guard<std::mutex> lk(mu);
+        const u32 k = pickSlot(std::max<size_t>(bytes, 8), gpu);
+        lslots[k].reserved = true;
+        return lslots[k].ptr;
+    }
     void linkSendDevice(const void* src, size_t bytes, Gpu& gpu) {
         std::lock_guard<std::mutex> lk(mu);
         WireMsg w{};
@@ -359,64 +427,26 @@ struct Pipe {
         w.kind = 1;
         w.slot = kNoSlot;
         w.device = gpu.device();
-        if (bytes) {
-            int k = -1;
-            u64 staged = 0;
-            for (const LinkSlot& ls : lslots) staged += ls.cap;
-            for (size_t i = 0; i < lslots.size() && k < 0; ++i)
-                if (lslots[i].cap >= bytes && link->posted((u32)i).load(std::memory_order_acquire) >= lslots[i].lastSeq)
-                    k = (int)i;
-            if (k < 0 && (lslots.size() >= LinkEnd::kMaxSlots || staged + bytes > LinkEnd::kMaxStagedBytes) &&
-                !lslots.empty()) {
-                // every slot holds a message the receiver has not taken yet and
-                // no more may be added: wait (up to the link timeout) until it
-                // takes the oldest one -- messages are taken in order, so a
-                // sender that runs ahead (party 2 of a truncating asyncMul only
-                // sends) is throttled instead of failing
-                size_t oldest = 0;
-                for (size_t i = 1; i < lslots.size(); ++i)
-                    if (lslots[i].lastSeq < lslots[oldest].lastSeq) oldest = i;
-                link->waitPosted((u32)oldest, lslots[oldest].lastSeq);
-            }
-            for (size_t i = 0; i < lslots.size() && k < 0; ++i)
-                if (lslots[i].cap >= bytes && link->posted((u32)i).load(std::memory_order_acquire) >= lslots[i].lastSeq)
-                    k = (int)i;
-            for (size_t i = 0; i < lslots.size() && k < 0; ++i)
-                if (link->posted((u32)i).load(std::memory_order_acquire) >= lslots[i].lastSeq) {
-                    // free but too small: replace it (the receiver may still be
-                    // reading the old buffer on its stream: retire, don't free)
-                    k = (int)i;
-                    retired.push_back(Retired{lslots[i].ptr, (u32)i, lslots[i].lastSeq});
-                    lslots[i].ptr = nullptr;
-                }
-            if (k < 0) {
-                lslots.emplace_back();
-                k = (int)lslots.size() - 1;
-            }
-            LinkSlot& s = lslots[(size_t)k];
-            if (!s.ptr) {
-                // capacities are powers of two from 2 MiB (whole blocks: the
-                // IPC export rule, aby3g_ipc_get_handle): a slot is outgrown at
-                // most log2(largest message / 2 MiB) times, so the retired
-                // buffers behind it (kept until teardown) add up to less than
-                // its current capacity, whatever the sequence of message sizes
-                size_t cap = ipcBytes(1);
-                while (cap < bytes) cap <<= 1;
-                s.cap = cap;
-                GPU_CALL(aby3g_malloc(&s.ptr, s.cap));
-                GPU_CALL(aby3g_ipc_get_handle(s.ptr, &s.h));
-                ++s.gen;
-            } else if (s.lastSeq) {
-                // the receiver's copy-out of the slot's previous message
-                GPU_CALL(aby3g_stream_wait_value(gpu.stream(), link->consumedDev((u32)k), s.lastSeq));
-            }
-            GPU_CALL(aby3g_memcpy(s.ptr, src, bytes, 2, gpu.stream()));
-            s.lastSeq = ++devSeq;
-            GPU_CALL(aby3g_stream_write_value(gpu.stream(), link->readyDev(), s.lastSeq));
+        int k = -1;
+        for (size_t i = 0; i < lslots.size() && k < 0; ++i)
+            if (lslots[i].reserved && lslots[i].ptr == src) k = (int)i;
+        if (k >= 0) {
+            // produced in place (linkReserve): no copy
+            if (bytes > lslots[(size_t)k].cap) throw std::runtime_error("link: message larger than its reserved slot");
+            lslots[(size_t)k].reserved = false;
+            if (!bytes) k = -1;
+        } else if (bytes) {
+            k = (int)pickSlot(bytes, gpu);
+            GPU_CALL(aby3g_memcpy(lslots[(size_t)k].ptr, src, bytes, 2, gpu.stream()));
+        }
+        if (k >= 0) {
+            LinkSlot& sl = lslots[(size_t)k];
+            sl.lastSeq = ++devSeq;
+            GPU_CALL(aby3g_stream_write_value(gpu.stream(), link->readyDev(), sl.lastSeq));
             w.slot = (u32)k;
-            w.gen = s.gen;
-            w.seq = s.lastSeq;
-            w.handle = s.h;
+            w.gen = sl.gen;
+            w.seq = sl.lastSeq;
+            w.handle = sl.h;
         }
         sent += bytes;
         ringWrite(std::vector<u8>((const u8*)&w, (const u8*)&w + sizeof w));
@@ -819,6 +849,13 @@ void Channel::asyncSendShared(std::shared_ptr<DeviceBuffer> buf, size_t bytes, G
     m.hsFlags = posted.flags;
     m.hsSeq = posted.seq;
     mOut->push(std::move(m));
+}
+
+std::shared_ptr<DeviceBuffer> Channel::linkSendBuffer(Gpu& gpu, size_t bytes) {
+    if (!mOut) throw std::runtime_error("channel not connected");
+    if (!mOut->link) return std::make_shared<DeviceBuffer>(gpu, std::max<size_t>(bytes, 8));
+    GPU_CALL(aby3g_set_device(gpu.device()));
+    return DeviceBuffer::borrow(mOut->linkReserve(bytes, gpu), std::max<size_t>(bytes, 8), &gpu);
 }
 
 RecvFuture Channel::asyncRecvShared(size_t bytes, Gpu& gpu) {

@@ -83,6 +83,15 @@ public:
     // messages keep the signal word (C3 0.313-0.315 vs 0.323 ms with events)
     void asyncSendSharedEvent(std::shared_ptr<DeviceBuffer> buf, size_t bytes, Gpu& gpu);
     RecvFuture asyncRecvShared(size_t bytes, Gpu& gpu);
+    // A buffer for a message this party is about to produce and then send
+    // with asyncSendShared / asyncSendSharedEvent on this channel. Between
+    // processes it is one of the direction's IPC-exported staging slots, so
+    // the send skips the staging copy (the producer writes the slot itself,
+    // ordered behind the receiver's copy-out of the slot's previous message);
+    // otherwise a buffer of this party's pool. It must be sent on this
+    // channel before the next linkSendBuffer; it may also go to other
+    // channels (they stage a copy) and be read by this party.
+    std::shared_ptr<DeviceBuffer> linkSendBuffer(Gpu& gpu, size_t bytes);
     // In-kernel hand-off of the next zero-copy message (co-located parties on
     // one device whose ring was made with kernel hand-offs): the flags and
     // sequence number for the producing kernel to publish a message of `rows`

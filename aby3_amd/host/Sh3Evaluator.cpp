@@ -121,8 +121,12 @@ Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, const si64Matrix& A, const si64Matri
             si64Matrix& C = tmp ? *tmp : Cref;
             C.resize(M, N);
             // z = product - r is revealed to P0 and P1 zero-copy: the buffer
-            // itself is the message (Channel::asyncSendShared)
-            auto z = std::make_shared<DeviceBuffer>(g, bytes);
+            // itself is the message (Channel::asyncSendShared); between
+            // processes it is produced straight into a staging slot of the
+            // first channel it goes to (linkSendBuffer: no staging copy)
+            const u64 pIdx = self.getRuntime().mPartyIdx;
+            const bool toNext = (pIdx + 1) % 3 < 2;
+            auto z = (toNext ? comm.mNext : comm.mPrev).linkSendBuffer(g, bytes);
             size_t wsBytes = 0;
             void* ws = workspace(mode, M, K, N, wsBytes, g);
             if (DEBUG_disable_randomization) {
@@ -149,7 +153,7 @@ Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, const si64Matrix& A, const si64Matri
             // reveal z to parties 0 and 1 (:681-684)
             const u64 p = self.getRuntime().mPartyIdx;
             const u64 next = (p + 1) % 3, prev = (p + 2) % 3;
-            if (next < 2) comm.mNext.asyncSendSharedEvent(z, bytes, g);
+            if (next < 2) comm.mNext.asyncSendSharedEvent(z, bytes, g);  // z's own channel first (toNext)
             if (prev < 2) comm.mPrev.asyncSendSharedEvent(z, bytes, g);
             if (p < 2) {
                 auto fu0 = comm.mNext.asyncRecvShared(bytes, g);

@@ -1,5 +1,6 @@
 #include "Channel.h"
 #include "Link.h"
+#include <cstdio>
 #include <cstring>
 #include <chrono>
 #include <cstdlib>
@@ -228,6 +229,13 @@ struct Pipe {
 
     ~Pipe() {
         stopWriter();
+        if (link && getenv("ABY3_LINK_STATS")) {
+            u64 gens = 0;
+            for (const LinkSlot& ls : lslots) gens += ls.gen;
+            std::fprintf(stderr, "link %s: %zu slots (%llu buffers made), %zu retired, %zu openings, %llu msgs sent\n",
+                         link->sender() ? "out" : "in", lslots.size(), (unsigned long long)gens, retired.size(),
+                         mapped.size(), (unsigned long long)devSeq);
+        }
         if (link) {
             aby3g_set_device(linkDevice);
             aby3g_device_sync();
@@ -850,6 +858,8 @@ void Channel::asyncSendShared(std::shared_ptr<DeviceBuffer> buf, size_t bytes, G
     m.hsSeq = posted.seq;
     mOut->push(std::move(m));
 }
+
+bool Channel::linked() const { return mOut && mOut->link; }
 
 std::shared_ptr<DeviceBuffer> Channel::linkSendBuffer(Gpu& gpu, size_t bytes) {
     if (!mOut) throw std::runtime_error("channel not connected");

@@ -92,6 +92,7 @@ public:
     // channel before the next linkSendBuffer; it may also go to other
     // channels (they stage a copy) and be read by this party.
     std::shared_ptr<DeviceBuffer> linkSendBuffer(Gpu& gpu, size_t bytes);
+    bool linked() const;  // the outgoing direction leads to another process
     // In-kernel hand-off of the next zero-copy message (co-located parties on
     // one device whose ring was made with kernel hand-offs): the flags and
     // sequence number for the producing kernel to publish a message of `rows`

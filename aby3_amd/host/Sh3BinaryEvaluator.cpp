@@ -134,6 +134,7 @@ void Sh3BinaryEvaluator::setCir(BetaCircuit* cir, u64 width, block prevSeed, blo
     releaseZ();
     mSendAll.reset();
     mArenaLease.reset();
+    mPerLevelSends = false;
     mAndDone = 0;
     const u64 zWords = (u64)cir->mAndCount * mWords;
     if (zWords) {
@@ -454,6 +455,16 @@ void Sh3BinaryEvaluator::setReplicatedInput(u64 i, const sbMatrix& in) {
     mLevel = 0;
 }
 
+// ABY3_LEVEL_SLOTS=0: a level's sends between processes without an arena
+// are staged copies out of one evaluation buffer (A/B runs)
+static bool levelSlotSends() {
+    static const bool on = [] {
+        const char* e = getenv("ABY3_LEVEL_SLOTS");
+        return !e || e[0] != '0';
+    }();
+    return on;
+}
+
 void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
     if (mLevel > mCir->mLevelCounts.size())
         throw std::runtime_error("evaluateRound() was called but no rounds remain... " LOCATION);
@@ -481,19 +492,29 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
     if (mLevel == 0 && mAndDone) {  // evaluated again after setCir: a fresh send buffer
         mSendAll.reset();
         mArenaLease.reset();
+        mPerLevelSends = false;
         mAndDone = 0;
     }
     std::shared_ptr<DeviceBuffer> send;
     if (nAnd) {
-        if (!mSendAll) {
-            // between processes on one GPU, the evaluation's messages live in
-            // the channel's IPC-mapped arena, read in place by the receiver
+        if (!mSendAll && !mPerLevelSends) {
+            // the evaluation's first AND level: between processes on one GPU
+            // its messages live in the channel's IPC-mapped arena, read in
+            // place by the receiver; between processes without an arena each
+            // level's AND shares are produced straight into a staging slot of
+            // the link (no staging copy); else one buffer of this party
             u64 andLevels = 0;
             for (u32 c : mCir->mLevelAndCounts) andLevels += c != 0;
             mSendAll = comm.mNext.evalSendBuffer(g, (u64)mCir->mAndCount * rowBytes, andLevels, &mArenaLease);
-            if (!mSendAll) mSendAll = std::make_shared<DeviceBuffer>(g, (u64)mCir->mAndCount * rowBytes);
+            if (!mSendAll) {
+                if (comm.mNext.linked() && levelSlotSends())
+                    mPerLevelSends = true;
+                else
+                    mSendAll = std::make_shared<DeviceBuffer>(g, (u64)mCir->mAndCount * rowBytes);
+            }
         }
-        send = DeviceBuffer::view(mSendAll, mAndDone * rowBytes, nAnd * rowBytes);
+        send = mPerLevelSends ? comm.mNext.linkSendBuffer(g, nAnd * rowBytes)
+                              : DeviceBuffer::view(mSendAll, mAndDone * rowBytes, nAnd * rowBytes);
     }
     mAndDone += nAnd;
     // this level's bytes (about 72 per gate and 64-row word)

@@ -131,6 +131,7 @@ private:
     // held while mSendAll is the channel's arena slot (Channel::evalSendBuffer);
     // dropped with mSendAll, after the evaluation's last message, or with this
     std::shared_ptr<void> mArenaLease;
+    bool mPerLevelSends = false;  // each level's sends in a staging slot of the link (Channel::linkSendBuffer)
     // setInputs' sources held for the first level's launch (DevCircuit::fuseInputs)
     std::vector<aby3g_wire_src> mPendingIn;
     // buffers the held sources read (e.g. a received message): kept alive

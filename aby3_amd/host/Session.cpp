@@ -22,6 +22,16 @@ namespace aby3 {
 namespace {
 thread_local std::string t_err;
 
+// one party per process on a shared GPU: the binary engine's AND-mask draws
+// on a second stream of the process (ABY3_PARTY_DRAW_STREAM=1, A/B runs)
+static bool partyDrawStream() {
+    static const bool on = [] {
+        const char* e = getenv("ABY3_PARTY_DRAW_STREAM");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 // co-located parties plan each share GEMM for 1/k of the CUs (k = 3 by
 // default; ABY3_GEMM_SHARING=1: full-chip plans, for A/B runs)
 static int colocatedGemmSharing() {
@@ -598,7 +608,7 @@ struct Session {
                 {
                     std::unique_lock<std::mutex> lk(turnMu);
                     turnCv.wait(lk, [&] { return turnNext > locals.back(); });
-                    if (colocated && locals.size() > 1) {
+                    if (colocated && (locals.size() > 1 || partyDrawStream())) {
                         auto& slot = drawStreams[device];
                         if (!slot) slot = std::make_shared<Gpu::SharedStream>(device);
                         ds = slot;

@@ -218,6 +218,16 @@ __global__ void __launch_bounds__(kBlock, 4) k_pubmul_helper(const u32* __restri
 
 }  // namespace
 
+// the share draws' workgroup cap for this thread (aby3g_set_draw_workgroups):
+// 256 (one per CU) beside co-located parties' work, more for a party alone
+// on its stream (one party per process), where the draws stand in its path
+thread_local u32 t_draw_wgs = 256;
+inline u32 aes_grid_wide(u64 items, u32 block, u32 cap) {
+    u64 g = (items + block - 1) / block;
+    if (g > cap) g = cap;
+    return (u32)(g ? g : 1);
+}
+
 void share_draws_launch(int kind, const u8* kprev, const u8* knext, u64 base, u64 n, const i64* addend, i64* out0,
                         i64* out1, hipStream_t s, int family) {
     ABY3G_REQUIRE(kind >= 0 && kind <= 2, "bad draw kind");
@@ -230,7 +240,7 @@ void share_draws_launch(int kind, const u8* kprev, const u8* knext, u64 base, u6
     // and fewer 64 KiB-LDS workgroups leave the levels more CUs (C3
     // 0.2999-0.3024 against 0.3088-0.3115 ms with aes_grid's 512, same box;
     // 128 measured 0.344-0.352)
-    const u32 grid = std::min<u32>(aes_grid(counters, kBlock), 256);
+    const u32 grid = std::min<u32>(aes_grid_wide(counters, kBlock, t_draw_wgs), t_draw_wgs);
     launch(family, k_share_draws, dim3(grid), dim3(kBlock), 0, s, aes_table(), kk, kind, base, n, addend, out0, out1);
 }
 
@@ -258,6 +268,13 @@ int aby3g_prng_fill(const uint8_t seed[16], uint64_t byte_off, uint64_t nbytes, 
         u64 counters = ((w0 + n - 1) >> 1) - (w0 >> 1) + 1;
         launch(PROBE_AES, k_prng_words, dim3(aes_grid(counters, kBlock)), dim3(kBlock), 0, S(stream),
                aes_table(), k, w0, n, (u64*)out);
+    });
+}
+
+int aby3g_set_draw_workgroups(int cap) {
+    return guarded([&] {
+        ABY3G_REQUIRE(cap >= 1 && cap <= 4096, "workgroup cap must be 1 .. 4096");
+        t_draw_wgs = (u32)cap;
     });
 }
 

@@ -32,6 +32,17 @@ static bool partyDrawStream() {
     return on;
 }
 
+// the share-draw workgroup cap of a party alone in its process
+// (aby3g_set_draw_workgroups; ABY3_PARTY_DRAW_WGS for A/B runs)
+static int partyDrawWorkgroups() {
+    static const int n = [] {
+        const char* e = getenv("ABY3_PARTY_DRAW_WGS");
+        const int v = e && *e ? atoi(e) : 512;
+        return v >= 1 && v <= 4096 ? v : 512;
+    }();
+    return n;
+}
+
 // co-located parties plan each share GEMM for 1/k of the CUs (k = 3 by
 // default; ABY3_GEMM_SHARING=1: full-chip plans, for A/B runs)
 static int colocatedGemmSharing() {
@@ -635,6 +646,9 @@ struct Session {
             }
             if (probe) GPU_CALL(aby3g_probe_enable_mask((u32)probe));
             p.ownProcess = locals.size() == 1;
+            // one party per process: its AND-mask draws run on its own stream
+            // in front of its first level, so they take more of the chip
+            if (p.ownProcess) GPU_CALL(aby3g_set_draw_workgroups(partyDrawWorkgroups()));
             job->setup(p);
             p.checkpoint("the job's setup");
             p.rt.gpu().sync();

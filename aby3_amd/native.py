@@ -81,6 +81,7 @@ _SIGS = {
     "aby3g_last_error": (c_char_p, []),
     "aby3g_version": (c_int, []),
     "aby3g_recent_calls": (c_int, [c_char_p, c_size_t]),
+    "aby3g_set_draw_workgroups": (c_int, [c_int]),
     "aby3g_device_count": (c_int, [POINTER(c_int)]),
     "aby3g_set_device": (c_int, [c_int]),
     "aby3g_get_device": (c_int, [POINTER(c_int)]),

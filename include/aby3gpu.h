@@ -196,6 +196,11 @@ int aby3g_aes_ctr_host(const uint8_t key[16], uint64_t ctr_base, uint64_t nblock
  * Sh3BinaryEvaluator.h:96-102, Sh3Evaluator.cpp:151-153,188,234-235). */
 int aby3g_prng_fill(const uint8_t seed[16], uint64_t byte_off, uint64_t nbytes, void* out, aby3g_stream stream);
 
+/* The calling thread's cap on the workgroups of aby3g_share_draws (default
+ * 256, one per CU: the draws run beside co-located parties' work). A party
+ * alone on its stream (one party per process) raises it: its draws stand in
+ * front of its own first level. (No reference counterpart.) */
+int aby3g_set_draw_workgroups(int cap);
 /* Sh3ShareGen draws j = draw_base .. draw_base+n-1 with the two zero-share
  * keys (k_prev = mShareGen[0], k_next = mShareGen[1]; Sh3ShareGen.h:19-20).
  *   ABY3G_DRAW_ARITH:    out0[i] = getShare()       (+ addend[i])   Sh3ShareGen.h:60-75

@@ -10,6 +10,8 @@ import re
 import sys
 
 O = sys.argv[1]
+# the kernel launched once per step by every party (steps are counted by it)
+STEP_KERNEL = sys.argv[2] if len(sys.argv) > 2 else "k_bin_level_in"
 rows = []
 for p in range(3):
     f = glob.glob(os.path.join(O, f"p{p}", "**", "*kernel_trace.csv"), recursive=True)
@@ -30,13 +32,13 @@ span = (t_hi - t_lo) / 1e3
 fam = collections.defaultdict(float)
 for s, e, p, k in win:
     fam[(p, k)] += (e - s) / 1e3
-nsteps = span / 1e3 / ms if ms else 1
-print(f"window {span:.0f} us (~{nsteps:.1f} steps); kernel us per step by party:")
+steps_p = collections.Counter(p for s, e, p, k in win if k == STEP_KERNEL)
+print(f"window {span:.0f} us; kernel us per step by party (steps counted by {STEP_KERNEL}):")
 for (p, k), us in sorted(fam.items(), key=lambda x: (x[0][0], -x[1])):
-    print(f"  party {p} {k:32s} {us / nsteps:8.1f}")
+    print(f"  party {p} {k:32s} {us / max(1, steps_p[p]):8.1f}")
 print("\ntimeline (first 2 steps of the window):")
 t0 = win[0][0]
 for s, e, p, k in win:
     if s - t0 > 2 * ms * 1e6:
-        break
+        break  # ms per step * 1e6 = ns per step
     print(f"{(s - t0) / 1e3:9.1f} us {(e - s) / 1e3:8.1f} us  P{p}  {k}")

@@ -37,15 +37,20 @@ def test_host_runtime_sanitized(tmp_path, sanitizer):
     assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-4000:]
 
 
-def test_party_processes_sanitized(tmp_path):
+@pytest.mark.parametrize("sanitizer", ["address", "thread"])
+def test_party_processes_sanitized(tmp_path, sanitizer):
     """Three processes, one party each (aby3h_party_create): every job over
-    the shared-memory links and IPC staging slots, under AddressSanitizer."""
-    exe = _build(str(tmp_path), "address", "party_procs.cpp")
-    # 1 MiB hand-off arenas: the null device's shared memory is a 1 GiB bump allocator
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1", ABY3_LINK_TIMEOUT_S="60", ABY3_ARENA_MB="1")
+    the shared-memory links and IPC staging slots in the three layouts, under
+    AddressSanitizer and ThreadSanitizer (each process's party thread, link
+    writer threads and link watchdog)."""
+    exe = _build(str(tmp_path), sanitizer, "party_procs.cpp")
+    # 1 MiB hand-off arenas: the null device's shared memory is a bump allocator
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1", TSAN_OPTIONS="halt_on_error=1",
+               ABY3_LINK_TIMEOUT_S="60", ABY3_ARENA_MB="1")
     r = subprocess.run([exe], capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
     assert "party_procs: ok" in r.stdout
+    assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-4000:]
 
 
 def test_party_failure_ends_peers_fast(tmp_path):

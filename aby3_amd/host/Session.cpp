@@ -36,9 +36,12 @@ static bool partyDrawStream() {
 // (aby3g_set_draw_workgroups; ABY3_PARTY_DRAW_WGS for A/B runs)
 static int partyDrawWorkgroups() {
     static const int n = [] {
+        // 256 (one per CU), as beside co-located parties: 512 and 1024
+        // measured no faster for C3 / C5 as three processes on one GPU
+        // (0.359 / 0.363-0.367 against 0.355-0.360 ms; C5 70.7-71.4 against 69.7-71.0 ms)
         const char* e = getenv("ABY3_PARTY_DRAW_WGS");
-        const int v = e && *e ? atoi(e) : 512;
-        return v >= 1 && v <= 4096 ? v : 512;
+        const int v = e && *e ? atoi(e) : 256;
+        return v >= 1 && v <= 4096 ? v : 256;
     }();
     return n;
 }

@@ -65,6 +65,12 @@ int main() {
     std::printf("cross-device: peer pairs 0x%x, %lu copies between devices\n", peers, kind3);
     std::vector<int64_t> a(64 * 48, 3), b(48 * 80, 5), sh(6 * 64 * 80), pl(64 * 80);
     if (aby3h_sim_mul(0, 1, 1, 16, a.data(), b.data(), 64, 48, 80, sh.data(), pl.data())) return fail("sim_mul");
+    // empty shapes: no rows, no inner dimension (a zero product, then truncated), no columns
+    for (const auto& s3 : {std::vector<uint64_t>{0, 5, 7}, {5, 0, 7}, {5, 7, 0}}) {
+        for (int trunc = 0; trunc < 2; ++trunc)
+            if (aby3h_sim_mul(0, 1, trunc, 16, a.data(), b.data(), s3[0], s3[1], s3[2], sh.data(), pl.data()))
+                return fail("sim_mul (empty shape)");
+    }
     std::vector<int64_t> x(300, 1), y(300, 2), o(300), osh(6 * 300);
     if (aby3h_sim_cipher_gt(0, x.data(), y.data(), 300, o.data(), osh.data())) return fail("sim_cipher_gt");
     // the merge network: general shapes (padding, explicit row lists) and

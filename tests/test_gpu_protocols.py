@@ -35,6 +35,12 @@ MUL_CASES = [
     (1, True, 27, 128, 256, 1),      # LR: X_B^T err >> (D + aB)
     (0, True, 8, 31, 9, 1),
     (1, True, 16, 256, 256, 256),
+    # empty shapes (Eigen's empty matrices in the reference): no rows, no
+    # columns, and no inner dimension -- a zero product, then the truncation
+    (1, False, 0, 0, 5, 7),
+    (1, False, 0, 5, 7, 0),
+    (1, True, 16, 5, 0, 7),
+    (0, True, 8, 0, 3, 3),
 ]
 
 

@@ -170,7 +170,7 @@ int main(int argc, char** argv) {
             std::printf("\n  ");
         }
         std::vector<double> gap;  // launch-to-launch gap: end of t-1 to start of t
-        for (u64 t = iters / 2; t < iters; ++t) gap.push_back(0.01 * (double)(stamps[p][S * t] - stamps[p][96 * (t - 1) + 11]));
+        for (u64 t = iters / 2; t < iters; ++t) gap.push_back(0.01 * (double)(stamps[p][S * t] - stamps[p][S * (t - 1) + 11]));
         std::sort(gap.begin(), gap.end());
         std::printf(" total %.1f us, gap between launches %.1f us\n", tot, gap[gap.size() / 2]);
     }

@@ -136,6 +136,8 @@ void Sh3BinaryEvaluator::setCir(BetaCircuit* cir, u64 width, block prevSeed, blo
     mArenaLease.reset();
     mPerLevelSends = false;
     mAndDone = 0;
+    mZByLevel = false;
+    mZDrawn = 0;
     const u64 zWords = (u64)cir->mAndCount * mWords;
     if (zWords) {
         mZStream = g.drawStream() ? g.drawStream() : g.aux();
@@ -171,14 +173,48 @@ void Sh3BinaryEvaluator::setCir(BetaCircuit* cir, u64 width, block prevSeed, blo
             mZFresh->record(g.stream());
             GPU_CALL(aby3g_stream_wait_event(mZStream, mZFresh->get()));
         }
-        GPU_CALL(aby3g_share_draws(ABY3G_DRAW_BIN, mKeyPrev.data(), mKeyNext.data(), 0, zWords, nullptr,
-                                   (i64*)mZPtr, nullptr, mZStream));
+        mZByLevel = !other && levelDraws() != 0;
+        if (mZByLevel)
+            drawZThrough(0);  // the first AND level's masks; the rest behind each level's launch
+        else
+            GPU_CALL(aby3g_share_draws(ABY3G_DRAW_BIN, mKeyPrev.data(), mKeyNext.data(), 0, zWords, nullptr,
+                                       (i64*)mZPtr, nullptr, mZStream));
         if (other) {
             if (!mZEv) mZEv = std::make_unique<Event>();
             mZEv->record(mZStream);
         }
         mZPending = true;
     }
+}
+
+// Where a party alone on its stream draws an evaluation's masks
+// (ABY3_LEVEL_DRAWS, A/B runs): 0 all in setCir; 1 the first AND level's in
+// setCir, each later level's behind the launch before it; 2 (default) the
+// first AND level's in setCir, all the others behind its launch. Three party
+// processes on one GPU, same box: C3 0.3326-0.3367 ms with 2, 0.3455-0.3499
+// with 1, 0.3526-0.3541 with 0; C5 64.8-65.4 / 68.3-68.6 / 65.2-65.9 ms (one
+// more launch per level costs the sort's many small evaluations more than
+// it hides).
+int Sh3BinaryEvaluator::levelDraws() {
+    static const int mode = [] {
+        const char* e = getenv("ABY3_LEVEL_DRAWS");
+        return e && *e ? atoi(e) : 2;
+    }();
+    return mode;
+}
+
+void Sh3BinaryEvaluator::drawZThrough(u64 level) {
+    // masks of the AND gates of levels 0 .. L, where L is the first level at
+    // or after `level` with AND gates (z rows are AND ordinals in level order)
+    const auto& c = mCir->mLevelAndCounts;
+    u64 end = 0, L = 0;
+    for (; L < c.size() && (L < level || !c[L]); ++L) end += c[L];
+    if (L < c.size()) end += c[L];
+    if (end <= mZDrawn) return;
+    GPU_CALL(aby3g_share_draws(ABY3G_DRAW_BIN, mKeyPrev.data(), mKeyNext.data(), mZDrawn * mWords,
+                               (end - mZDrawn) * mWords, nullptr, (i64*)(mZPtr + mZDrawn * mWords), nullptr,
+                               mZStream));
+    mZDrawn = end;
 }
 
 void Sh3BinaryEvaluator::waitZ() {
@@ -519,6 +555,7 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
     mAndDone += nAnd;
     // this level's bytes (about 72 per gate and 64-row word)
     if (nAnd) hp = comm.mNext.handoffPost(g, mRows, (u64)mCir->mLevelCounts[mLevel] * mWords * 72, send->data());
+    if (nAnd && mZByLevel) drawZThrough(mLevel);  // (drawn behind the previous level's launch)
     if (nb && mZPending) waitZ();
     // the first level with its inputs (aby3g_bin_level_in) when the held
     // sources make up every input wire (an input set another way lives in
@@ -553,6 +590,10 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
         // the evaluation's last message is sent: the arena may serve the next one
         if (mAndDone == mCir->mAndCount) mArenaLease.reset();
     }
+    // a party alone on its stream: the later levels' masks run here, after
+    // this level's send, while the peers' messages for the next level are
+    // still in flight, instead of all in front of the first level
+    if (mZByLevel) drawZThrough(levelDraws() == 2 ? mCir->mLevelAndCounts.size() : mLevel + 1);
     ++mLevel;
     if (hasMoreRounds()) task.then([this](CommPkg& c, Sh3Task& t) { roundCallback(c, t); }, "callback");
 }

@@ -2,8 +2,8 @@
 //
 // Memory: one device allocation [2][wires][words] (wire-major, 64 rows per
 // u64, rows padded to a multiple of 2048 as mMem.reset(width, wires, 8)).
-// AND masks: all z words of the circuit are generated on device before the
-// first round (they depend only on the setCir keys), z[k][w] = draw
+// AND masks: the z words of the circuit are generated on device before the
+// rounds that use them (they depend only on the setCir keys), z[k][w] = draw
 // k*words + w of the (prev, next) keys -- exactly getShares()'s counter
 // schedule (Sh3BinaryEvaluator.cpp:1406-1434).
 // One communication round per AND level, as roundCallback (:539-1196):
@@ -144,6 +144,15 @@ private:
     bool pendingCoversInputs() const;
     int mZSlot = -1;
     aby3g_stream mZStream = nullptr;     // the stream the masks are drawn on
+    // Masks drawn on the party's own stream (no draw stream: one party per
+    // process) are drawn in pieces: the first AND level's in setCir, the
+    // later levels' behind the first level's launch and send, where the
+    // stream would otherwise idle until the peers' shares arrive
+    // (levelDraws()).
+    bool mZByLevel = false;
+    u64 mZDrawn = 0;  // AND rows (ordinals) whose masks are enqueued
+    static int levelDraws();
+    void drawZThrough(u64 level);
     std::unique_ptr<Event> mZEv, mZFresh; // draws done / main stream's position for fresh memory
     void waitZ();      // main stream waits for the draws
     // the ring slot is free once the main stream passes this point (at the

@@ -1,7 +1,7 @@
 /*
  * aby3.h -- C entry points of the host runtime (aby3_amd/lib/libaby3.so),
  * for drivers that are not C++ (bench.py, the Python tests, a cgo/ctypes
- * binding). The C++ API itself is aby3_amd/host/*.h (namespace aby3),
+ * binding). The C++ API itself is the headers under aby3_amd/host/ (namespace aby3),
  * mirroring the reference's Sh3Runtime / Sh3Encryptor / Sh3Evaluator /
  * Sh3BinaryEvaluator / Sh3Piecewise classes.
  *

@@ -114,24 +114,45 @@ struct MulJob : Job {
     // into its own output matrix), so one product's reshare round overlaps
     // the next one's share GEMM on the party's stream
     u64 inflight;
+    // rows [r0, r1) of the M-row product (a row split): A's
+    // slice shared and multiplied with the whole product's randomness taken
+    u64 r0 = 0, r1 = 0;
     i64Matrix a, b;
     si64Matrix A[3], B[3], C[3][2];
     std::deque<Sh3Task> pending[3];
     int slot[3] = {0, 0, 0};
     int last[3] = {0, 0, 0};
-    MulJob(u64 m, u64 k, u64 n, u64 d, MulMode md, bool t, u64 inf = 1)
+    MulJob(u64 m, u64 k, u64 n, u64 d, MulMode md, bool t, u64 inf = 1, u64 shard = 0, u64 shards = 1)
         : M(m), K(k), N(n), D(d), mode(md), trunc(t), inflight(inf < 1 ? 1 : inf > 2 ? 2 : inf) {
+        if (shards < 1 || shard >= shards)
+            throw std::invalid_argument("row split: shard " + std::to_string(shard) + " of " + std::to_string(shards));
+        if (shards > 1 && (mode != MulMode::Gemm || !trunc))
+            throw std::invalid_argument("row split: the truncated GEMM product only");
+        r0 = M * shard / shards;
+        r1 = M * (shard + 1) / shards;
         const u64 br = mode == MulMode::Gemm ? K : M, bc = mode == MulMode::Gemm ? N : K;
         // fixed-point operands in [-8, 8) * 2^D
         const i64 bound = trunc ? (8ll << D) : 0;
         a = randomMat(M, K, 1, bound);
         b = randomMat(br, bc, 2, bound);
     }
+    bool split() const { return r1 - r0 != M; }
     void setup(PartyCtx& p) override {
         const u64 br = mode == MulMode::Gemm ? K : M, bc = mode == MulMode::Gemm ? N : K;
-        A[p.idx].resize(M, K);
+        A[p.idx].resize(r1 - r0, K);
         B[p.idx].resize(br, bc);
-        if (p.idx == 0) {
+        if (split()) {
+            // this slice's rows of A (the whole matrix's draws taken), all of B
+            if (p.idx == 0) {
+                i64Matrix rows(r1 - r0, K);
+                if (r1 > r0) std::memcpy(rows.data(), a.data() + r0 * K, (r1 - r0) * K * sizeof(i64));
+                p.enc.localIntMatrixRows(p.rt, rows, A[0], r0, M).get();
+                p.enc.localIntMatrix(p.rt, b, B[0]).get();
+            } else {
+                p.enc.remoteIntMatrixRows(p.rt, A[p.idx], r0, M).get();
+                p.enc.remoteIntMatrix(p.rt, B[p.idx]).get();
+            }
+        } else if (p.idx == 0) {
             p.enc.localIntMatrix(p.rt, a, A[0]).get();
             p.enc.localIntMatrix(p.rt, b, B[0]).get();
         } else {
@@ -144,8 +165,9 @@ struct MulJob : Job {
         si64Matrix& c = C[i][slot[i]];
         last[i] = slot[i];
         slot[i] = (slot[i] + 1) % (int)inflight;
-        pending[i].push_back(trunc ? p.eval.asyncMul(p.rt, A[i], B[i], c, D, mode)
-                                   : p.eval.asyncMul(p.rt, A[i], B[i], c, mode));
+        pending[i].push_back(split()  ? p.eval.asyncMulRows(p.rt, A[i], B[i], c, D, r0, M)
+                             : trunc ? p.eval.asyncMul(p.rt, A[i], B[i], c, D, mode)
+                                     : p.eval.asyncMul(p.rt, A[i], B[i], c, mode));
         if (pending[i].size() >= inflight) {
             pending[i].front().get();
             pending[i].pop_front();
@@ -165,15 +187,15 @@ struct MulJob : Job {
         if (p.idx != 0) return true;
         // spot-check 64 entries against the plaintext product
         u64 x = 99;
-        for (int t = 0; t < 64; ++t) {
-            const u64 i = xorshift(x) % M, j = xorshift(x) % N;
+        for (int t = 0; t < 64 && r1 > r0; ++t) {
+            const u64 i = r0 + xorshift(x) % (r1 - r0), j = xorshift(x) % N;
             __int128 s = 0;
             if (mode == MulMode::Gemm)
                 for (u64 k = 0; k < K; ++k) s += (__int128)a(i, k) * b(k, j);
             else
                 s = (__int128)a(i, j) * b(i, j);
             const i64 exact = (i64)(u64)s;
-            const i64 got = r(i, j);
+            const i64 got = r(i - r0, j);
             if (trunc) {
                 const i64 e = (i64)(s >> D);
                 if (got - e > 1 || e - got >= 4) return false;
@@ -184,7 +206,7 @@ struct MulJob : Job {
         return true;
     }
     void info(double* o) override {
-        o[ABY3H_INFO_MULTS_PER_STEP] = mode == MulMode::Gemm ? (double)M * N * K : (double)M * N;
+        o[ABY3H_INFO_MULTS_PER_STEP] = mode == MulMode::Gemm ? (double)(r1 - r0) * N * K : (double)M * N;
         o[ABY3H_INFO_GEMM_INT8_OPS] = mode == MulMode::Gemm ? 144.0 * M * N * K : 0;
     }
     const SharedMat* result(int i) const override { return &C[i][last[i]]; }
@@ -543,6 +565,7 @@ struct Session {
     int probeFamily = 0;
     bool checkOk = true;
     u64 digests[3] = {0, 0, 0};
+    std::vector<i64> results[3][2];  // command 8: each party's result shares on the host
     std::vector<CommPkg> comms;
     double hostEnqueueUs[3] = {0, 0, 0}, hostDrainUs[3] = {0, 0, 0}, hostRecvWaitUs[3] = {0, 0, 0};
     size_t poolCached[3] = {0, 0, 0};  // each party's cached pool bytes after its last run
@@ -717,6 +740,13 @@ struct Session {
                     // wait on a peer, so trim's device-wide wait cannot block
                     p.rt.gpu().trim();
                     poolCached[i] = 0;
+                } else if (c == 8) {
+                    const SharedMat* r = job->result(i);
+                    std::vector<i64> v[2];
+                    if (r && !r->empty())
+                        for (int sh = 0; sh < 2; ++sh) v[sh] = r->shareToHost(sh);
+                    std::lock_guard<std::mutex> lk(mu);
+                    for (int sh = 0; sh < 2; ++sh) results[i][sh] = std::move(v[sh]);
                 } else if (c == 6) {
                     const SharedMat* r = job->result(i);
                     u64 h = 0xcbf29ce484222325ull;  // FNV-1a over both shares' bytes
@@ -771,7 +801,8 @@ std::unique_ptr<Job> makeJob(int job, const uint64_t* params, int nparams) {
     switch (job) {
         case ABY3H_JOB_MUL_TRUNC:
             return std::make_unique<MulJob>(P(0, 1024), P(1, 1024), P(2, 1024), P(3, 16),
-                                            P(4, 1) ? MulMode::Gemm : MulMode::Hadamard, true, P(5, 1));
+                                            P(4, 1) ? MulMode::Gemm : MulMode::Hadamard, true, P(5, 1), P(6, 0),
+                                            P(7, 1));
         case ABY3H_JOB_MUL:
             return std::make_unique<MulJob>(P(0, 128), P(1, 128), P(2, 128), 0, P(3, 0) ? MulMode::Gemm : MulMode::Hadamard,
                                             false);
@@ -949,6 +980,28 @@ int aby3h_session_info(aby3h_session* h, double* out, int n) {
     for (int l : h->s.locals) dw += h->s.deviceWaitUs[l];
     tmp[ABY3H_INFO_DEVICE_WAIT_US] = dw / (double)h->s.locals.size();
     for (int i = 0; i < n && i < ABY3H_INFO_COUNT; ++i) out[i] = tmp[i];
+    return 0;
+}
+
+int aby3h_session_result(aby3h_session* h, int party, int share, int64_t* out, uint64_t count,
+                         uint64_t* elements) {
+    Session& s = h->s;
+    if (std::find(s.locals.begin(), s.locals.end(), party) == s.locals.end()) {
+        t_err = "result: party " + std::to_string(party) + " is not run by this session";
+        return 1;
+    }
+    if (share < 0 || share > 1 || !elements || (count && !out)) {
+        t_err = "result: share must be 0 or 1, elements and (for count > 0) out non-null";
+        return 1;
+    }
+    s.command(8);
+    if (!s.err.empty()) {
+        t_err = s.err;
+        return 1;
+    }
+    const std::vector<i64>& v = s.results[party][share];
+    *elements = v.size();
+    if (count) std::memcpy(out, v.data(), std::min<u64>(count, v.size()) * sizeof(i64));
     return 0;
 }
 

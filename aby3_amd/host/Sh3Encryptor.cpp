@@ -11,9 +11,14 @@ void Sh3Encryptor::init(u64 partyIdx, CommPkg& comm, block seed) {
     mShareGen.init(comm, seed);
 }
 
-Sh3Task Sh3Encryptor::shareImpl(Sh3Task dep, const i64Matrix* m, SharedMat& dest, int kind) {
+Sh3Task Sh3Encryptor::shareImpl(Sh3Task dep, const i64Matrix* m, SharedMat& dest, int kind, u64 rowOffset,
+                                 u64 totalRows) {
+    if (totalRows && rowOffset + dest.rows() > totalRows)
+        throw std::invalid_argument("sharing rows [" + std::to_string(rowOffset) + ", " +
+                                    std::to_string(rowOffset + dest.rows()) + ") of a " + std::to_string(totalRows) +
+                                    "-row matrix " LOCATION);
     return dep
-        .then([this, m, &dest, kind](CommPkg& comm, Sh3Task& self) {
+        .then([this, m, &dest, kind, rowOffset, totalRows](CommPkg& comm, Sh3Task& self) {
             Gpu& g = self.getRuntime().gpu();
             if (m && (m->rows() != dest.rows() || m->cols() != dest.cols()))
                 throw std::runtime_error("localMatrix: shape mismatch " LOCATION);
@@ -24,7 +29,9 @@ Sh3Task Sh3Encryptor::shareImpl(Sh3Task dep, const i64Matrix* m, SharedMat& dest
                 addend->reset(g, bytes);
                 toDevice(addend->data(), m->data(), bytes, g);
             }
-            aby3g_zero_share zs = mShareGen.zeroShare(mShareGen.takeDraws(n));
+            // a row slice: the whole matrix's draws are taken, the slice's used
+            const u64 all = totalRows ? totalRows * dest.cols() : n;
+            aby3g_zero_share zs = mShareGen.zeroShare(mShareGen.takeDraws(all) + rowOffset * dest.cols());
             GPU_CALL(aby3g_share_draws(kind, zs.k_prev, zs.k_next, zs.draw_base, n,
                                        m ? addend->as<i64>() : nullptr, dest.share(0), nullptr, g.stream()));
             comm.mNext.asyncSendDevice(dest.share(0), bytes, g);
@@ -39,6 +46,13 @@ Sh3Task Sh3Encryptor::localIntMatrix(Sh3Task dep, const i64Matrix& m, si64Matrix
 }
 Sh3Task Sh3Encryptor::remoteIntMatrix(Sh3Task dep, si64Matrix& dest) {
     return shareImpl(dep, nullptr, dest, ABY3G_DRAW_ARITH);
+}
+Sh3Task Sh3Encryptor::localIntMatrixRows(Sh3Task dep, const i64Matrix& m, si64Matrix& dest, u64 rowOffset,
+                                         u64 totalRows) {
+    return shareImpl(dep, &m, dest, ABY3G_DRAW_ARITH, rowOffset, totalRows);
+}
+Sh3Task Sh3Encryptor::remoteIntMatrixRows(Sh3Task dep, si64Matrix& dest, u64 rowOffset, u64 totalRows) {
+    return shareImpl(dep, nullptr, dest, ABY3G_DRAW_ARITH, rowOffset, totalRows);
 }
 Sh3Task Sh3Encryptor::localBinMatrix(Sh3Task dep, const i64Matrix& m, sbMatrix& dest) {
     return shareImpl(dep, &m, dest, ABY3G_DRAW_BIN);

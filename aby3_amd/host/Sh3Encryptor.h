@@ -15,6 +15,14 @@ public:
     // receive x_{i-1} from prev (Sh3Encryptor.cpp:229-279).
     Sh3Task localIntMatrix(Sh3Task dep, const i64Matrix& m, si64Matrix& dest);
     Sh3Task remoteIntMatrix(Sh3Task dep, si64Matrix& dest);
+    // Rows [rowOffset, rowOffset + dest.rows()) of the sharing of a
+    // totalRows-row matrix (m holds those rows): the draws of the whole
+    // matrix are taken from the share stream and the slice's rows used, so
+    // the slice's shares are those rows of the unsplit sharing and the
+    // stream ends where the unsplit sharing leaves it (a party whose rows are
+    // split over GPUs; DESIGN.md §6 "Row split")
+    Sh3Task localIntMatrixRows(Sh3Task dep, const i64Matrix& m, si64Matrix& dest, u64 rowOffset, u64 totalRows);
+    Sh3Task remoteIntMatrixRows(Sh3Task dep, si64Matrix& dest, u64 rowOffset, u64 totalRows);
     // binary: x_i = getBinaryShare() ^ m (Sh3Encryptor.cpp:282-340)
     Sh3Task localBinMatrix(Sh3Task dep, const i64Matrix& m, sbMatrix& dest);
     Sh3Task remoteBinMatrix(Sh3Task dep, sbMatrix& dest);
@@ -36,7 +44,9 @@ public:
     Sh3ShareGen mShareGen;
 
 private:
-    Sh3Task shareImpl(Sh3Task dep, const i64Matrix* m, SharedMat& dest, int kind);
+    // totalRows 0: dest is the whole matrix
+    Sh3Task shareImpl(Sh3Task dep, const i64Matrix* m, SharedMat& dest, int kind, u64 rowOffset = 0,
+                      u64 totalRows = 0);
     Sh3Task revealImpl(Sh3Task dep, const SharedMat& x, i64Matrix& dest, bool binary);
     Sh3Task revealSend(Sh3Task dep, u64 partyIdx, const SharedMat& x);
 };

@@ -110,12 +110,29 @@ Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, const si64Matrix& A, const si64Matri
 
 Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, const si64Matrix& A, const si64Matrix& B, si64Matrix& C, u64 shift,
                                MulMode mode) {
+    return mulTrunc(dep, A, B, C, shift, mode, 0, 0);
+}
+
+Sh3Task Sh3Evaluator::asyncMulRows(Sh3Task dep, const si64Matrix& A, const si64Matrix& B, si64Matrix& C, u64 shift,
+                                   u64 rowOffset, u64 totalRows) {
+    if (!totalRows || rowOffset + A.rows() > totalRows)
+        throw std::invalid_argument("asyncMulRows: rows [" + std::to_string(rowOffset) + ", " +
+                                    std::to_string(rowOffset + A.rows()) + ") of a " + std::to_string(totalRows) +
+                                    "-row product " LOCATION);
+    return mulTrunc(dep, A, B, C, shift, MulMode::Gemm, rowOffset, totalRows);
+}
+
+Sh3Task Sh3Evaluator::mulTrunc(Sh3Task dep, const si64Matrix& A, const si64Matrix& B, si64Matrix& C, u64 shift,
+                               MulMode mode, u64 rowOffset, u64 totalRows) {
     return dep
-        .then([this, &A, &B, &Cref = C, shift, mode](CommPkg& comm, Sh3Task& self) {
+        .then([this, &A, &B, &Cref = C, shift, mode, rowOffset, totalRows](CommPkg& comm, Sh3Task& self) {
             Gpu& g = self.getRuntime().gpu();
             u64 M, K, N;
             shape(mode, A, B, M, K, N);
             const u64 n = M * N, bytes = n * sizeof(i64);
+            // a row slice takes the whole product's truncation words and uses
+            // its rows' (the words are row-major: row r starts at word r * N)
+            const u64 allWords = totalRows ? totalRows * N : n, skip = rowOffset * N;
             std::shared_ptr<si64Matrix> tmp;
             if (aliases(Cref, A) || aliases(Cref, B)) tmp = std::make_shared<si64Matrix>();
             si64Matrix& C = tmp ? *tmp : Cref;
@@ -139,8 +156,8 @@ Sh3Task Sh3Evaluator::asyncMul(Sh3Task dep, const si64Matrix& A, const si64Matri
                 aby3g_trunc_streams ts;
                 std::memcpy(ts.next_seed, mShareGen.mNextSeed.data(), 16);
                 std::memcpy(ts.prev_seed, mShareGen.mPrevSeed.data(), 16);
-                ts.next_off = mShareGen.takeNext(8 * n);
-                ts.prev_off = mShareGen.takePrev(8 * n);
+                ts.next_off = mShareGen.takeNext(8 * allWords) + 8 * skip;
+                ts.prev_off = mShareGen.takePrev(8 * allWords) + 8 * skip;
                 // The truncation pair's AES-CTR runs in the product's epilogue
                 // pass (k_finish_trunc): the element-wise / small-GEMM epilogue,
                 // or, after a share GEMM, the pass that reads its product (or

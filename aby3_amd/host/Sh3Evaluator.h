@@ -38,6 +38,16 @@ public:
     Sh3Task asyncMul(Sh3Task dep, const si64Matrix& A, const si64Matrix& B, si64Matrix& C, u64 shift,
                      MulMode mode);
 
+    // Rows [rowOffset, rowOffset + A.rows()) of the truncated matrix product
+    // of a totalRows-row A (A holds those rows, B all of B): the randomness
+    // of the whole product is taken and the slice's rows used, so C holds
+    // those rows of the unsplit product's shares and the party's streams end
+    // where the unsplit product leaves them. One party's rows split over
+    // GPUs: each GPU runs its slice with the matching slice
+    // of the other parties, no exchange between one party's GPUs.
+    Sh3Task asyncMulRows(Sh3Task dep, const si64Matrix& A, const si64Matrix& B, si64Matrix& C, u64 shift,
+                         u64 rowOffset, u64 totalRows);
+
     template <Decimal D>
     Sh3Task asyncMul(Sh3Task dep, const sf64Matrix<D>& A, const sf64Matrix<D>& B, sf64Matrix<D>& C) {
         return asyncMul(dep, A.i64Cast(), B.i64Cast(), C.i64Cast(), (u64)D);
@@ -68,6 +78,9 @@ private:
     DeviceBuffer mWs;  // GEMM workspace (digit planes + split-K slabs), reused
     void* workspace(MulMode mode, u64 M, u64 K, u64 N, size_t& bytes, Gpu& g);
     void shape(MulMode mode, const si64Matrix& A, const si64Matrix& B, u64& M, u64& K, u64& N) const;
+    // asyncMul(.., shift, mode); totalRows != 0: rows from rowOffset of a totalRows-row product
+    Sh3Task mulTrunc(Sh3Task dep, const si64Matrix& A, const si64Matrix& B, si64Matrix& C, u64 shift, MulMode mode,
+                     u64 rowOffset, u64 totalRows);
 };
 
 }  // namespace aby3

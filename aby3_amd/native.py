@@ -250,6 +250,7 @@ _HOST_SIGS = {
     "aby3h_session_info": (c_int, [c_void_p, POINTER(c_double), c_int]),
     "aby3h_session_check": (c_int, [c_void_p]),
     "aby3h_session_digest": (c_int, [c_void_p, c_int, c_void_p]),
+    "aby3h_session_result": (c_int, [c_void_p, c_int, c_int, c_void_p, c_uint64, c_void_p]),
     "aby3h_session_destroy": (None, [c_void_p]),
     "aby3h_circuit": (c_int, [c_char_p, c_uint64, c_uint64, POINTER(c_uint64), c_void_p, c_void_p, c_void_p,
                               c_void_p, c_void_p, c_void_p]),
@@ -350,6 +351,23 @@ class Session:
         if self.host.aby3h_session_digest(self._h, party, ctypes.byref(out)) != 0:
             raise NativeError("aby3h_session_digest: " + self.host.aby3h_last_error().decode())
         return out.value
+
+    def result(self, party: int):
+        """`party`'s two shares of the last step's result, as two int64
+        numpy arrays (row-major)."""
+        import numpy as np
+
+        out = []
+        for share in (0, 1):
+            n = c_uint64()
+            if self.host.aby3h_session_result(self._h, party, share, None, 0, ctypes.byref(n)) != 0:
+                raise NativeError("aby3h_session_result: " + self.host.aby3h_last_error().decode())
+            a = np.empty(n.value, dtype=np.int64)
+            if self.host.aby3h_session_result(self._h, party, share, a.ctypes.data_as(c_void_p), n.value,
+                                              ctypes.byref(n)) != 0:
+                raise NativeError("aby3h_session_result: " + self.host.aby3h_last_error().decode())
+            out.append(a)
+        return out[0], out[1]
 
     def close(self):
         if self._h:

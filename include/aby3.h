@@ -29,7 +29,12 @@ enum {
      * Sh3Evaluator::asyncMul(A, B, C, D) with truncation (Sh3Evaluator.cpp:651-730).
      * inflight 2: step s issues product s (into one of two output matrices)
      * and then waits for product s - 1, so the runtime holds two independent
-     * products; the run's last one completes when the run ends. */
+     * products; the run's last one completes when the run ends.
+     * [, shard, shards] (GEMM only): this session runs rows [shard * M / shards,
+     * (shard + 1) * M / shards) of the product -- A's slice shared by
+     * localIntMatrixRows, the product by Sh3Evaluator::asyncMulRows -- so the
+     * result holds those rows of the unsplit job's shares (one party's rows
+     * split over `shards` GPUs, each GPU with its own three-party session). */
     ABY3H_JOB_MUL_TRUNC = 0,
     /* params: M, K, N, mode. One step = asyncMul without truncation (:92-116). */
     ABY3H_JOB_MUL = 1,
@@ -109,6 +114,10 @@ int aby3h_session_info(aby3h_session* s, double* out, int n);
  * party this session runs): share-level comparisons between layouts, e.g. one
  * party per process against three in one process on the same seeds. */
 int aby3h_session_digest(aby3h_session* s, int party, uint64_t* out);
+/* Party `party`'s share `share` (0 or 1) of the last step's result: copies
+ * min(count, elements) int64 values (row-major) into out and stores the
+ * result's element count in *elements. Between runs only. */
+int aby3h_session_result(aby3h_session* s, int party, int share, int64_t* out, uint64_t count, uint64_t* elements);
 /* reveals the last step's result and checks it against plaintext; 0 = ok */
 int aby3h_session_check(aby3h_session* s);
 void aby3h_session_destroy(aby3h_session* s);

@@ -26,6 +26,8 @@ int main() {
         {ABY3H_JOB_MUL, {32, 32, 32, 0}, 3},           {ABY3H_JOB_MUL, {32, 16, 8, 1}, 3},
         {ABY3H_JOB_MSB, {3000}, 2},                    {ABY3H_JOB_LR, {2048, 16, 64, 16, 11}, 3},
         {ABY3H_JOB_SORT, {4096}, 1},                  {ABY3H_JOB_MUL_TRUNC, {64, 48, 80, 16, 1}, 2},
+        // row splits (rows [32, 64) of 64; rows [42, 63) of 63)
+        {ABY3H_JOB_MUL_TRUNC, {64, 48, 80, 16, 1, 1, 1, 2}, 2}, {ABY3H_JOB_MUL_TRUNC, {63, 48, 80, 16, 1, 1, 2, 3}, 2},
     };
     // rounds 0 / 1: the three parties on one device, without and with probes;
     // round 2: each on its own device (the north-star layout inside one
@@ -46,6 +48,18 @@ int main() {
                 return 1;
             }
             if (aby3h_session_check(s) == 2) return fail("check");
+            if (j.job == ABY3H_JOB_MUL_TRUNC) {  // the result's shares: the slice's rows x N
+                const uint64_t S = j.p.size() > 7 ? j.p[7] : 1, k = j.p.size() > 7 ? j.p[6] : 0;
+                const uint64_t want = (j.p[0] * (k + 1) / S - j.p[0] * k / S) * j.p[2];
+                std::vector<int64_t> r(want + 1);
+                uint64_t n = 0;
+                if (aby3h_session_result(s, 1, 1, r.data(), r.size(), &n)) return fail("result");
+                if (n != want) {
+                    std::printf("FAIL job params %zu: result of %lu elements, expected %lu\n", j.p.size(),
+                                (unsigned long)n, (unsigned long)want);
+                    return 1;
+                }
+            }
             double ms;
             uint64_t n;
             aby3h_session_probe(s, 0, &ms, &n);

@@ -90,6 +90,30 @@ __global__ void __launch_bounds__(kBlock, 4) k_share_draws(const u32* __restrict
     }
 }
 
+// Rows of draws (one party's row slice of the binary engine's masks):
+// out0[r * rowLen + i] = draw (base + r * rowStride + i), r < nRows, i < rowLen;
+// base, rowLen and rowStride even, so every row is whole counters. A thread
+// encrypts one counter under both keys, as k_share_draws.
+__global__ void __launch_bounds__(kBlock, 4) k_share_draws_rows(const u32* __restrict__ T0g, AesKeyPair kk, int kind,
+                                                                u64 base, u64 rowLen, u64 rowStride, u64 nRows,
+                                                                i64* __restrict__ out0) {
+    __shared__ u32 lds[kAesLdsWords];  // static: lookups fold the table base into ds_read's offset
+    aes_fill_lds(lds, T0g);
+    const u32 lane32 = threadIdx.x & 31;
+    const AesKeyV kn = key_to_vgprs(kk.k[1]);
+    const u64 cpr = rowLen >> 1, total = cpr * nRows;
+    for (u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (u64)gridDim.x * blockDim.x) {
+        const u64 r = t / cpr, q = t - r * cpr;
+        const u64 c = ((base + r * rowStride) >> 1) + q;
+        u64 p[2], v[2];
+        aes_ctr_block(lds, lane32, kk.k[0], c, p[0], p[1]);
+        aes_ctr_block_v(lds, lane32, kn, c, v[0], v[1]);
+        i64* o = out0 + r * rowLen + 2 * q;
+        o[0] = (i64)(kind == ABY3G_DRAW_ARITH ? p[0] - v[0] : p[0] ^ v[0]);
+        o[1] = (i64)(kind == ABY3G_DRAW_ARITH ? p[1] - v[1] : p[1] ^ v[1]);
+    }
+}
+
 // --- 3-party OT multiplication, party 0 (Sh3Evaluator.cpp:132-163, SharedOT.cpp:6-94)
 __global__ void __launch_bounds__(kBlock, 4) k_bitmul_p0(const u32* __restrict__ T0g, const i64* __restrict__ A0,
                                                       const i64* __restrict__ A1, const i64* __restrict__ B0,
@@ -282,6 +306,22 @@ int aby3g_share_draws(int kind, const uint8_t k_prev[16], const uint8_t k_next[1
                       const int64_t* addend, int64_t* out0, int64_t* out1, aby3g_stream stream) {
     return guarded(
         [&] { share_draws_launch(kind, k_prev, k_next, draw_base, n, addend, out0, out1, S(stream), PROBE_AES); });
+}
+
+int aby3g_share_draws_rows(int kind, const uint8_t k_prev[16], const uint8_t k_next[16], uint64_t draw_base,
+                           uint64_t row_len, uint64_t row_stride, uint64_t nrows, int64_t* out0, aby3g_stream stream) {
+    return guarded([&] {
+        ABY3G_REQUIRE(kind == ABY3G_DRAW_ARITH || kind == ABY3G_DRAW_BIN, "row draws: ARITH or BIN only");
+        ABY3G_REQUIRE(draw_base % 2 == 0 && row_len % 2 == 0 && row_stride % 2 == 0,
+                      "row draws: base, row length and row stride must be even");
+        ABY3G_REQUIRE(nrows <= 1 || row_stride >= row_len, "row draws: rows overlap");
+        if (!row_len || !nrows) return;
+        const AesKeyPair kk{{expand_key(k_prev), expand_key(k_next)}};
+        const u64 counters = row_len / 2 * nrows;
+        const u32 grid = std::min<u32>(aes_grid_wide(counters, kBlock, t_draw_wgs), t_draw_wgs);
+        launch(PROBE_AES, k_share_draws_rows, dim3(grid), dim3(kBlock), 0, S(stream), aes_table(), kk, kind,
+               draw_base, row_len, row_stride, nrows, out0);
+    });
 }
 
 int aby3g_trunc_tuple(const aby3g_trunc_streams* ts, uint64_t n, unsigned d, int64_t* R, int64_t* RT,

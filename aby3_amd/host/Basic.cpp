@@ -27,10 +27,14 @@ void evalCircuit(BetaCircuit* cir, const std::vector<const sbMatrix*>& in, const
 // (0, x1, 0) (BuildingBlocks.cpp:475-502, :709-735), fed straight into the
 // circuit's input wires (setTwoInputSharing: one launch, one message), then
 // the circuit (inputs c0, c1; output 0) evaluated into `res`.
+// (totalRows != 0: rows from rowOffset of a totalRows-row evaluation, setCirRows)
 static void evalTwoInput(BetaCircuit* cir, int pIdx, const std::vector<std::pair<const si64Matrix*, i64>>& x, i64 sign,
-                         sbMatrix& res, Sh3Evaluator& eval, Sh3Runtime& rt) {
+                         sbMatrix& res, Sh3Evaluator& eval, Sh3Runtime& rt, u64 rowOffset = 0, u64 totalRows = 0) {
     Sh3BinaryEvaluator binEng;
-    binEng.setCir(cir, x[0].first->size(), eval.mShareGen);
+    if (totalRows)
+        binEng.setCirRows(cir, x[0].first->size(), eval.mShareGen, rowOffset, totalRows);
+    else
+        binEng.setCir(cir, x[0].first->size(), eval.mShareGen);
     setTwoInputSharing(binEng, pIdx, x, sign, {0}, {0}, 1, rt.mComm, rt.gpu());
     binEng.asyncEvaluate(rt.noDependencies())
         .then([&](Sh3Task&) { binEng.getOutput(0, res); })
@@ -52,6 +56,21 @@ int cipher_gt(int pIdx, const si64Matrix& A, const si64Matrix& B, sbMatrix& res,
               Sh3Runtime& runtime) {
     checkShapes(A, B);
     evalTwoInput(basicLibrary().int_comp_helper(64), pIdx, {{&B, 1}, {&A, -1}}, 1, res, eval, runtime);
+    return 0;
+}
+
+int cipher_gt_rows(int pIdx, const si64Matrix& A, const si64Matrix& B, sbMatrix& res, Sh3Evaluator& eval,
+                   Sh3Runtime& runtime, u64 rowOffset, u64 totalRows) {
+    checkShapes(A, B);
+    if (A.cols() != 1) throw std::invalid_argument("cipher_gt_rows: one value per row " LOCATION);
+    if (!A.rows()) {  // an empty slice: the circuit's keys are still taken, as by the unsplit evaluation
+        eval.mShareGen.getPrevBlock();
+        eval.mShareGen.getNextBlock();
+        res.resize(0, 1);
+        return 0;
+    }
+    evalTwoInput(basicLibrary().int_comp_helper(64), pIdx, {{&B, 1}, {&A, -1}}, 1, res, eval, runtime, rowOffset,
+                 totalRows);
     return 0;
 }
 

@@ -16,6 +16,14 @@ int fetch_msb(int pIdx, const si64Matrix& diffAB, sbMatrix& res, Sh3Evaluator& e
 // [A > B] = MSB(B - A)   (:525-532)
 int cipher_gt(int pIdx, const si64Matrix& A, const si64Matrix& B, sbMatrix& res, Sh3Evaluator& eval,
               Sh3Runtime& runtime);
+// cipher_gt for rows [rowOffset, rowOffset + A.rows()) of a totalRows-row
+// comparison (A, B hold those rows): the circuit's masks are those rows'
+// words (Sh3BinaryEvaluator::setCirRows), so res holds those rows of the
+// unsplit comparison's shares -- one party's rows split over GPUs (SURVEY.md
+// §8e). rowOffset is a multiple of 2048, A.rows() too unless the slice ends
+// at totalRows.
+int cipher_gt_rows(int pIdx, const si64Matrix& A, const si64Matrix& B, sbMatrix& res, Sh3Evaluator& eval,
+                   Sh3Runtime& runtime, u64 rowOffset, u64 totalRows);
 // [A >= B] = !MSB(A - B) (:593-602)
 int cipher_ge(int pIdx, const si64Matrix& A, const si64Matrix& B, sbMatrix& res, Sh3Evaluator& eval,
               Sh3Runtime& runtime);

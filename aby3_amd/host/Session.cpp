@@ -230,38 +230,55 @@ double gateBytes(const BetaCircuit& c) {
 // ---- C3: fetch_msb / cipher_gt over `rows` values -------------------------
 struct MsbJob : Job {
     u64 rows;
+    // rows [r0, r1) of the comparison (a row split): slice
+    // boundaries at multiples of 2048 rows (the engine's row padding)
+    u64 r0 = 0, r1 = 0;
     i64Matrix a, b;
     si64Matrix A[3], B[3];
     sbMatrix R[3];
     CircuitLibrary lib;
-    explicit MsbJob(u64 r) : rows(r) {
+    explicit MsbJob(u64 r, u64 shard = 0, u64 shards = 1) : rows(r) {
+        if (shards < 1 || shard >= shards)
+            throw std::invalid_argument("row split: shard " + std::to_string(shard) + " of " + std::to_string(shards));
+        auto edge = [&](u64 k) { return k == shards ? rows : rows * k / shards / 2048 * 2048; };
+        r0 = edge(shard);
+        r1 = edge(shard + 1);
         a = randomMat(rows, 1, 3, 0);
         b = randomMat(rows, 1, 4, 0);
     }
+    bool split() const { return r1 - r0 != rows; }
     void setup(PartyCtx& p) override {
-        A[p.idx].resize(rows, 1);
-        B[p.idx].resize(rows, 1);
+        A[p.idx].resize(r1 - r0, 1);
+        B[p.idx].resize(r1 - r0, 1);
         if (p.idx == 0) {
-            p.enc.localIntMatrix(p.rt, a, A[0]).get();
-            p.enc.localIntMatrix(p.rt, b, B[0]).get();
+            i64Matrix as(r1 - r0, 1), bs(r1 - r0, 1);
+            for (u64 i = r0; i < r1; ++i) as(i - r0, 0) = a(i, 0), bs(i - r0, 0) = b(i, 0);
+            p.enc.localIntMatrixRows(p.rt, as, A[0], r0, rows).get();
+            p.enc.localIntMatrixRows(p.rt, bs, B[0], r0, rows).get();
         } else {
-            p.enc.remoteIntMatrix(p.rt, A[p.idx]).get();
-            p.enc.remoteIntMatrix(p.rt, B[p.idx]).get();
+            p.enc.remoteIntMatrixRows(p.rt, A[p.idx], r0, rows).get();
+            p.enc.remoteIntMatrixRows(p.rt, B[p.idx], r0, rows).get();
         }
     }
-    void step(PartyCtx& p) override { cipher_gt(p.idx, A[p.idx], B[p.idx], R[p.idx], p.eval, p.rt); }
+    void step(PartyCtx& p) override {
+        if (split())
+            cipher_gt_rows(p.idx, A[p.idx], B[p.idx], R[p.idx], p.eval, p.rt, r0, rows);
+        else
+            cipher_gt(p.idx, A[p.idx], B[p.idx], R[p.idx], p.eval, p.rt);
+    }
     const SharedMat* result(int i) const override { return &R[i]; }
     bool check(PartyCtx& p) override {
         i64Matrix r;
         p.enc.revealAll(p.rt, R[p.idx], r).get();
         if (p.idx != 0) return true;
-        for (u64 i = 0; i < rows; ++i)
-            if ((r(i, 0) & 1) != (i64)(((u64)b(i, 0) - (u64)a(i, 0)) >> 63)) return false;
+        for (u64 i = r0; i < r1; ++i)
+            if ((r(i - r0, 0) & 1) != (i64)(((u64)b(i, 0) - (u64)a(i, 0)) >> 63)) return false;
         return true;
     }
     void info(double* o) override {
         BetaCircuit* c = lib.int_comp_helper(64);
-        const double words = std::ceil(rows / 64.0), padded = 32.0 * ((rows + 2047) / 2048);
+        const u64 n = r1 - r0;
+        const double words = std::ceil(n / 64.0), padded = 32.0 * ((n + 2047) / 2048);
         o[ABY3H_INFO_MULTS_PER_STEP] = c->mAndCount * words;
         o[ABY3H_INFO_AND_WORDS] = c->mAndCount * words;
         o[ABY3H_INFO_GATE_WORDS] = c->mGates.size() * words;
@@ -806,7 +823,7 @@ std::unique_ptr<Job> makeJob(int job, const uint64_t* params, int nparams) {
         case ABY3H_JOB_MUL:
             return std::make_unique<MulJob>(P(0, 128), P(1, 128), P(2, 128), 0, P(3, 0) ? MulMode::Gemm : MulMode::Hadamard,
                                             false);
-        case ABY3H_JOB_MSB: return std::make_unique<MsbJob>(P(0, 1 << 20));
+        case ABY3H_JOB_MSB: return std::make_unique<MsbJob>(P(0, 1 << 20), P(1, 0), P(2, 1));
         case ABY3H_JOB_LR:
             return std::make_unique<LrJob>(P(0, 1000000), P(1, 128), P(2, 256), P(3, 16), P(4, 11), P(5, 0));
         case ABY3H_JOB_SORT: return std::make_unique<SortJob>(P(0, 1 << 20), P(1, 0));

@@ -11,7 +11,22 @@ constexpr bool kFuseInputsDefault = true;
 void Sh3BinaryEvaluator::setCir(BetaCircuit* cir, u64 width, Sh3ShareGen& gen) {
     block p = gen.getPrevBlock();
     block n = gen.getNextBlock();
-    setCir(cir, width, p, n);
+    setCirImpl(cir, width, p, n, 0, 0);
+}
+
+void Sh3BinaryEvaluator::setCir(BetaCircuit* cir, u64 width, block prevSeed, block nextSeed) {
+    setCirImpl(cir, width, prevSeed, nextSeed, 0, 0);
+}
+
+void Sh3BinaryEvaluator::setCirRows(BetaCircuit* cir, u64 width, Sh3ShareGen& gen, u64 rowOffset, u64 totalRows) {
+    if (rowOffset % 2048 || rowOffset + width > totalRows || (width % 2048 && rowOffset + width != totalRows))
+        throw std::invalid_argument("setCirRows: rows [" + std::to_string(rowOffset) + ", " +
+                                    std::to_string(rowOffset + width) + ") of " + std::to_string(totalRows) +
+                                    ": the slice must start at a multiple of 2048 rows and end at one or at the "
+                                    "last row " LOCATION);
+    block p = gen.getPrevBlock();
+    block n = gen.getNextBlock();
+    setCirImpl(cir, width, p, n, rowOffset / 64, 32 * ((totalRows + 2047) / 2048));
 }
 
 void Sh3BinaryEvaluator::upload(Gpu& g) {
@@ -113,7 +128,8 @@ void Sh3BinaryEvaluator::upload(Gpu& g) {
     }));
 }
 
-void Sh3BinaryEvaluator::setCir(BetaCircuit* cir, u64 width, block prevSeed, block nextSeed) {
+void Sh3BinaryEvaluator::setCirImpl(BetaCircuit* cir, u64 width, block prevSeed, block nextSeed, u64 wordOffset,
+                                    u64 rowStride) {
     if (!cir->levelized()) cir->levelByAndDepth();
     mCir = cir;
     mRows = width;
@@ -138,6 +154,9 @@ void Sh3BinaryEvaluator::setCir(BetaCircuit* cir, u64 width, block prevSeed, blo
     mAndDone = 0;
     mZByLevel = false;
     mZDrawn = 0;
+    // (a whole evaluation is the slice of itself: the contiguous draws)
+    mZWordOffset = rowStride == mWords ? 0 : wordOffset;
+    mZRowStride = rowStride == mWords ? 0 : rowStride;
     const u64 zWords = (u64)cir->mAndCount * mWords;
     if (zWords) {
         mZStream = g.drawStream() ? g.drawStream() : g.aux();
@@ -177,8 +196,7 @@ void Sh3BinaryEvaluator::setCir(BetaCircuit* cir, u64 width, block prevSeed, blo
         if (mZByLevel)
             drawZThrough(0);  // the first AND level's masks; the rest behind each level's launch
         else
-            GPU_CALL(aby3g_share_draws(ABY3G_DRAW_BIN, mKeyPrev.data(), mKeyNext.data(), 0, zWords, nullptr,
-                                       (i64*)mZPtr, nullptr, mZStream));
+            drawZRows(0, cir->mAndCount);
         if (other) {
             if (!mZEv) mZEv = std::make_unique<Event>();
             mZEv->record(mZStream);
@@ -211,10 +229,20 @@ void Sh3BinaryEvaluator::drawZThrough(u64 level) {
     for (; L < c.size() && (L < level || !c[L]); ++L) end += c[L];
     if (L < c.size()) end += c[L];
     if (end <= mZDrawn) return;
-    GPU_CALL(aby3g_share_draws(ABY3G_DRAW_BIN, mKeyPrev.data(), mKeyNext.data(), mZDrawn * mWords,
-                               (end - mZDrawn) * mWords, nullptr, (i64*)(mZPtr + mZDrawn * mWords), nullptr,
-                               mZStream));
+    drawZRows(mZDrawn, end);
     mZDrawn = end;
+}
+
+void Sh3BinaryEvaluator::drawZRows(u64 first, u64 end) {
+    if (end <= first) return;
+    if (mZRowStride)  // a row slice: words [offset, offset + mWords) of each AND row
+        GPU_CALL(aby3g_share_draws_rows(ABY3G_DRAW_BIN, mKeyPrev.data(), mKeyNext.data(),
+                                        first * mZRowStride + mZWordOffset, mWords, mZRowStride, end - first,
+                                        (i64*)(mZPtr + first * mWords), mZStream));
+    else
+        GPU_CALL(aby3g_share_draws(ABY3G_DRAW_BIN, mKeyPrev.data(), mKeyNext.data(), first * mWords,
+                                   (end - first) * mWords, nullptr, (i64*)(mZPtr + first * mWords), nullptr,
+                                   mZStream));
 }
 
 void Sh3BinaryEvaluator::waitZ() {

@@ -35,6 +35,13 @@ public:
     // (Sh3BinaryEvaluator.h:96-102)
     void setCir(BetaCircuit* cir, u64 width, Sh3ShareGen& gen);
     void setCir(BetaCircuit* cir, u64 width, block prevSeed, block nextSeed);
+    // setCir for rows [rowOffset, rowOffset + width) of a totalRows-row
+    // evaluation (one party's rows split over GPUs): the AND
+    // masks are the slice's words of every gate's row of draws, so the
+    // slice's shares are those rows of the unsplit evaluation's. rowOffset is
+    // a multiple of 2048 (the engine's row padding), and so is width unless
+    // the slice ends at totalRows.
+    void setCirRows(BetaCircuit* cir, u64 width, Sh3ShareGen& gen, u64 rowOffset, u64 totalRows);
     void setInput(u64 i, const sbMatrix& in);
     // setInput from mapped rows of `in` (circuit row p <- row map(p)): the
     // compare-exchange gather of a merge round fused into the transpose
@@ -151,6 +158,11 @@ private:
     // (levelDraws()).
     bool mZByLevel = false;
     u64 mZDrawn = 0;  // AND rows (ordinals) whose masks are enqueued
+    // a row slice (setCirRows): the slice's first word and the unsplit
+    // evaluation's words per AND row (0: not a slice)
+    u64 mZWordOffset = 0, mZRowStride = 0;
+    void setCirImpl(BetaCircuit* cir, u64 width, block prevSeed, block nextSeed, u64 wordOffset, u64 rowStride);
+    void drawZRows(u64 first, u64 end);  // the masks of AND rows [first, end)
     static int levelDraws();
     void drawZThrough(u64 level);
     std::unique_ptr<Event> mZEv, mZFresh; // draws done / main stream's position for fresh memory

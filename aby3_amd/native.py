@@ -124,6 +124,8 @@ _SIGS = {
     "aby3g_aes_ctr": (c_int, [c_u8p, c_uint64, c_uint64, c_void_p, c_void_p]),
     "aby3g_prng_fill": (c_int, [c_u8p, c_uint64, c_uint64, c_void_p, c_void_p]),
     "aby3g_share_draws": (c_int, [c_int, c_u8p, c_u8p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "aby3g_share_draws_rows": (c_int, [c_int, c_u8p, c_u8p, c_uint64, c_uint64, c_uint64, c_uint64, c_void_p,
+                                       c_void_p]),
     "aby3g_mul_workspace_bytes": (c_size_t, [c_int, c_uint64, c_uint64, c_uint64]),
     "aby3g_mul_local": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64, c_uint64,
                                 POINTER(ZeroShare), c_void_p, c_size_t, c_void_p]),

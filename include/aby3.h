@@ -38,8 +38,11 @@ enum {
     ABY3H_JOB_MUL_TRUNC = 0,
     /* params: M, K, N, mode. One step = asyncMul without truncation (:92-116). */
     ABY3H_JOB_MUL = 1,
-    /* params: rows. One step = cipher_gt / fetch_msb over `rows` 64-bit
-     * values: reshare + MSB(a+b) circuit (BuildingBlocks.cpp:464-532). */
+    /* params: rows[, shard, shards]. One step = cipher_gt / fetch_msb over
+     * `rows` 64-bit values: reshare + MSB(a+b) circuit (BuildingBlocks.cpp:
+     * 464-532). shard k of `shards`: rows [e(k), e(k+1)) with e(k) = rows * k /
+     * shards rounded down to a multiple of 2048 (e(shards) = rows), by
+     * cipher_gt_rows: those rows of the unsplit job's shares. */
     ABY3H_JOB_MSB = 2,
     /* params: rows (dataset), dim, batch, D, lr_log2[, sample]. One step = one
      * SGD_Logistic iteration (aby3-ML/Regression.h:249-293): xw = X_B w,

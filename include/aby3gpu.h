@@ -212,6 +212,14 @@ int aby3g_set_draw_workgroups(int cap);
 enum { ABY3G_DRAW_ARITH = 0, ABY3G_DRAW_BIN = 1, ABY3G_DRAW_RANDPAIR = 2 };
 int aby3g_share_draws(int kind, const uint8_t k_prev[16], const uint8_t k_next[16], uint64_t draw_base, uint64_t n,
                       const int64_t* addend, int64_t* out0, int64_t* out1, aby3g_stream stream);
+/* Rows of draws (kind ARITH or BIN): out0[r * row_len + i] = draw
+ * (draw_base + r * row_stride + i) for r < nrows, i < row_len; draw_base,
+ * row_len and row_stride even. A row slice of the binary engine's masks: z[k]
+ * of words [w0, w0 + row_len) of a circuit over row_stride words is
+ * draw_base = w0, row stride row_stride (Sh3BinaryEvaluator::setCirRows).
+ * (No reference counterpart: the reference never splits a party's rows.) */
+int aby3g_share_draws_rows(int kind, const uint8_t k_prev[16], const uint8_t k_next[16], uint64_t draw_base,
+                           uint64_t row_len, uint64_t row_stride, uint64_t nrows, int64_t* out0, aby3g_stream stream);
 
 /* -------------------------------------------------- arithmetic evaluator -- */
 /* Local share product of Sh3Evaluator::asyncMul:

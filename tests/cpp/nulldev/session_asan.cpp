@@ -28,6 +28,8 @@ int main() {
         {ABY3H_JOB_SORT, {4096}, 1},                  {ABY3H_JOB_MUL_TRUNC, {64, 48, 80, 16, 1}, 2},
         // row splits (rows [32, 64) of 64; rows [42, 63) of 63)
         {ABY3H_JOB_MUL_TRUNC, {64, 48, 80, 16, 1, 1, 1, 2}, 2}, {ABY3H_JOB_MUL_TRUNC, {63, 48, 80, 16, 1, 1, 2, 3}, 2},
+        {ABY3H_JOB_MSB, {5000, 1, 2}, 2},  // rows [2048, 5000) of 5000
+        {ABY3H_JOB_MSB, {1000, 0, 2}, 2},  // an empty slice
     };
     // rounds 0 / 1: the three parties on one device, without and with probes;
     // round 2: each on its own device (the north-star layout inside one

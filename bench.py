@@ -68,9 +68,12 @@ def parse():
     ap.add_argument("--gemm-turns", action="store_true",
                     help="co-located parties' share GEMMs take turns in every pass (aby3g_mfma_turn), so that a "
                          "profiler's launch spans are the kernel's own (scripts/gpu_profile.sh)")
-    ap.add_argument("--deployment", choices=("replicas", "parties"), default="replicas",
+    ap.add_argument("--deployment", choices=("replicas", "parties", "rowsplit"), default="replicas",
                     help="replicas: every rank runs a whole 3-party job on its GPU; parties: every 3 ranks form "
-                         "one job, one party per rank and GPU (the north_star layout; world size a multiple of 3)")
+                         "one job, one party per rank and GPU (the north_star layout; world size a multiple of 3); "
+                         "rowsplit: the ranks split one product's rows, rank r running rows [r*M/N, (r+1)*M/N) as "
+                         "a 3-party job on its GPU, every party's rows split over the N GPUs (SURVEY.md §8e; "
+                         "strong scaling)")
     return ap.parse_args()
 
 
@@ -581,6 +584,52 @@ def main_parties(args, world, rank, local, pg, nt):
         pg.destroy_process_group()
 
 
+def main_rowsplit(args, world, rank, local, pg, nt):
+    """--deployment rowsplit: rank r runs rows [r*M/N, (r+1)*M/N) of ONE C2
+    product as a three-party job on its GPU (ABY3H_JOB_MUL_TRUNC's shard
+    parameters: every slice's shares are those rows of the unsplit product's,
+    tests/test_gpu_rowsplit.py); no exchange between the ranks' jobs. A step
+    is the whole product: value = M*N*K / the slowest rank's time."""
+    import ctypes
+
+    n = ctypes.c_int(0)
+    nt.lib().device_count(ctypes.byref(n))
+    dev = local % max(n.value, 1)
+    M, K, N, D = args.m, args.k, args.n, args.decimal
+    s = nt.Session(nt.JOB_MUL_TRUNC, [M, K, N, D, 1, 1, rank, world], devices=(dev, dev, dev), probe=False)
+    s.run(2)
+    ok = s.check()
+    if allmax(pg, 0.0 if ok else 1.0) > 0:
+        raise SystemExit("bench: revealed product slice does not match the plaintext")
+    dt = timed(s, args.steps, pg, secs=args.prewarm_s, warmup=args.warmup)
+    s.close()
+    out = {
+        "metric": "secret-shared 64-bit mults/sec (matmul + binary-AND) per party, 3 parties on 3 MI355X",
+        "value": args.steps * M * N * K / dt,
+        "unit": "mults/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic: fixed-point operands round(U[-8,8) * 2^16), shared by party 0",
+        "config": {
+            "workload": f"sf64Matrix asyncMul + truncation {M}x{K} . {K}x{N} (D{D}), upstream GEMM semantics, "
+                        f"the product's rows split over {world} GPU(s), each slice 3 parties co-located",
+            "parties_per_gpu": 3,
+            "global_batch": 1,
+            "parallelism": f"rowsplit{world}",
+        },
+    }
+    if rank == 0:
+        print(json.dumps(out))
+    if pg is not None:
+        pg.destroy_process_group()
+
+
 def main():
     args = parse()
     world, rank, local, pg = dist_setup()
@@ -588,6 +637,8 @@ def main():
 
     if args.deployment == "parties":
         return main_parties(args, world, rank, local, pg, nt)
+    if args.deployment == "rowsplit":
+        return main_rowsplit(args, world, rank, local, pg, nt)
 
     import ctypes
 

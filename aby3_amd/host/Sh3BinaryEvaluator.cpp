@@ -194,7 +194,7 @@ void Sh3BinaryEvaluator::setCirImpl(BetaCircuit* cir, u64 width, block prevSeed,
         }
         mZByLevel = !other && levelDraws() != 0;
         if (mZByLevel)
-            drawZThrough(0);  // the first AND level's masks; the rest behind each level's launch
+            drawZThrough(0);  // the first AND level's masks; the rest in roundCallback (levelDraws)
         else
             drawZRows(0, cir->mAndCount);
         if (other) {
@@ -583,7 +583,7 @@ void Sh3BinaryEvaluator::roundCallback(CommPkg& comm, Sh3Task task) {
     mAndDone += nAnd;
     // this level's bytes (about 72 per gate and 64-row word)
     if (nAnd) hp = comm.mNext.handoffPost(g, mRows, (u64)mCir->mLevelCounts[mLevel] * mWords * 72, send->data());
-    if (nAnd && mZByLevel) drawZThrough(mLevel);  // (drawn behind the previous level's launch)
+    if (nAnd && mZByLevel) drawZThrough(mLevel);  // (normally drawn already, behind an earlier launch)
     if (nb && mZPending) waitZ();
     // the first level with its inputs (aby3g_bin_level_in) when the held
     // sources make up every input wire (an input set another way lives in

@@ -847,7 +847,9 @@ const char* aby3h_last_error(void) { return t_err.c_str(); }
 
 aby3h_session* aby3h_session_create(int job, const uint64_t* params, int nparams, const int* devices, int probe) {
     try {
-        auto* h = new aby3h_session;
+        // destroyed (threads joined) on any failure below
+        std::unique_ptr<aby3h_session, void (*)(aby3h_session*)> guard(new aby3h_session, aby3h_session_destroy);
+        aby3h_session* h = guard.get();
         Session& s = h->s;
         s.job = makeJob(job, params, nparams);
         s.locals = {0, 1, 2};
@@ -876,12 +878,8 @@ aby3h_session* aby3h_session_create(int job, const uint64_t* params, int nparams
             std::unique_lock<std::mutex> lk(s.mu);
             s.done.wait(lk, [&] { return s.finished == 3; });
         }
-        if (!s.err.empty()) {
-            std::string e = s.err;
-            aby3h_session_destroy(h);
-            throw std::runtime_error(e);
-        }
-        return h;
+        if (!s.err.empty()) throw std::runtime_error(s.err);
+        return guard.release();
     } catch (const std::exception& e) {
         t_err = e.what();
         return nullptr;
@@ -893,7 +891,9 @@ aby3h_session* aby3h_party_create(int job, const uint64_t* params, int nparams, 
     try {
         if (party < 0 || party > 2) throw std::runtime_error("party must be 0, 1 or 2");
         if (!link) throw std::runtime_error("null link name");
-        auto* h = new aby3h_session;
+        // destroyed (thread joined, links closed) on any failure below
+        std::unique_ptr<aby3h_session, void (*)(aby3h_session*)> guard(new aby3h_session, aby3h_session_destroy);
+        aby3h_session* h = guard.get();
         Session& s = h->s;
         s.job = makeJob(job, params, nparams);
         s.locals = {party};
@@ -912,12 +912,8 @@ aby3h_session* aby3h_party_create(int job, const uint64_t* params, int nparams, 
             std::unique_lock<std::mutex> lk(s.mu);
             s.done.wait(lk, [&] { return s.finished == 1; });
         }
-        if (!s.err.empty()) {
-            std::string e = s.err;
-            aby3h_session_destroy(h);
-            throw std::runtime_error(e);
-        }
-        return h;
+        if (!s.err.empty()) throw std::runtime_error(s.err);
+        return guard.release();
     } catch (const std::exception& e) {
         t_err = e.what();
         return nullptr;

@@ -5,6 +5,7 @@
 // meaningless here; only the host code's memory behaviour is under test.
 #include <aby3.h>
 #include <cstdio>
+#include <cstring>
 #include <vector>
 
 extern "C" void nulldev_stats(unsigned* peer_bits, unsigned long* kind3_copies);
@@ -80,6 +81,18 @@ int main() {
     }
     std::printf("cross-device: peer pairs 0x%x, %lu copies between devices\n", peers, kind3);
     std::vector<int64_t> a(64 * 48, 3), b(48 * 80, 5), sh(6 * 64 * 80), pl(64 * 80);
+    // row splits the jobs refuse: a shard past the last, a split Hadamard product
+    for (const auto& bad : {std::vector<uint64_t>{64, 64, 64, 16, 1, 1, 2, 2}, {64, 64, 64, 16, 0, 1, 0, 2}}) {
+        if (aby3h_session* s = aby3h_session_create(ABY3H_JOB_MUL_TRUNC, bad.data(), (int)bad.size(), dev, 0)) {
+            aby3h_session_destroy(s);
+            std::printf("FAIL a bad row split was accepted\n");
+            return 1;
+        }
+        if (!std::strstr(aby3h_last_error(), "row split")) {
+            std::printf("FAIL bad row split: unexpected error '%s'\n", aby3h_last_error());
+            return 1;
+        }
+    }
     if (aby3h_sim_mul(0, 1, 1, 16, a.data(), b.data(), 64, 48, 80, sh.data(), pl.data())) return fail("sim_mul");
     // empty shapes: no rows, no inner dimension (a zero product, then truncated), no columns
     for (const auto& s3 : {std::vector<uint64_t>{0, 5, 7}, {5, 0, 7}, {5, 7, 0}}) {

@@ -68,6 +68,8 @@ def colocated_digests(job, params, steps):
     (nt.JOB_SORT, [4096], 1),                           # C5 network, every key checked
     (nt.JOB_A2B, [5000], 2),                            # toBinaryMatrix
     (nt.JOB_BITINJ, [777, 13], 2),                      # bitInjection (OT messages)
+    (nt.JOB_MSB, [6244, 1, 2], 2),                      # a row slice: its masks in two strided pieces
+    (nt.JOB_MUL_TRUNC, [257, 200, 250, 8, 1, 1, 1, 3], 2),  # a row slice of the GEMM
 ])
 def test_three_party_processes(gpu, job, params, steps):
     """Every job by three processes: the revealed result checked against

@@ -88,6 +88,30 @@ def test_share_draws(gpu, kind, base, n):
         assert np.array_equal(host(o0).view(np.uint64), exp)
 
 
+@pytest.mark.parametrize("kind", [nt.DRAW_ARITH, nt.DRAW_BIN])
+@pytest.mark.parametrize("base,row_len,stride,nrows", [(0, 32, 64, 5), (64, 96, 512, 181), (1024, 2, 2, 7),
+                                                       (6, 4096, 16384, 3), (0, 0, 64, 4), (8, 64, 64, 0)])
+def test_share_draws_rows(gpu, kind, base, row_len, stride, nrows):
+    """A row slice of the binary engine's masks (aby3g_share_draws_rows):
+    row r of the output is draws [base + r*stride, base + r*stride + row_len)
+    of the oracle's stream."""
+    kp, kn = k16(7), k16(8)
+    out = empty(max(row_len * nrows, 1))
+    gpu.share_draws_rows(kind, nt.key16(kp), nt.key16(kn), base, row_len, stride, nrows, P(out), None)
+    if not row_len or not nrows:
+        return
+    r0, _ = orc.share_draws(kind, kp, kn, base, stride * (nrows - 1) + row_len)
+    exp = np.concatenate([r0[r * stride:r * stride + row_len] for r in range(nrows)])
+    assert np.array_equal(host(out), exp)
+
+
+def test_share_draws_rows_rejects_odd(gpu):
+    out = empty(8)
+    for args in [(1, 2, 2, 1), (0, 3, 4, 1), (0, 2, 3, 2), (0, 4, 2, 2)]:  # odd base / length / stride, overlap
+        with pytest.raises(nt.NativeError):
+            gpu.share_draws_rows(nt.DRAW_BIN, nt.key16(k16(7)), nt.key16(k16(8)), *args, P(out), None)
+
+
 def _zs(kp, kn, base):
     z = nt.ZeroShare()
     z.k_prev[:] = kp
